@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DUCKNet-17 training images/sec at 352x352, bf16, 1..N MI355X (weak scaling).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
+``torch.distributed.run`` with one rank per GPU (RCCL).  Each step is a full reference training
+iteration (``core/seg_trainer.py:24-95`` semantics): zero_grad, forward, CE loss, backward (DDP
+bucketed all-reduce + SyncBN), optimizer step (Adam, MyConfig default), OneCycle scheduler step and
+EMA update.  W untimed warmup steps, then K steps bracketed by barrier + synchronize; the MAX
+elapsed over ranks is reported.  Data: synthetic 352x352 polyp images/masks, random-init weights.
+
+``--impl fused`` (default) runs the MI355X-native engine (HIP kernels + hipGraph); ``--impl eager``
+runs the same step with stock PyTorch-ROCm (MIOpen convs, torch DDP/SyncBN) = the in-house
+"reference speed" of BASELINE.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--batch', type=int, default=16, help='per-GPU micro-batch (images)')
+    p.add_argument('--size', type=int, default=352)
+    p.add_argument('--base-channel', type=int, default=17)
+    p.add_argument('--impl', choices=['fused', 'eager'], default='eager')
+    p.add_argument('--channels-last', action='store_true')
+    p.add_argument('--no-graph', action='store_true')
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus and rank == 0:
+        print(f'[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
+
+    from medical_segmentation_pytorch_amd.runtime.bench_step import build_bench_step
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    device = torch.device('cuda', local_rank)
+
+    impl = args.impl
+    step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
+                            base_channel=args.base_channel, device=device,
+                            channels_last=args.channels_last, use_graph=not args.no_graph,
+                            distributed=world > 1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    ms = elapsed / args.steps * 1e3
+    global_batch = args.batch * world
+    value = global_batch * args.steps / elapsed
+    baseline = None
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')) as f:
+            published = json.load(f).get('published') or {}
+        baseline = published.get('images_per_sec')
+    except Exception:
+        pass
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'images/sec (whole node) + val Dice, DUCKNet-17 352x352 at 1/2/4/8 MI355X',
+            'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': (value / baseline) if baseline else None,
+            'dtype': 'bf16', 'data': 'synthetic 352x352 polyp images/masks, random-init weights',
+            'config': {'model': f'DUCKNet-{args.base_channel}', 'global_batch': global_batch,
+                       'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
+                       'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
+                       'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1},
+        }), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,161 @@
+"""Configuration object with the reference's field names -- ``configs/base_config.py:5-123``.
+
+Every default of the reference ``BaseConfig`` is kept (Appendix A of SURVEY.md).  Additions are the
+MI355X engine knobs at the bottom (``engine``, ``use_graph``, ``bucket_cap_mb`` ...) which old
+configs simply do not set.  ``init_dependent_config`` derives the same fields as the reference
+(``base_config.py:106-123``) and, unlike it, may be re-run after CLI overrides
+(SURVEY Appendix E.4): derived fields are only filled when still unset.
+"""
+from __future__ import annotations
+
+import os
+
+
+class BaseConfig:
+    def __init__(self):
+        # Dataset
+        self.dataset = None
+        self.subset = None
+        self.dataroot = None
+        self.data_root = None          # field read by the polyp dataset (reference polyp.py:14)
+        self.num_class = -1
+        self.ignore_index = 255
+        self.num_channel = None
+        self.use_test_set = False
+
+        # Model
+        self.model = None
+        self.encoder = None
+        self.decoder = None
+        self.encoder_weights = 'imagenet'
+        self.base_channel = None
+
+        # Training
+        self.total_epoch = 200
+        self.base_lr = 0.01
+        self.train_bs = 16             # per GPU
+        self.use_aux = False
+        self.aux_coef = None
+
+        # Validating
+        self.metrics = ['dice']        # the first one drives best-checkpoint selection
+        self.val_bs = 16
+        self.begin_val_epoch = 0
+        self.val_interval = 1
+        self.val_img_stride = 1
+
+        # Testing
+        self.is_testing = False
+        self.test_bs = 16
+        self.test_data_folder = None
+        self.colormap = 'random'
+        self.colormap_path = None
+        self.save_mask = True
+        self.blend_prediction = True
+        self.blend_alpha = 0.3
+
+        # Loss
+        self.loss_type = 'ce'
+        self.class_weights = None
+        self.ohem_thrs = 0.7
+        self.reduction = 'mean'
+
+        # Scheduler
+        self.lr_policy = 'cos_warmup'
+        self.warmup_epochs = 3
+        self.step_size = None          # reference StepLR needs it but never defines it (Appendix E.3)
+
+        # Optimizer
+        self.optimizer_type = 'sgd'
+        self.momentum = 0.9
+        self.weight_decay = 1e-4
+
+        # Monitoring
+        self.save_ckpt = True
+        self.save_dir = 'save'
+        self.use_tb = True
+        self.tb_log_dir = None
+        self.ckpt_name = None
+        self.logger_name = None
+
+        # Training setting
+        self.amp_training = False
+        self.resume_training = True
+        self.load_ckpt = True
+        self.load_ckpt_path = None
+        self.base_workers = 8
+        self.random_seed = 1
+        self.use_ema = False
+
+        # Augmentation
+        self.crop_size = 512
+        self.crop_h = None
+        self.crop_w = None
+        self.scale = 1.0
+        self.randscale = 0.0
+        self.brightness = 0.0
+        self.contrast = 0.0
+        self.saturation = 0.0
+        self.h_flip = 0.0
+        self.v_flip = 0.0
+
+        # DDP
+        self.synBN = True
+        self.destroy_ddp_process = True
+        self.local_rank = int(os.getenv('LOCAL_RANK', -1))
+        self.main_rank = self.local_rank in [-1, 0]
+
+        # Knowledge distillation
+        self.kd_training = False
+        self.teacher_ckpt = ''
+        self.teacher_model = 'smp'
+        self.teacher_encoder = None
+        self.teacher_decoder = None
+        self.kd_loss_type = 'kl_div'
+        self.kd_loss_coefficient = 1.0
+        self.kd_temperature = 4.0
+
+        # ---- MI355X engine knobs (new; absent from the reference) ----
+        self.engine = 'auto'           # 'auto' | 'fused' (HIP kernels) | 'eager' (stock torch ops)
+        self.amp_dtype = 'bf16'        # CDNA4 autocast dtype when amp_training: 'bf16' | 'fp16'
+        self.use_graph = True          # capture the static-shape train step in a hipGraph
+        self.bucket_cap_mb = 64        # gradient bucket size for the RCCL all-reduce
+        self.grad_compress = None      # None | 'bf16' all-reduce compression
+        self.gpu_augment = True        # run augmentation on the GPU over an HBM-resident dataset
+        self.dist_backend = None       # None -> 'nccl' (RCCL) on GPU, 'gloo' on CPU
+        self.log_interval = 50         # device-side loss accumulation, host sync every N iters
+        self.ckpt_extra_state = True   # also save scaler/EMA/RNG (extra keys; old readers ignore)
+        self.synthetic_data = False    # generate a synthetic polyp set when data_root is missing
+        self.synthetic_num = (64, 16, 16)
+        self.synthetic_size = 352
+
+    # ------------------------------------------------------------------
+    def init_dependent_config(self):
+        assert len(self.metrics) > 0
+
+        if self.load_ckpt_path is None and not self.is_testing:
+            self.load_ckpt_path = f'{self.save_dir}/last.pth'
+
+        if self.tb_log_dir is None:
+            self.tb_log_dir = f'{self.save_dir}/tb_logs/'
+
+        if self.crop_h is None:
+            self.crop_h = self.crop_size
+        if self.crop_w is None:
+            self.crop_w = self.crop_size
+
+        if self.data_root is None and self.dataroot is not None:
+            self.data_root = self.dataroot
+        if self.dataroot is None and self.data_root is not None:
+            self.dataroot = self.data_root
+
+        if self.logger_name is None:
+            self.logger_name = 'seg_trainer'
+
+        if self.dataset == 'polyp':
+            self.num_class = 2 if self.num_class == -1 else self.num_class
+            self.num_channel = 3 if self.num_channel is None else self.num_channel
+        return self
+
+    def to_dict(self):
+        return {k: v for k, v in vars(self).items() if not k.startswith('_')}

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 ``*_results.db`` (rocpd SQLite) into a per-kernel time table.
+
+Usage: python tools/rocpd_summary.py path/to/results.db [--top 40] [--steps N] [--group]
+``--group`` buckets kernels into families (conv fwd / dgrad / wgrad / BN / elementwise ...).
+"""
+import argparse
+import collections
+import re
+import sqlite3
+
+FAMILIES = [
+    ('conv(MIOpen/ours)', r'conv|igemm|Conv|naive_conv|implicit|gemm|Cijk|MIOpen|xdlops|batched_transpose|transpose'),
+    ('batchnorm', r'[Bb]atch[Nn]orm|bn_|welford|MIOpenBatchNorm'),
+    ('elementwise', r'elementwise|vectorized|unrolled_elementwise|Elementwise'),
+    ('reduce', r'reduce|Reduce'),
+    ('optimizer/foreach', r'foreach|multi_tensor|adam|Adam'),
+    ('upsample/pool', r'upsample|pool|Pool'),
+    ('loss', r'nll|softmax|log_softmax|cross'),
+    ('copy', r'copy|Copy|fill'),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('db')
+    ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--steps', type=int, default=1)
+    ap.add_argument('--group', action='store_true')
+    a = ap.parse_args()
+    db = sqlite3.connect(a.db)
+    rows = db.execute('select name, start, end from kernels').fetchall()
+    tot = collections.defaultdict(float)
+    cnt = collections.Counter()
+    for name, s, e in rows:
+        tot[name] += (e - s) / 1e6
+        cnt[name] += 1
+    total = sum(tot.values())
+    span = (max(r[2] for r in rows) - min(r[1] for r in rows)) / 1e6 if rows else 0
+    print(f'kernels={len(rows)} busy_ms={total:.2f} span_ms={span:.2f} per_step_busy_ms={total / a.steps:.2f}')
+    if a.group:
+        fam = collections.defaultdict(float)
+        fcnt = collections.Counter()
+        for n, t in tot.items():
+            for fname, pat in FAMILIES:
+                if re.search(pat, n):
+                    break
+            else:
+                fname = 'other'
+            fam[fname] += t
+            fcnt[fname] += cnt[n]
+        for f, t in sorted(fam.items(), key=lambda x: -x[1]):
+            print(f'{t:10.2f} ms {100 * t / total:5.1f}% {fcnt[f]:7d}  {f}')
+        print()
+    for n, t in sorted(tot.items(), key=lambda x: -x[1])[:a.top]:
+        print(f'{t:10.2f} ms {100 * t / total:5.1f}% {cnt[n]:6d}  {n[:150]}')
+
+
+if __name__ == '__main__':
+    main()
