@@ -33,7 +33,9 @@ def parse_args(argv=None):
     p.add_argument('--batch', type=int, default=16, help='per-GPU micro-batch (images)')
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
-    p.add_argument('--impl', choices=['fused', 'eager'], default='eager')
+    p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
+    p.add_argument('--model', choices=['ducknet', 'unet'], default='ducknet')
+    p.add_argument('--graph-ddp', action='store_true', help='also capture the multi-GPU step in a hipGraph')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
     return p.parse_args(argv)
@@ -56,9 +58,10 @@ def main(argv=None):
     device = torch.device('cuda', local_rank)
 
     impl = args.impl
+    use_graph = not args.no_graph and (world == 1 or args.graph_ddp)
     step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
                             base_channel=args.base_channel, device=device,
-                            channels_last=args.channels_last, use_graph=not args.no_graph,
+                            channels_last=args.channels_last, use_graph=use_graph,
                             distributed=world > 1)
 
     for _ in range(args.warmup):
@@ -100,7 +103,7 @@ def main(argv=None):
             'config': {'model': f'DUCKNet-{args.base_channel}', 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
-                       'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1},
+                       'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph},
         }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -1,0 +1,315 @@
+// PyTorch binding of the MI355X kernels (module `medical_segmentation_pytorch_amd._C`).
+// Thin adapters only: shape/dtype/device checks, then the plain launchers in launchers.h on the
+// current HIP stream (so everything composes with torch streams and hipGraph capture).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "launchers.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda() && (t).is_contiguous(), #t " must be a contiguous GPU tensor")
+#define CHECK_BF16(t) CHECK_DEV(t); TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) CHECK_DEV(t); TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
+#define CHECK_I64(t) CHECK_DEV(t); TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+
+inline uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+inline float* f32(const at::Tensor& t) { return t.data_ptr<float>(); }
+inline const float* f32_opt(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_F32(*t);
+  return t->data_ptr<float>();
+}
+inline float* f32_opt_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(f32_opt(t)); }
+
+ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>& dy, const std::vector<int64_t>& dx) {
+  TORCH_CHECK(dims.size() == 13, "geom dims = [N, IH, IW, Gi, Cgi, OH, OW, Go, Cgo, Cgo_l, T, Kp, stride]");
+  ConvGeom g{};
+  g.N = dims[0]; g.IH = dims[1]; g.IW = dims[2]; g.Gi = dims[3]; g.Cgi = dims[4];
+  g.OH = dims[5]; g.OW = dims[6]; g.Go = dims[7]; g.Cgo = dims[8]; g.Cgo_l = dims[9];
+  g.T = dims[10]; g.Kp = dims[11]; g.stride = dims[12];
+  TORCH_CHECK(g.T >= 1 && g.T <= kMaxTaps && (int)dy.size() == g.T && (int)dx.size() == g.T, "bad tap table");
+  TORCH_CHECK(g.Gi >= 1 && g.Gi <= kMaxGroups && g.Go >= 1 && g.Go <= kMaxGroups, "1..8 channel groups");
+  TORCH_CHECK(g.Cgi % 8 == 0 && g.Cgo % 8 == 0, "channel dims must be padded to a multiple of 8");
+  TORCH_CHECK(g.Kp % 32 == 0 && g.Kp >= g.T * g.Gi * g.Cgi, "Kp must be a multiple of 32 covering T*Cip");
+  TORCH_CHECK(g.Cgo_l <= g.Cgo && g.stride >= 1, "bad output channels / stride");
+  for (int i = 0; i < g.T; ++i) { g.dy[i] = dy[i]; g.dx[i] = dx[i]; }
+  return g;
+}
+
+void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys,
+              const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& stat_part,
+              std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  ConvGeom g = make_geom(dims, dy, dx);
+  TORCH_CHECK((int)xs.size() == g.Gi && (int)ys.size() == g.Go, "group count mismatch");
+  ConvArgs a{};
+  for (int i = 0; i < g.Gi; ++i) {
+    CHECK_BF16(xs[i]);
+    TORCH_CHECK(xs[i].numel() == (int64_t)g.N * g.IH * g.IW * g.Cgi, "x numel mismatch");
+    a.x[i] = bf(xs[i]);
+  }
+  for (int i = 0; i < g.Go; ++i) {
+    CHECK_BF16(ys[i]);
+    TORCH_CHECK(ys[i].numel() == (int64_t)g.N * g.OH * g.OW * g.Cgo, "y numel mismatch");
+    a.y[i] = bf(ys[i]);
+  }
+  CHECK_BF16(wp);
+  TORCH_CHECK(wp.numel() == (int64_t)conv_rows_alloc(g.Go * g.Cgo) * g.Kp, "packed weight numel mismatch");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(g.Go == 1 && bias->numel() == g.Cgo_l, "bias: 1 group only");
+  if (stat_part.has_value() && stat_part->defined())
+    TORCH_CHECK(stat_part->numel() == conv_stat_blocks(g) * 2 * g.Go * g.Cgo, "stat_part numel mismatch");
+  a.w = bf(wp);
+  a.bias = f32_opt(bias);
+  a.stat_part = f32_opt_mut(stat_part);
+  a.g = g;
+  conv_igemm(a, trans, cur_stream());
+}
+
+void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const at::Tensor& dw,
+                  std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  ConvGeom g = make_geom(dims, dy, dx);
+  TORCH_CHECK((int)xs.size() == g.Gi && (int)dys.size() == g.Go, "group count mismatch");
+  std::vector<const uint16_t*> px, pd;
+  for (auto& t : xs) { CHECK_BF16(t); TORCH_CHECK(t.numel() == (int64_t)g.N * g.IH * g.IW * g.Cgi); px.push_back(bf(t)); }
+  for (auto& t : dys) { CHECK_BF16(t); TORCH_CHECK(t.numel() == (int64_t)g.N * g.OH * g.OW * g.Cgo); pd.push_back(bf(t)); }
+  CHECK_F32(dw);
+  TORCH_CHECK(dw.numel() == (int64_t)g.Go * g.Cgo * g.T * g.Gi * g.Cgi, "dw numel mismatch");
+  conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cur_stream());
+}
+
+int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  return conv_stat_blocks(make_geom(dims, dy, dx));
+}
+
+void pack_weight_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
+                   int64_t Kp, int64_t t_base, int64_t c_base, int64_t s_row, int64_t s_ch) {
+  CHECK_F32(src); CHECK_BF16(dst);
+  TORCH_CHECK(dst.numel() >= nrow * Kp && (t_base + T - 1) * Cpk + c_base + nch <= Kp, "dst too small");
+  TORCH_CHECK(src.numel() >= (nrow - 1) * s_row + (nch - 1) * s_ch + T, "src too small");
+  pack_weight(f32(src), bf(dst), nrow, nch, T, Cpk, Kp, t_base, c_base, s_row, s_ch, cur_stream());
+}
+
+void unpack_wgrad_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
+                    int64_t Ktot, int64_t t_base, int64_t c_base, int64_t s_row, int64_t s_ch, bool accumulate) {
+  CHECK_F32(src);
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat, "dst must be fp32 GPU");
+  TORCH_CHECK(src.numel() >= nrow * Ktot && (t_base + T - 1) * Cpk + c_base + nch <= Ktot, "src too small");
+  TORCH_CHECK(dst.numel() >= (nrow - 1) * s_row + (nch - 1) * s_ch + T, "dst too small");
+  unpack_wgrad(f32(src), dst.data_ptr<float>(), nrow, nch, T, Cpk, Ktot, t_base, c_base, s_row, s_ch, accumulate,
+               cur_stream());
+}
+
+void pack_batch_t(const at::Tensor& jobs, const at::Tensor& prefix, int64_t total_blocks) {
+  CHECK_I64(jobs);
+  CHECK_DEV(prefix);
+  TORCH_CHECK(prefix.scalar_type() == at::kInt && jobs.dim() == 2 && jobs.size(1) == 12 &&
+              prefix.numel() == jobs.size(0), "pack_batch: bad job table");
+  pack_batch(jobs.data_ptr<int64_t>(), prefix.data_ptr<int>(), (int)jobs.size(0), (int)total_blocks, cur_stream());
+}
+
+void sum_stats_t(std::vector<at::Tensor> inputs, const c10::optional<at::Tensor>& out, const at::Tensor& part,
+                 int64_t P, int64_t Cp) {
+  TORCH_CHECK(!inputs.empty() && (int)inputs.size() <= kMaxSumInputs, "1..8 inputs");
+  TORCH_CHECK(Cp % 8 == 0 && Cp <= 2048, "Cp must be a multiple of 8, <= 2048");
+  std::vector<const uint16_t*> ptrs;
+  for (auto& t : inputs) { CHECK_BF16(t); TORCH_CHECK(t.numel() == P * Cp, "input numel mismatch"); ptrs.push_back(bf(t)); }
+  uint16_t* o = nullptr;
+  if (out.has_value() && out->defined()) { CHECK_BF16(*out); TORCH_CHECK(out->numel() == P * Cp); o = bf(*out); }
+  CHECK_F32(part);
+  TORCH_CHECK(part.numel() == bn_partial_blocks(P, Cp) * 2 * Cp, "part numel mismatch");
+  sum_stats(ptrs.data(), (int)ptrs.size(), o, f32(part), P, Cp, cur_stream());
+}
+
+void bn_reduce_partials_t(const at::Tensor& part, int64_t nblk, int64_t width, int64_t col_off, int64_t Cp,
+                          const at::Tensor& sums) {
+  CHECK_F32(part); CHECK_F32(sums);
+  TORCH_CHECK(part.numel() == nblk * 2 * width && col_off + Cp <= width && sums.numel() == 2 * Cp, "size mismatch");
+  auto tmp = at::empty({(int64_t)bn_reduce_splits(nblk) * 2 * Cp}, sums.options().dtype(at::kDouble));
+  bn_reduce_partials(f32(part), nblk, width, col_off, Cp, f32(sums), tmp.data_ptr<double>(), cur_stream());
+}
+
+void bn_finalize_t(const at::Tensor& sums, int64_t C, int64_t Cp, double count, const c10::optional<at::Tensor>& gamma,
+                   const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& rmean,
+                   const c10::optional<at::Tensor>& rvar, double momentum, double eps, bool training,
+                   const at::Tensor& stats) {
+  CHECK_F32(sums); CHECK_F32(stats);
+  TORCH_CHECK(stats.numel() == 4 * Cp, "stats = [scale, shift, mean, invstd] x Cp");
+  TORCH_CHECK(training || (rmean.has_value() && rvar.has_value()), "eval BN needs running stats");
+  float* st = f32(stats);
+  bn_finalize(f32(sums), C, Cp, (float)count, f32_opt(gamma), f32_opt(beta), f32_opt_mut(rmean), f32_opt_mut(rvar),
+              (float)momentum, (float)eps, training ? 1 : 0, st, st + Cp, st + 2 * Cp, st + 3 * Cp, cur_stream());
+}
+
+void bn_act_apply_t(const at::Tensor& y, const at::Tensor& stats, const at::Tensor& z, int64_t P, int64_t Cp, bool relu) {
+  CHECK_BF16(y); CHECK_BF16(z); CHECK_F32(stats);
+  TORCH_CHECK(y.numel() == P * Cp && z.numel() == P * Cp && stats.numel() == 4 * Cp);
+  const float* st = f32(stats);
+  bn_act_apply(bf(y), st, st + Cp, bf(z), P, Cp, relu ? 1 : 0, cur_stream());
+}
+
+void bn_act_bwd_partial_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& part,
+                          int64_t P, int64_t Cp, bool relu) {
+  CHECK_BF16(dz); CHECK_BF16(y); CHECK_F32(stats); CHECK_F32(part);
+  TORCH_CHECK(dz.numel() == P * Cp && y.numel() == P * Cp && stats.numel() == 4 * Cp);
+  TORCH_CHECK(part.numel() == bn_partial_blocks(P, Cp) * 2 * Cp, "part numel mismatch");
+  const float* st = f32(stats);
+  bn_act_bwd_partial(bf(dz), bf(y), st, st + Cp, st + 2 * Cp, f32(part), P, Cp, relu ? 1 : 0, cur_stream());
+}
+
+void bn_bwd_finalize_t(const at::Tensor& sums, int64_t C, int64_t Cp, double count, const at::Tensor& stats,
+                       const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+                       const at::Tensor& coef) {
+  CHECK_F32(sums); CHECK_F32(stats); CHECK_F32(coef);
+  TORCH_CHECK(coef.numel() == 3 * Cp && stats.numel() == 4 * Cp && sums.numel() == 2 * Cp);
+  const float* st = f32(stats);
+  bn_bwd_finalize(f32(sums), C, Cp, (float)count, st, st + 3 * Cp, st + 2 * Cp, f32_opt_mut(dgamma),
+                  f32_opt_mut(dbeta), f32(coef), cur_stream());
+}
+
+void bn_act_bwd_apply_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& coef,
+                        const at::Tensor& dy, int64_t P, int64_t Cp, bool relu) {
+  CHECK_BF16(dz); CHECK_BF16(y); CHECK_BF16(dy); CHECK_F32(stats); CHECK_F32(coef);
+  TORCH_CHECK(dz.numel() == P * Cp && y.numel() == P * Cp && dy.numel() == P * Cp);
+  const float* st = f32(stats);
+  bn_act_bwd_apply(bf(dz), bf(y), st, st + Cp, f32(coef), bf(dy), P, Cp, relu ? 1 : 0, cur_stream());
+}
+
+void nchw_to_nhwc_t(const at::Tensor& x, const at::Tensor& y, int64_t Cp) {
+  CHECK_F32(x); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.numel() == (int64_t)N * H * W * Cp && C <= Cp);
+  nchw_to_nhwc(f32(x), bf(y), N, C, H, W, Cp, cur_stream());
+}
+
+void nhwc_to_nchw_t(const at::Tensor& x, const at::Tensor& y, int64_t Cp) {
+  CHECK_BF16(x); CHECK_F32(y);
+  TORCH_CHECK(y.dim() == 4, "y must be NCHW");
+  const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  TORCH_CHECK(x.numel() == (int64_t)N * H * W * Cp && C <= Cp);
+  nhwc_to_nchw(bf(x), f32(y), N, C, H, W, Cp, cur_stream());
+}
+
+void up2_add_t(const at::Tensor& low, const at::Tensor& skip, const at::Tensor& out, int64_t N, int64_t h, int64_t w,
+               int64_t Cp) {
+  CHECK_BF16(low); CHECK_BF16(skip); CHECK_BF16(out);
+  TORCH_CHECK(low.numel() == N * h * w * Cp && skip.numel() == 4 * N * h * w * Cp && out.numel() == skip.numel());
+  up2_add(bf(low), bf(skip), bf(out), N, h, w, Cp, cur_stream());
+}
+
+void pool2_sum_t(const at::Tensor& g, const at::Tensor& out, int64_t N, int64_t h, int64_t w, int64_t Cp) {
+  CHECK_BF16(g); CHECK_BF16(out);
+  TORCH_CHECK(out.numel() == N * h * w * Cp && g.numel() == 4 * out.numel());
+  pool2_sum(bf(g), bf(out), N, h, w, Cp, cur_stream());
+}
+
+void add_n_t(std::vector<at::Tensor> inputs, const at::Tensor& out) {
+  TORCH_CHECK(!inputs.empty() && (int)inputs.size() <= kMaxSumInputs);
+  CHECK_BF16(out);
+  TORCH_CHECK(out.numel() % 8 == 0);
+  std::vector<const uint16_t*> ptrs;
+  for (auto& t : inputs) { CHECK_BF16(t); TORCH_CHECK(t.numel() == out.numel()); ptrs.push_back(bf(t)); }
+  add_n(ptrs.data(), (int)ptrs.size(), bf(out), out.numel(), cur_stream());
+}
+
+void scale_f32_t(const at::Tensor& x, const c10::optional<at::Tensor>& scalar, double mult) {
+  CHECK_F32(x);
+  scale_f32(f32(x), f32_opt(scalar), (float)mult, x.numel(), cur_stream());
+}
+
+int64_t ce_blocks_t(int64_t P) { return ce_blocks(P); }
+
+void ce_fwd_bwd_t(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& weight,
+                  const at::Tensor& grad, const c10::optional<at::Tensor>& pix_loss, const at::Tensor& part,
+                  int64_t ignore_index) {
+  CHECK_F32(logits); CHECK_I64(target); CHECK_F32(grad); CHECK_F32(part);
+  TORCH_CHECK(logits.dim() == 4, "logits must be NCHW");
+  const int N = logits.size(0), C = logits.size(1);
+  const long HW = logits.size(2) * logits.size(3);
+  TORCH_CHECK(target.numel() == (int64_t)N * HW && grad.numel() == logits.numel());
+  TORCH_CHECK(part.numel() == 2 * ce_blocks((long)N * HW));
+  float* pl = f32_opt_mut(pix_loss);
+  if (pl) TORCH_CHECK(pix_loss->numel() == (int64_t)N * HW);
+  ce_fwd_bwd(f32(logits), target.data_ptr<int64_t>(), f32_opt(weight), f32(grad), pl, f32(part), N, C, HW,
+             (int)ignore_index, cur_stream());
+}
+
+void kd_kl_fwd_bwd_t(const at::Tensor& s, const at::Tensor& t, const at::Tensor& grad, const at::Tensor& part,
+                     double T) {
+  CHECK_F32(s); CHECK_F32(t); CHECK_F32(grad); CHECK_F32(part);
+  TORCH_CHECK(s.dim() == 4 && s.sizes() == t.sizes() && grad.numel() == s.numel());
+  const int N = s.size(0), C = s.size(1);
+  const long HW = s.size(2) * s.size(3);
+  TORCH_CHECK(part.numel() == ce_blocks((long)N * HW));
+  kd_kl_fwd_bwd(f32(s), f32(t), f32(grad), f32(part), N, C, HW, (float)T, cur_stream());
+}
+
+void adam_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+                 const at::Tensor& hyper, bool adamw) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(hyper);
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel() && hyper.numel() >= 8);
+  adam_step(f32(p), f32(g), f32(m), f32(v), f32(hyper), p.numel(), adamw ? 1 : 0, cur_stream());
+}
+
+void sgd_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, const at::Tensor& hyper) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_F32(buf); CHECK_F32(hyper);
+  TORCH_CHECK(g.numel() == p.numel() && buf.numel() == p.numel() && hyper.numel() >= 4);
+  sgd_step(f32(p), f32(g), f32(buf), f32(hyper), p.numel(), cur_stream());
+}
+
+void ema_update_t(const at::Tensor& ema, const at::Tensor& model, const at::Tensor& hyper) {
+  CHECK_F32(ema); CHECK_F32(model); CHECK_F32(hyper);
+  TORCH_CHECK(ema.numel() == model.numel());
+  ema_update(f32(ema), f32(model), f32(hyper), ema.numel(), cur_stream());
+}
+
+void confmat_update_t(const at::Tensor& logits, const at::Tensor& target, const at::Tensor& confmat,
+                      int64_t ignore_index) {
+  CHECK_F32(logits); CHECK_I64(target); CHECK_I64(confmat);
+  TORCH_CHECK(logits.dim() == 4);
+  const int N = logits.size(0), C = logits.size(1);
+  const long HW = logits.size(2) * logits.size(3);
+  TORCH_CHECK(C * C <= 1024 && confmat.numel() == (int64_t)C * C && target.numel() == (int64_t)N * HW);
+  confmat_update(f32(logits), target.data_ptr<int64_t>(), confmat.data_ptr<int64_t>(), N, C, HW, (int)ignore_index,
+                 cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_wgrad", &conv_wgrad_t);
+  m.def("conv_pick_mi", &conv_pick_mi);
+  m.def("conv_rows_alloc", &conv_rows_alloc);
+  m.def("conv_stat_blocks", &conv_stat_blocks_t);
+  m.def("pack_weight", &pack_weight_t);
+  m.def("unpack_wgrad", &unpack_wgrad_t);
+  m.def("pack_batch", &pack_batch_t);
+  m.def("pack_per_block", &pack_per_block);
+  m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });
+  m.def("sum_stats", &sum_stats_t);
+  m.def("bn_reduce_partials", &bn_reduce_partials_t);
+  m.def("bn_finalize", &bn_finalize_t);
+  m.def("bn_act_apply", &bn_act_apply_t);
+  m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize_t);
+  m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc_t);
+  m.def("nhwc_to_nchw", &nhwc_to_nchw_t);
+  m.def("up2_add", &up2_add_t);
+  m.def("pool2_sum", &pool2_sum_t);
+  m.def("add_n", &add_n_t);
+  m.def("scale_f32", &scale_f32_t);
+  m.def("ce_blocks", &ce_blocks_t);
+  m.def("ce_fwd_bwd", &ce_fwd_bwd_t);
+  m.def("kd_kl_fwd_bwd", &kd_kl_fwd_bwd_t);
+  m.def("adam_step", &adam_step_t);
+  m.def("sgd_step", &sgd_step_t);
+  m.def("ema_update", &ema_update_t);
+  m.def("confmat_update", &confmat_update_t);
+}

@@ -1,0 +1,309 @@
+// BatchNorm(+ReLU) for NHWC bf16 feature maps: training statistics, finalize (running stats with
+// momentum + unbiased variance, exactly nn.BatchNorm2d / SyncBatchNorm semantics), fused
+// normalize+ReLU apply, and the two-pass backward (channel reductions, then the elementwise dx).
+//
+// Reference ops replaced: every BatchNorm2d / SyncBatchNorm + ReLU pair of the models
+// (models/modules.py:83-84, models/ducknet.py:99,120,137; SURVEY §2.5 K8-K10, K11 branch sums).
+//
+// Reductions are deterministic: each block writes per-channel partials ([nblk][2][Cp] fp32) and a
+// second kernel sums them in a fixed order in fp64.  The cross-rank SyncBN exchange happens on the
+// tiny [2][Cp] sums between `bn_reduce_partials` and `bn_finalize` (host side, RCCL all_reduce).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct SumInputs { const uint16_t* p[kMaxSumInputs]; };
+
+// Thread layout for per-channel reductions over NHWC: cg = tid % CG (8-channel group), r = tid / CG.
+__global__ __launch_bounds__(kBlock) void sum_stats_kernel(SumInputs in, int k, uint16_t* __restrict__ out,
+                                                           float* __restrict__ part, long P, int Cp) {
+  __shared__ float red[2][kBlock][8];
+  const int CG = Cp >> 3;
+  const int R = kBlock / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, r = tid / CG;
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (r < R) {
+    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
+      const long off = p * Cp + 8 * cg;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(in.p[0] + off), v);
+      for (int i = 1; i < k; ++i) {
+        float u[8];
+        unpack8(*reinterpret_cast<const uint4*>(in.p[i] + off), u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += u[e];
+      }
+      if (out != nullptr) {
+        uint4 pk = pack8(v);
+        *reinterpret_cast<uint4*>(out + off) = pk;
+        unpack8(pk, v);  // statistics of the stored (rounded) tensor
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] += v[e]; q[e] += v[e] * v[e]; }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+  __syncthreads();
+  for (int c = tid; c < Cp; c += kBlock) {
+    const int g = c >> 3, e = c & 7;
+    float ss = 0.f, qq = 0.f;
+    for (int rr = 0; rr < R; ++rr) { ss += red[0][rr * CG + g][e]; qq += red[1][rr * CG + g][e]; }
+    part[((long)blockIdx.x * 2 + 0) * Cp + c] = ss;
+    part[((long)blockIdx.x * 2 + 1) * Cp + c] = qq;
+  }
+}
+
+// Two-stage deterministic column reduction of [nblk][2][width] partials:
+//   stage 1: grid (column chunks of 64, S row splits); 256 threads = 64 columns x 4 row lanes
+//   stage 2: one thread per column sums the S split results in order (fp64).
+constexpr int kRedCols = 64, kRedRows = 4, kRedSplits = 64;
+
+__global__ __launch_bounds__(256) void reduce_partials_stage1(const float* __restrict__ part, long nblk, int width,
+                                                              int col_off, int Cp, double* __restrict__ tmp) {
+  __shared__ double red[kRedRows][kRedCols];
+  const int ncol = 2 * Cp;
+  const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int col = blockIdx.x * kRedCols + cl;
+  const long per = (nblk + gridDim.y - 1) / gridDim.y;
+  const long r0 = (long)blockIdx.y * per;
+  const long r1 = r0 + per < nblk ? r0 + per : nblk;
+  double acc = 0.0;
+  if (col < ncol) {
+    const int sidx = col / Cp, c = col - sidx * Cp;
+    const float* src = part + (long)sidx * width + col_off + c;
+    for (long b = r0 + rl; b < r1; b += kRedRows) acc += (double)src[b * 2 * width];
+  }
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && col < ncol) {
+    double s = 0.0;
+    for (int r = 0; r < kRedRows; ++r) s += red[r][cl];
+    tmp[(long)blockIdx.y * ncol + col] = s;
+  }
+}
+
+__global__ void reduce_partials_stage2(const double* __restrict__ tmp, int splits, int ncol, float* __restrict__ sums) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= ncol) return;
+  double s = 0.0;
+  for (int i = 0; i < splits; ++i) s += tmp[(long)i * ncol + col];
+  sums[col] = (float)s;
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ sums, int C, int Cp, float count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
+                                   float eps, int training, float* __restrict__ scale,
+                                   float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cp) return;
+  if (c >= C) { scale[c] = 0.f; shift[c] = 0.f; mean_out[c] = 0.f; invstd_out[c] = 0.f; return; }
+  float mean, var;
+  if (training) {
+    const double m = (double)sums[c] / count;
+    double v = (double)sums[Cp + c] / count - m * m;
+    if (v < 0) v = 0;
+    mean = (float)m; var = (float)v;
+    if (rmean != nullptr) {
+      const float unbiased = count > 1.f ? (float)(v * count / (count - 1.f)) : (float)v;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+    }
+  } else {
+    mean = rmean[c]; var = rvar[c];
+  }
+  const float inv = rsqrtf(var + eps);
+  const float gm = gamma != nullptr ? gamma[c] : 1.f;
+  const float bt = beta != nullptr ? beta[c] : 0.f;
+  scale[c] = gm * inv;
+  shift[c] = bt - mean * gm * inv;
+  mean_out[c] = mean;
+  invstd_out[c] = inv;
+}
+
+__global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __restrict__ y,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              uint16_t* __restrict__ z, long nvec, int CG,
+                                                              int relu) {
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
+    const int c0 = (int)(i % CG) * 8;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), v);
+    const float4 a0 = *reinterpret_cast<const float4*>(scale + c0), a1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(shift + c0), b1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
+    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = fmaf(v[e], a[e], b[e]);
+      v[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+    *reinterpret_cast<uint4*>(z + i * 8) = pack8(v);
+  }
+}
+
+DEVI void load8f(const float* p, float* d) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+__global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
+    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, float* __restrict__ part, long P,
+    int Cp, int relu) {
+  __shared__ float red[2][kBlock][8];
+  const int CG = Cp >> 3;
+  const int R = kBlock / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, r = tid / CG;
+  float s[8], q[8], a[8], b[8], mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  load8f(scale + 8 * cg, a);
+  load8f(shift + 8 * cg, b);
+  load8f(mean + 8 * cg, mu);
+  if (r < R) {
+    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
+      const long off = p * Cp + 8 * cg;
+      float g[8], v[8];
+      unpack8(*reinterpret_cast<const uint4*>(dz + off), g);
+      unpack8(*reinterpret_cast<const uint4*>(y + off), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
+        s[e] += gr;
+        q[e] += gr * (v[e] - mu[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+  __syncthreads();
+  for (int c = tid; c < Cp; c += kBlock) {
+    const int g = c >> 3, e = c & 7;
+    float ss = 0.f, qq = 0.f;
+    for (int rr = 0; rr < R; ++rr) { ss += red[0][rr * CG + g][e]; qq += red[1][rr * CG + g][e]; }
+    part[((long)blockIdx.x * 2 + 0) * Cp + c] = ss;
+    part[((long)blockIdx.x * 2 + 1) * Cp + c] = qq;
+  }
+}
+
+// coef[3][Cp]: dy = k1*dzr + k2*y + k3  (k1 = gamma*invstd, k2 = -k1*invstd*sum(dzr*xmu)/M,
+// k3 = -k1*sum(dzr)/M - k2*mean).  dgamma/dbeta are ACCUMULATED into the fp32 parameter grads.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ sums, int C, int Cp, float count,
+                                       const float* __restrict__ scale, const float* __restrict__ invstd,
+                                       const float* __restrict__ mean, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cp) return;
+  if (c >= C) { coef[c] = 0.f; coef[Cp + c] = 0.f; coef[2 * Cp + c] = 0.f; return; }
+  const float sd = sums[c], sdx = sums[Cp + c];
+  if (dgamma != nullptr) dgamma[c] += sdx * invstd[c];
+  if (dbeta != nullptr) dbeta[c] += sd;
+  const float k1 = scale[c];
+  const float k2 = -k1 * invstd[c] * invstd[c] * sdx / count;
+  const float k3 = -k1 * sd / count - k2 * mean[c];
+  coef[c] = k1; coef[Cp + c] = k2; coef[2 * Cp + c] = k3;
+}
+
+__global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
+    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ coef, uint16_t* __restrict__ dy, long nvec,
+    int CG, int relu) {
+  const int Cp = CG * 8;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
+    const int c0 = (int)(i % CG) * 8;
+    float g[8], v[8], a[8], b[8], k1[8], k2[8], k3[8];
+    unpack8(*reinterpret_cast<const uint4*>(dz + i * 8), g);
+    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), v);
+    load8f(scale + c0, a); load8f(shift + c0, b);
+    load8f(coef + c0, k1); load8f(coef + Cp + c0, k2); load8f(coef + 2 * Cp + c0, k3);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
+      g[e] = k1[e] * gr + k2[e] * v[e] + k3[e];
+    }
+    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(g);
+  }
+}
+
+int grid_for(long nvec) {
+  long b = (nvec + kBlock - 1) / kBlock;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+long bn_partial_blocks(long P, int Cp) {
+  const int CG = Cp / 8;
+  const int R = kBlock / CG;
+  long b = (P + (long)R * 16 - 1) / ((long)R * 16);
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return b;
+}
+
+void sum_stats(const uint16_t* const* inputs, int k, uint16_t* out, float* part, long P, int Cp, hipStream_t s) {
+  SumInputs in{};
+  for (int i = 0; i < k; ++i) in.p[i] = inputs[i];
+  hipLaunchKernelGGL(sum_stats_kernel, dim3(bn_partial_blocks(P, Cp)), dim3(kBlock), 0, s, in, k, out, part, P, Cp);
+}
+
+int bn_reduce_splits(long nblk) {
+  long sp = nblk / 32;
+  if (sp > kRedSplits) sp = kRedSplits;
+  if (sp < 1) sp = 1;
+  return (int)sp;
+}
+
+void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, float* sums, double* tmp,
+                        hipStream_t s) {
+  const int splits = bn_reduce_splits(nblk);
+  hipLaunchKernelGGL(reduce_partials_stage1, dim3(cdiv(2 * Cp, kRedCols), splits), dim3(256), 0, s, part, nblk, width,
+                     col_off, Cp, tmp);
+  hipLaunchKernelGGL(reduce_partials_stage2, dim3(cdiv(2 * Cp, 256)), dim3(256), 0, s, tmp, splits, 2 * Cp, sums);
+}
+
+void bn_finalize(const float* sums, int C, int Cp, float count, const float* gamma, const float* beta,
+                 float* running_mean, float* running_var, float momentum, float eps, int training,
+                 float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, sums, C, Cp, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, training, scale, shift, mean, invstd);
+}
+
+void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
+                  int relu, hipStream_t s) {
+  const long nvec = P * (Cp / 8);
+  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, y, scale, shift, z, nvec,
+                     Cp / 8, relu);
+}
+
+void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                        const float* mean, float* part, long P, int Cp, int relu, hipStream_t s) {
+  hipLaunchKernelGGL(bn_act_bwd_partial_kernel, dim3(bn_partial_blocks(P, Cp)), dim3(kBlock), 0, s, dz, y, scale,
+                     shift, mean, part, P, Cp, relu);
+}
+
+void bn_bwd_finalize(const float* sums, int C, int Cp, float count, const float* scale, const float* invstd,
+                     const float* mean, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, sums, C, Cp, count, scale,
+                     invstd, mean, dgamma, dbeta, coef);
+}
+
+void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                      const float* coef, uint16_t* dy, long P, int Cp, int relu, hipStream_t s) {
+  const long nvec = P * (Cp / 8);
+  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, dz, y, scale, shift, coef,
+                     dy, nvec, Cp / 8, relu);
+}

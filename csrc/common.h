@@ -1,0 +1,54 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * Feature maps are NHWC bf16 with the channel dim padded to a multiple of 8 ("Cp"), so one
+//     16-byte vector = 8 channels of one pixel and every vector access is 16-B aligned.  Padded
+//     channels always hold +0.0 (producers write zeros there), so consumers may read them freely.
+//   * bf16 is carried as raw uint16_t bits on the device side; math is fp32.
+//   * Wave size is 64 (CDNA).  Block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+#define DEVI __device__ __forceinline__
+
+DEVI float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+DEVI uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+DEVI uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+DEVI void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+DEVI uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+DEVI bf16x8_t as_bf16x8(const uint4& v) {
+  union { uint4 u; bf16x8_t b; } c; c.u = v; return c.b;
+}
+
+DEVI f32x4_t mfma16x16x32(const uint4& a, const uint4& b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+DEVI float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

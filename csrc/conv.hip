@@ -1,0 +1,510 @@
+// Implicit-GEMM convolution for CDNA4 (gfx950): forward, data-gradient and weight-gradient, NHWC bf16
+// activations with fp32 accumulation on v_mfma_f32_16x16x32_bf16.
+//
+// Replaces every cuDNN/MIOpen convolution the reference dispatches:
+//   3x3 d1/d2/d3 (models/ducknet.py:95-96,160-170), 1x7/7x1 (ducknet.py:177-178), 1x1
+//   (ducknet.py:93, heads), 3x3 s2 and 2x2 s2 (ducknet.py:60-61), and the UNet transposed conv
+//   (models/modules.py:99-102) which is exactly the data-gradient of a strided conv.
+//
+// GEMM view (one kernel family for all of them):
+//     D[co][m] = sum_k  Wp[co][k] * Xcol[k][m]        m = output pixel (n, oh, ow), k = t*Cip + ci
+// A operand = packed weights Wp[co][k] (8 consecutive k are contiguous -> one 16-B load per lane).
+// B operand = the im2col column of pixel m; in NHWC the 8 consecutive k of a lane are 8 consecutive
+// channels of ONE shifted input pixel -> one aligned 16-B load per lane, no transpose needed.
+// Taps are an explicit (dy, dx) offset table, so dilation, asymmetric kernels (1x7), the 1x1 centre
+// tap of horizontally fused convs and the flipped taps of the data-gradient are the same code.
+// Output layout of the 16x16x32 tile: lane holds rows 4*(lane>>4)+r (= 4 consecutive co) of column
+// lane&15 (= one pixel) -> 8-B NHWC stores.
+//
+// "TRANS" mode maps output pixel o to input pixel (o + d) / stride when divisible: the data-gradient
+// of a stride-s conv, and the forward of ConvTranspose2d.
+// Channel GROUPS (launchers.h): the logical input/output channel dims may be split over up to 8
+// separate NHWC tensors; group pointers are staged in LDS and selected per lane per k-step.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+// Per-lane position in the flattened K = (tap, input group, channel) walk, advanced 32 at a time.
+struct KPos { int t, gi, cl; };
+
+DEVI KPos kpos_init(int kg, const ConvGeom& g) {
+  const int Cip = g.Gi * g.Cgi;
+  KPos p;
+  p.t = kg / Cip;
+  const int rem = kg - p.t * Cip;
+  p.gi = rem / g.Cgi;
+  p.cl = rem - p.gi * g.Cgi;
+  return p;
+}
+
+DEVI void kpos_advance(KPos& p, int by, const ConvGeom& g) {
+  p.cl += by;
+  while (p.cl >= g.Cgi) {
+    p.cl -= g.Cgi;
+    if (++p.gi == g.Gi) { p.gi = 0; ++p.t; }
+  }
+}
+
+// Maps output pixel (ph, pw) [already multiplied by stride in fwd mode] + tap offset to an input
+// pixel index, or -1 when the tap falls in the zero padding / is not stride-aligned.
+template <bool TRANS>
+DEVI int in_pixel(int pn, int ph, int pw, int2 d, const ConvGeom& g) {
+  if (!TRANS) {
+    const int ih = ph + d.x, iw = pw + d.y;
+    if ((unsigned)ih < (unsigned)g.IH && (unsigned)iw < (unsigned)g.IW) return pn + ih * g.IW + iw;
+    return -1;
+  } else {
+    const int a = ph + d.x, b = pw + d.y;
+    if (a < 0 || b < 0) return -1;
+    const int ih = a / g.stride, iw = b / g.stride;
+    if (ih * g.stride != a || iw * g.stride != b || ih >= g.IH || iw >= g.IW) return -1;
+    return pn + ih * g.IW + iw;
+  }
+}
+
+template <int MI, int NJ, int WPX, bool TRANS>
+__global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
+  const ConvGeom& g = a.g;
+  __shared__ int2 s_tap[kMaxTaps];
+  __shared__ const uint16_t* s_x[kMaxGroups];
+  __shared__ uint16_t* s_y[kMaxGroups];
+  __shared__ float s_stat[WPX][2][16 * MI];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid], g.dx[tid]);
+  if (tid < kMaxGroups) { s_x[tid] = a.x[tid]; s_y[tid] = a.y[tid]; }
+  __syncthreads();
+
+  const long OHW = (long)g.OH * g.OW;
+  const long M = (long)g.N * OHW;
+  const long m0 = ((long)blockIdx.x * WPX + wave) * (16 * NJ);
+  const int co0 = blockIdx.y * (16 * MI);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int IHW = g.IH * g.IW;
+  const int rows = g.Go * g.Cgo;
+
+  int pn[NJ], ph[NJ], pw[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const long m = m0 + 16 * j + lr;
+    if (m < M) {
+      const int n = (int)(m / OHW);
+      const int r = (int)(m - (long)n * OHW);
+      const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
+      pn[j] = n * IHW;
+      ph[j] = TRANS ? oh : oh * g.stride;
+      pw[j] = TRANS ? ow : ow * g.stride;
+    } else {
+      pn[j] = -1; ph[j] = 0; pw[j] = 0;
+    }
+  }
+  const uint16_t* wrow[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + 8 * lg;
+
+  KPos kp = kpos_init(8 * lg, g);
+
+  auto load_b = [&](uint4* B, const KPos& p) {
+    const bool kval = p.t < g.T;
+    const int2 d = kval ? s_tap[p.t] : make_int2(0, 0);
+    const uint16_t* xb = s_x[kval ? p.gi : 0] + p.cl;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (pn[j] >= 0 && kval) {
+        const int pix = in_pixel<TRANS>(pn[j], ph[j], pw[j], d, g);
+        if (pix >= 0) v = *reinterpret_cast<const uint4*>(xb + (long)pix * g.Cgi);
+      }
+      B[j] = v;
+    }
+  };
+  auto load_a = [&](uint4* A, int k0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + k0);
+  };
+
+  f32x4_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 A[MI], B[NJ];
+  load_a(A, 0);
+  load_b(B, kp);
+  for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+    uint4 An[MI], Bn[NJ];
+    const bool more = k0 + 32 < g.Kp;
+    if (more) {
+      kpos_advance(kp, 32, g);
+      load_a(An, k0 + 32);
+      load_b(Bn, kp);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) A[i] = An[i];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) B[j] = Bn[j];
+    }
+  }
+
+  // Epilogue: bias, bf16 pack, 8-B NHWC stores into the row's output group; optional per-channel
+  // (sum, sum^2) partials of the stored (bf16-rounded) values for the BatchNorm that follows.
+  float csum[MI][4], csq[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
+    const int cb = co0 + 16 * i + 4 * lg;
+    if (cb >= rows) continue;
+    const int og = cb / g.Cgo, cl = cb - (cb / g.Cgo) * g.Cgo;
+    uint16_t* yb = s_y[og] + cl;
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = (a.bias != nullptr && cl + r < g.Cgo_l) ? a.bias[cl + r] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const long m = m0 + 16 * j + lr;
+      if (m < M) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
+          v[r] = bf2f(f2bf(o));
+          csum[i][r] += v[r];
+          csq[i][r] += v[r] * v[r];
+        }
+        *reinterpret_cast<uint2*>(yb + m * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+  if (a.stat_part != nullptr) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = csum[i][r], q = csq[i][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+        if (lr == 0) { s_stat[wave][0][16 * i + 4 * lg + r] = s; s_stat[wave][1][16 * i + 4 * lg + r] = q; }
+      }
+    __syncthreads();
+    const long blk = (long)blockIdx.x;
+    for (int c = tid; c < 16 * MI; c += 64 * WPX) {
+      const int co = co0 + c;
+      if (co < rows) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < WPX; ++wv) { s += s_stat[wv][0][c]; q += s_stat[wv][1][c]; }
+        a.stat_part[(blk * 2 + 0) * rows + co] = s;
+        a.stat_part[(blk * 2 + 1) * rows + co] = q;
+      }
+    }
+  }
+}
+
+// Weight gradient: dW[co][k] = sum_m dY[m][co] * Xcol[k][m].  The reduction runs over pixels, so
+// both operands need 8 consecutive PIXELS per lane: the block stages a 128-pixel chunk of dY
+// ([128][CO_T]) and of the gathered im2col rows ([128][K_T]) in LDS in their natural NHWC row
+// layout and feeds the MFMA with ds_read_b64_tr_b16 (hardware transpose read, CDNA4).  The next
+// chunk's global loads are issued into registers before the current chunk's MFMAs (register
+// double-buffering).  Each of the 4 waves reduces 32 pixels of a chunk; the waves' partial tiles are
+// summed through LDS, then across pixel splits with fp32 atomics into dW (zeroed by the caller).
+constexpr int WG_M = 128;
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+DEVI uint2 tr_read(const uint16_t* p) {
+  s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t __attribute__((address_space(3)))*)(p));
+  union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
+}
+
+struct WgradPtrs { const uint16_t* dy[kMaxGroups]; const uint16_t* x[kMaxGroups]; };
+
+template <int CO_T, int K_T, bool TRANS>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g, int KT) {
+  constexpr int SA_LD = CO_T + 8, SB_LD = K_T + 8;
+  constexpr int A_CG = CO_T / 8, B_CG = K_T / 8;          // 16-B vectors per row
+  constexpr int A_RS = 256 / A_CG, B_RS = 256 / B_CG;     // row stride between a thread's vectors
+  constexpr int A_V = WG_M / A_RS, B_V = WG_M / B_RS;     // vectors per thread
+  constexpr int FI = CO_T / 16, FJ = K_T / 16;
+  constexpr int LDS_BYTES = WG_M * (SA_LD + SB_LD) * 2;
+  static_assert(LDS_BYTES >= CO_T * K_T * 4, "reduction buffer must fit in the staging LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WG_M * (SA_LD + SB_LD)];
+  uint16_t* sA = smem;
+  uint16_t* sB = smem + WG_M * SA_LD;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k0 = blockIdx.x * K_T;
+  const int co0 = blockIdx.y * CO_T;
+  const int rows = g.Go * g.Cgo;
+  const long OHW = (long)g.OH * g.OW;
+  const long M = (long)g.N * OHW;
+  const long nchunks = (M + WG_M - 1) / WG_M;
+
+  const int a_c8 = tid % A_CG, a_r = tid / A_CG;
+  const int b_c8 = tid % B_CG, b_r = tid / B_CG;
+  const int aco = co0 + 8 * a_c8;
+  const bool a_valid = aco < rows;
+  const int a_g = a_valid ? aco / g.Cgo : 0;
+  const uint16_t* a_base = P.dy[a_g] + (aco - a_g * g.Cgo);
+  const int kk = k0 + 8 * b_c8;
+  const bool b_valid = kk < KT;
+  const KPos bp = kpos_init(b_valid ? kk : 0, g);
+  const int2 btap = make_int2(g.dy[bp.t], g.dx[bp.t]);
+  const uint16_t* b_base = P.x[bp.gi] + bp.cl;
+  const int IHW = g.IH * g.IW;
+
+  uint4 ra[A_V], rb[B_V];
+  auto load = [&](long c) {
+    const long mb = c * WG_M;
+#pragma unroll
+    for (int v = 0; v < A_V; ++v) {
+      const long m = mb + a_r + A_RS * v;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (m < M && a_valid) val = *reinterpret_cast<const uint4*>(a_base + m * g.Cgo);
+      ra[v] = val;
+    }
+#pragma unroll
+    for (int v = 0; v < B_V; ++v) {
+      const long m = mb + b_r + B_RS * v;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (m < M && b_valid) {
+        const int n = (int)(m / OHW);
+        const int r = (int)(m - (long)n * OHW);
+        const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
+        const int pix = TRANS ? in_pixel<true>(n * IHW, oh, ow, btap, g)
+                              : in_pixel<false>(n * IHW, oh * g.stride, ow * g.stride, btap, g);
+        if (pix >= 0) val = *reinterpret_cast<const uint4*>(b_base + (long)pix * g.Cgi);
+      }
+      rb[v] = val;
+    }
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  const int q = lr >> 2, p4 = lr & 3;   // tr-read: lane 4q+p supplies row q, cols 4p..4p+3
+  const int rbase = 32 * wave + 8 * lg;
+
+  long c = blockIdx.z;
+  if (c < nchunks) load(c);
+  for (; c < nchunks; c += gridDim.z) {
+#pragma unroll
+    for (int v = 0; v < A_V; ++v) *reinterpret_cast<uint4*>(&sA[(a_r + A_RS * v) * SA_LD + 8 * a_c8]) = ra[v];
+#pragma unroll
+    for (int v = 0; v < B_V; ++v) *reinterpret_cast<uint4*>(&sB[(b_r + B_RS * v) * SB_LD + 8 * b_c8]) = rb[v];
+    __syncthreads();
+    if (c + gridDim.z < nchunks) load(c + gridDim.z);     // next chunk in flight during the MFMAs
+    uint4 fa[FI];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const uint2 lo = tr_read(&sA[(rbase + q) * SA_LD + 16 * i + 4 * p4]);
+      const uint2 hi = tr_read(&sA[(rbase + 4 + q) * SA_LD + 16 * i + 4 * p4]);
+      fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const uint2 lo = tr_read(&sB[(rbase + q) * SB_LD + 16 * j + 4 * p4]);
+      const uint2 hi = tr_read(&sB[(rbase + 4 + q) * SB_LD + 16 * j + 4 * p4]);
+      const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) acc[i][j] = mfma16x16x32(fa[i], fb, acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  // sequential cross-wave accumulation in LDS (fp32 tile), then one atomic per element
+  float* red = reinterpret_cast<float*>(smem);
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* d = &red[(16 * i + 4 * lg + r) * K_T + 16 * j + lr];
+            *d = (w == 0 ? 0.f : *d) + acc[i][j][r];
+          }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < CO_T * K_T; e += 256) {
+    const int ci = e / K_T, kj = e - (e / K_T) * K_T;
+    const int co = co0 + ci, k = k0 + kj;
+    if (co < rows && (co % g.Cgo) < g.Cgo_l && k < KT) atomicAdd(&dw[(long)co * KT + k], red[e]);
+  }
+}
+
+__global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, int nrow, int nch,
+                                   int T, int Cpk, int Kp, int t_base, int c_base, long s_row, long s_ch) {
+  const long total = (long)nrow * nch * T;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const long rc = i / T;
+    const int c = (int)(rc % nch);
+    const int row = (int)(rc / nch);
+    dst[(long)row * Kp + (t_base + t) * Cpk + c_base + c] = f2bf(src[row * s_row + c * s_ch + t]);
+  }
+}
+
+__global__ void unpack_wgrad_kernel(const float* __restrict__ src, float* __restrict__ dst, int nrow, int nch, int T,
+                                    int Cpk, int Ktot, int t_base, int c_base, long s_row, long s_ch, int accumulate) {
+  const long total = (long)nrow * nch * T;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const long rc = i / T;
+    const int c = (int)(rc % nch);
+    const int row = (int)(rc / nch);
+    const float v = src[(long)row * Ktot + (t_base + t) * Cpk + c_base + c];
+    float* d = dst + row * s_row + c * s_ch + t;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// Batched weight packing: one launch re-packs every conv weight of the model after the optimizer
+// step (jobs = rows of an int64 table; blocks map to jobs through a prefix array).
+constexpr int kPackPerBlock = 2048;
+
+__global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restrict__ jobs, const int* __restrict__ prefix,
+                                                         int njobs) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {   // last job j with prefix[j] <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* J = jobs + 12 * lo;
+  const float* src = reinterpret_cast<const float*>(J[0]);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(J[1]);
+  const int nch = (int)J[3], T = (int)J[4], Cpk = (int)J[5], Kp = (int)J[6];
+  const int t_base = (int)J[7], c_base = (int)J[8];
+  const long s_row = J[9], s_ch = J[10], total = J[11];
+  const long start = (long)(b - prefix[lo]) * kPackPerBlock;
+  for (long i = start + threadIdx.x; i < start + kPackPerBlock && i < total; i += 256) {
+    const int t = (int)(i % T);
+    const long rc = i / T;
+    const int c = (int)(rc % nch);
+    const int row = (int)(rc / nch);
+    dst[(long)row * Kp + (t_base + t) * Cpk + c_base + c] = f2bf(src[row * s_row + c * s_ch + t]);
+  }
+}
+
+template <int MI, int NJ, int WPX, bool TRANS>
+void launch_igemm(const ConvArgs& a, hipStream_t s) {
+  const long M = (long)a.g.N * a.g.OH * a.g.OW;
+  dim3 grid(cdiv(M, 16 * NJ * WPX), cdiv(a.g.Go * a.g.Cgo, 16 * MI));
+  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS>), grid, dim3(64 * WPX), 0, s, a);
+}
+
+template <bool TRANS>
+void dispatch_igemm(const ConvArgs& a, int mi, int wpx, hipStream_t s) {
+#define CASE(MI_, WPX_)                                         \
+  if (mi == MI_ && wpx == WPX_) { launch_igemm<MI_, 4, WPX_, TRANS>(a, s); return; }
+  CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
+  CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
+  CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1)
+#undef CASE
+}
+
+int grid1d(long total) {
+  long b = (total + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+// Tile choice: co tile = 16*MI rows, MI in 1..4, minimising padded MFMA rows + per-tile re-read cost.
+int conv_pick_mi(int rows) {
+  int best = 1;
+  long best_cost = 1L << 60;
+  for (int mi = 1; mi <= 4; ++mi) {
+    const int tiles = cdiv(rows, 16 * mi);
+    const long cost = (long)tiles * 16 * mi + 8L * tiles;
+    if (cost < best_cost) { best_cost = cost; best = mi; }
+  }
+  return best;
+}
+
+int conv_rows_alloc(int rows) { const int mi = conv_pick_mi(rows); return cdiv(rows, 16 * mi) * 16 * mi; }
+
+static int conv_pick_wpx(const ConvGeom& g, int mi) {
+  const long M = (long)g.N * g.OH * g.OW;
+  const long co_tiles = cdiv(g.Go * g.Cgo, 16 * mi);
+  for (int wpx = 4; wpx > 1; wpx >>= 1)
+    if ((long)cdiv(M, 64 * wpx) * co_tiles >= 1024) return wpx;
+  return 1;
+}
+
+long conv_stat_blocks(const ConvGeom& g) {
+  const int mi = conv_pick_mi(g.Go * g.Cgo);
+  const int wpx = conv_pick_wpx(g, mi);
+  const long M = (long)g.N * g.OH * g.OW;
+  return cdiv(M, 64 * wpx);
+}
+
+void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
+  const int mi = conv_pick_mi(a.g.Go * a.g.Cgo);
+  const int wpx = conv_pick_wpx(a.g, mi);
+  if (trans) dispatch_igemm<true>(a, mi, wpx, s);
+  else dispatch_igemm<false>(a, mi, wpx, s);
+}
+
+void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
+                hipStream_t s) {
+  const int KT = g.T * g.Gi * g.Cgi;
+  const int rows = g.Go * g.Cgo;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long nchunks = (M + WG_M - 1) / WG_M;
+  const int co_t = rows <= 32 ? 32 : 64;
+  const int k_t = KT <= 64 ? 64 : 128;
+  const int gx = cdiv(KT, k_t), gy = cdiv(rows, co_t);
+  long target = 2048 / ((long)gx * gy);
+  if (target < 1) target = 1;
+  if (target > nchunks) target = nchunks;
+  WgradPtrs P{};
+  for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
+  for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
+  dim3 grid(gx, gy, (unsigned)target);
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT, s);
+#define WG(CO_, K_)                                                                                  \
+  if (co_t == CO_ && k_t == K_) {                                                                    \
+    if (trans) hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, true>), grid, dim3(256), 0, s, P, dw, g, KT); \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, false>), grid, dim3(256), 0, s, P, dw, g, KT);      \
+    return;                                                                                          \
+  }
+  WG(32, 64) WG(32, 128) WG(64, 64) WG(64, 128)
+#undef WG
+}
+
+void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base, int c_base,
+                 long s_row, long s_ch, hipStream_t s) {
+  const long total = (long)nrow * nch * T;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(grid1d(total)), dim3(256), 0, s, src, dst, nrow, nch, T, Cpk, Kp, t_base,
+                     c_base, s_row, s_ch);
+}
+
+void pack_batch(const int64_t* jobs, const int* prefix, int njobs, int total_blocks, hipStream_t s) {
+  if (njobs <= 0 || total_blocks <= 0) return;
+  hipLaunchKernelGGL(pack_batch_kernel, dim3(total_blocks), dim3(256), 0, s, jobs, prefix, njobs);
+}
+
+int pack_per_block() { return kPackPerBlock; }
+
+void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base, int c_base,
+                  long s_row, long s_ch, bool accumulate, hipStream_t s) {
+  const long total = (long)nrow * nch * T;
+  hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid1d(total)), dim3(256), 0, s, src, dst, nrow, nch, T, Cpk, Ktot,
+                     t_base, c_base, s_row, s_ch, accumulate ? 1 : 0);
+}

@@ -1,0 +1,145 @@
+// Layout conversion and bandwidth-bound glue kernels for NHWC bf16 feature maps (16-B vectors).
+//   nchw_to_nhwc / nhwc_to_nchw : model boundary (fp32 NCHW images / logits <-> internal NHWC bf16)
+//   up2_add / pool2_sum         : DUCKNet decoder `F.interpolate(nearest, 2x) + skip`
+//                                 (reference models/ducknet.py:82-84) and its backward
+//   add_n                       : encoder `x_i + x` merges (ducknet.py:39-43)
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+constexpr int kBlock = 256;
+
+int grid_for(long n) {
+  long b = (n + kBlock - 1) / kBlock;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int N, int C, long HW,
+                                    int Cp) {
+  const int CG = Cp / 8;
+  const long total = (long)N * HW * CG;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int g = (int)(i % CG);
+    const long pix = i / CG;
+    const long n = pix / HW, p = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 8 * g + e;
+      v[e] = c < C ? x[(n * C + c) * HW + p] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(v);
+  }
+}
+
+__global__ void nhwc_to_nchw_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int N, int C, long HW,
+                                    int Cp) {
+  const long total = (long)N * C * HW;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const long p = i % HW;
+    const long nc = i / HW;
+    const int c = (int)(nc % C);
+    const long n = nc / C;
+    y[i] = bf2f(x[(n * HW + p) * Cp + c]);
+  }
+}
+
+__global__ void up2_add_kernel(const uint16_t* __restrict__ low, const uint16_t* __restrict__ skip,
+                               uint16_t* __restrict__ out, int N, int h, int w, int Cp) {
+  const int CG = Cp / 8, H = 2 * h, W = 2 * w;
+  const long total = (long)N * H * W * CG;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int g = (int)(i % CG);
+    long pix = i / CG;
+    const int X = (int)(pix % W);
+    pix /= W;
+    const int Y = (int)(pix % H);
+    const long n = pix / H;
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4*>(skip + i * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(low + ((n * h + (Y >> 1)) * w + (X >> 1)) * Cp + 8 * g), b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += b[e];
+    *reinterpret_cast<uint4*>(out + i * 8) = pack8(a);
+  }
+}
+
+__global__ void pool2_sum_kernel(const uint16_t* __restrict__ gr, uint16_t* __restrict__ out, int N, int h, int w,
+                                 int Cp) {
+  const int CG = Cp / 8, W = 2 * w;
+  const long total = (long)N * h * w * CG;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int g = (int)(i % CG);
+    long pix = i / CG;
+    const int x = (int)(pix % w);
+    pix /= w;
+    const int y = (int)(pix % h);
+    const long n = pix / h;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(gr + ((n * 2 * h + 2 * y + dy) * W + 2 * x + dx) * Cp + 8 * g), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    *reinterpret_cast<uint4*>(out + i * 8) = pack8(acc);
+  }
+}
+
+struct Ptrs { const uint16_t* p[kMaxSumInputs]; };
+
+__global__ void add_n_kernel(Ptrs in, int k, uint16_t* __restrict__ out, long nvec) {
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
+    float a[8];
+    unpack8(*reinterpret_cast<const uint4*>(in.p[0] + i * 8), a);
+    for (int j = 1; j < k; ++j) {
+      float b[8];
+      unpack8(*reinterpret_cast<const uint4*>(in.p[j] + i * 8), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    *reinterpret_cast<uint4*>(out + i * 8) = pack8(a);
+  }
+}
+
+__global__ void scale_f32_kernel(float* __restrict__ x, const float* __restrict__ scalar, float mult, long n) {
+  const float s = (scalar != nullptr ? scalar[0] : 1.f) * mult;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) x[i] *= s;
+}
+}  // namespace
+
+void nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
+  const long total = (long)N * H * W * (Cp / 8);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, x, y, N, C, (long)H * W, Cp);
+}
+
+void nhwc_to_nchw(const uint16_t* x, float* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
+  const long total = (long)N * C * H * W;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, x, y, N, C, (long)H * W, Cp);
+}
+
+void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s) {
+  const long total = (long)N * 4 * h * w * (Cp / 8);
+  hipLaunchKernelGGL(up2_add_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, low, skip, out, N, h, w, Cp);
+}
+
+void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s) {
+  const long total = (long)N * h * w * (Cp / 8);
+  hipLaunchKernelGGL(pool2_sum_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, g, out, N, h, w, Cp);
+}
+
+void add_n(const uint16_t* const* inputs, int k, uint16_t* out, long n_elem, hipStream_t s) {
+  Ptrs in{};
+  for (int i = 0; i < k; ++i) in.p[i] = inputs[i];
+  const long nvec = n_elem / 8;
+  hipLaunchKernelGGL(add_n_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, in, k, out, nvec);
+}
+
+void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s) {
+  hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, x, scalar, mult, n);
+}

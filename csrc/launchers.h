@@ -1,0 +1,103 @@
+// Host-side launch API of the HIP kernels (plain pointers + hipStream_t; no torch types here, so the
+// kernel translation units compile without the PyTorch headers).  bindings.cpp adapts torch tensors.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+constexpr int kMaxTaps = 16;
+
+// Convolution geometry shared by the forward / data-gradient / weight-gradient kernels.
+// Inputs and outputs may be split into up to 8 channel GROUPS, each its own NHWC tensor with the
+// same padded width: the logical input is the channel-concat of Gi tensors of Cgi channels (UNet's
+// torch.cat is never materialised) and the logical output is Go tensors of Cgo channels (Cgo_l of
+// them real): horizontally fused sibling convs write each branch's activation straight into its own
+// tensor, and the data-gradient of such a fused conv reads the branches' gradients in place.
+// Forward:    input pixel of output (oh, ow) for tap t = (oh*stride + dy[t], ow*stride + dx[t]).
+// Transposed: input pixel = ((oh + dy[t]) / stride, (ow + dx[t]) / stride) when divisible.
+constexpr int kMaxGroups = 8;
+struct ConvGeom {
+  int N, IH, IW;
+  int Gi, Cgi;          // input: Gi tensors [N, IH, IW, Cgi]; Cip = Gi*Cgi
+  int OH, OW;
+  int Go, Cgo, Cgo_l;   // output: Go tensors [N, OH, OW, Cgo]; GEMM rows = Go*Cgo
+  int T, Kp;            // taps, packed K (multiple of 32, >= T*Cip)
+  int stride;
+  int dy[kMaxTaps], dx[kMaxTaps];
+};
+
+struct ConvArgs {
+  const uint16_t* x[kMaxGroups];
+  uint16_t* y[kMaxGroups];
+  const uint16_t* w;    // packed [conv_rows_alloc(Go*Cgo)][Kp]
+  const float* bias;    // nullable, [Cgo_l] (Go == 1 only)
+  float* stat_part;     // nullable, [conv_stat_blocks][2][Go*Cgo]
+  ConvGeom g;
+};
+
+// conv.hip
+int conv_pick_mi(int rows);
+int conv_rows_alloc(int rows);
+long conv_stat_blocks(const ConvGeom& g);
+void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
+// dw: fp32 [Go*Cgo][T*Cip] (overwritten)
+void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
+                hipStream_t s);
+// dst[row][(t_base + t)*Cpk + c_base + c] = src[row*s_row + c*s_ch + t], row < nrow, c < nch, t < T
+void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base,
+                 int c_base, long s_row, long s_ch, hipStream_t s);
+// jobs: int64 [njobs][12] = {src, dst, nrow, nch, T, Cpk, Kp, t_base, c_base, s_row, s_ch, nelem};
+// prefix: int32 [njobs] first block of each job (job j owns ceil(nelem/pack_per_block()) blocks)
+void pack_batch(const int64_t* jobs, const int* prefix, int njobs, int total_blocks, hipStream_t s);
+int pack_per_block();
+// dst[row*s_row + c*s_ch + t] (+)= src[row*Ktot + (t_base + t)*Cpk + c_base + c]
+void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base, int c_base,
+                  long s_row, long s_ch, bool accumulate, hipStream_t s);
+
+// bn.hip  (P = number of pixels, Cp = padded channels; partial buffers are [nblk][2][Cp] fp32)
+constexpr int kMaxSumInputs = 8;
+long bn_partial_blocks(long P, int Cp);
+void sum_stats(const uint16_t* const* inputs, int k, uint16_t* out, float* part, long P, int Cp,
+               hipStream_t s);
+// sums[2][Cp] = sum_b part[b][s][col_off + c]; part rows are [2][width]; tmp = fp64 workspace of
+// bn_reduce_splits(nblk) * 2*Cp elements
+int bn_reduce_splits(long nblk);
+void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, float* sums, double* tmp,
+                        hipStream_t s);
+void bn_finalize(const float* sums, int C, int Cp, float count, const float* gamma, const float* beta,
+                 float* running_mean, float* running_var, float momentum, float eps, int training,
+                 float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
+                  int relu, hipStream_t s);
+void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                        const float* mean, float* part, long P, int Cp, int relu, hipStream_t s);
+void bn_bwd_finalize(const float* sums, int C, int Cp, float count, const float* scale,
+                     const float* invstd, const float* mean, float* dgamma, float* dbeta,
+                     float* coef, hipStream_t s);
+void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                      const float* coef, uint16_t* dy, long P, int Cp, int relu, hipStream_t s);
+
+// elementwise.hip
+void nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t s);
+void nhwc_to_nchw(const uint16_t* x, float* y, int N, int C, int H, int W, int Cp, hipStream_t s);
+void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cp,
+             hipStream_t s);
+void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s);
+void add_n(const uint16_t* const* inputs, int k, uint16_t* out, long n_elem, hipStream_t s);
+void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s);
+
+// loss.hip  (logits NCHW fp32 [N, C, HW]; targets int64 [N, HW])
+long ce_blocks(long P);
+void ce_fwd_bwd(const float* logits, const int64_t* target, const float* weight, float* grad,
+                float* pix_loss, float* part, int N, int C, long HW, int ignore_index, hipStream_t s);
+void kd_kl_fwd_bwd(const float* s_logits, const float* t_logits, float* grad, float* part, int N, int C,
+                   long HW, float T, hipStream_t s);
+
+// optim.hip  (flat fp32 buffers; hyper = device fp32 array, see optim.hip for the layout)
+void adam_step(float* p, const float* g, float* m, float* v, const float* hyper, long n, int adamw,
+               hipStream_t s);
+void sgd_step(float* p, const float* g, float* buf, const float* hyper, long n, hipStream_t s);
+void ema_update(float* ema, const float* model, const float* hyper, long n, hipStream_t s);
+
+// metrics.hip
+void confmat_update(const float* logits, const int64_t* target, int64_t* confmat, int N, int C, long HW,
+                    int ignore_index, hipStream_t s);

@@ -1,0 +1,113 @@
+// Fused losses over NCHW fp32 logits (one pass computes the loss partials AND the gradient).
+//   ce_fwd_bwd    : nn.CrossEntropyLoss(weight, ignore_index) with mean reduction; also emits the
+//                   per-pixel loss for OHEM (reference core/loss.py:6-31).
+//   kd_kl_fwd_bwd : F.kl_div(log_softmax(s/T), softmax(t/T)) * T^2, elementwise-mean reduction
+//                   (reference core/loss.py:42-46).
+// Partials are per block ([nblk][2] = {weighted loss sum, weight sum}); the host sums them.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+constexpr int kBlock = 256;
+constexpr int kMaxC = 64;
+
+__global__ __launch_bounds__(kBlock) void ce_kernel(const float* __restrict__ logits, const int64_t* __restrict__ target,
+                                                    const float* __restrict__ weight, float* __restrict__ grad,
+                                                    float* __restrict__ pix_loss, float* __restrict__ part, int N,
+                                                    int C, long HW, int ignore_index) {
+  __shared__ float red[2][kBlock / 64];
+  const long P = (long)N * HW;
+  float ls = 0.f, ws = 0.f;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < P; i += (long)gridDim.x * kBlock) {
+    const long n = i / HW, p = i - n * HW;
+    const float* x = logits + n * C * HW + p;
+    float* gx = grad + n * C * HW + p;
+    const long t = target[i];
+    if (t == ignore_index || t < 0 || t >= C) {
+      for (int c = 0; c < C; ++c) gx[c * HW] = 0.f;
+      if (pix_loss) pix_loss[i] = 0.f;
+      continue;
+    }
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, x[c * HW]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += __expf(x[c * HW] - m);
+    const float lse = m + __logf(se);
+    const float l = lse - x[t * HW];
+    const float w = weight ? weight[t] : 1.f;
+    ls += w * l;
+    ws += w;
+    if (pix_loss) pix_loss[i] = l;
+    const float inv = 1.f / se;
+    for (int c = 0; c < C; ++c) {
+      const float pc = __expf(x[c * HW] - m) * inv;
+      gx[c * HW] = w * (pc - (c == t ? 1.f : 0.f));
+    }
+  }
+  ls = wave_sum(ls);
+  ws = wave_sum(ws);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = ls; red[1][threadIdx.x >> 6] = ws; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < kBlock / 64; ++w) { a += red[0][w]; b += red[1][w]; }
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void kd_kl_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                       float* __restrict__ grad, float* __restrict__ part, int N,
+                                                       int C, long HW, float T) {
+  __shared__ float red[kBlock / 64];
+  const long P = (long)N * HW;
+  const float invT = 1.f / T;
+  const float gscale = T / (float)((double)N * C * HW);
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < P; i += (long)gridDim.x * kBlock) {
+    const long n = i / HW, p = i - n * HW;
+    const float* xs = s + n * C * HW + p;
+    const float* xt = t + n * C * HW + p;
+    float ms = -INFINITY, mt = -INFINITY;
+    for (int c = 0; c < C; ++c) { ms = fmaxf(ms, xs[c * HW] * invT); mt = fmaxf(mt, xt[c * HW] * invT); }
+    float ss = 0.f, st = 0.f;
+    for (int c = 0; c < C; ++c) { ss += __expf(xs[c * HW] * invT - ms); st += __expf(xt[c * HW] * invT - mt); }
+    const float lss = ms + __logf(ss), lst = mt + __logf(st);
+    for (int c = 0; c < C; ++c) {
+      const float lq = xs[c * HW] * invT - lss;   // log q (student)
+      const float lp = xt[c * HW] * invT - lst;   // log p (teacher)
+      const float pc = __expf(lp);
+      acc += pc > 0.f ? pc * (lp - lq) : 0.f;
+      grad[n * C * HW + c * HW + p] = gscale * (__expf(lq) - pc);
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f;
+    for (int w = 0; w < kBlock / 64; ++w) a += red[w];
+    part[blockIdx.x] = a;
+  }
+}
+}  // namespace
+
+long ce_blocks(long P) {
+  long b = (P + kBlock * 8 - 1) / (kBlock * 8);
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return b;
+}
+
+void ce_fwd_bwd(const float* logits, const int64_t* target, const float* weight, float* grad, float* pix_loss,
+                float* part, int N, int C, long HW, int ignore_index, hipStream_t s) {
+  (void)kMaxC;
+  hipLaunchKernelGGL(ce_kernel, dim3(ce_blocks((long)N * HW)), dim3(kBlock), 0, s, logits, target, weight, grad,
+                     pix_loss, part, N, C, HW, ignore_index);
+}
+
+void kd_kl_fwd_bwd(const float* s_logits, const float* t_logits, float* grad, float* part, int N, int C, long HW,
+                   float T, hipStream_t s) {
+  hipLaunchKernelGGL(kd_kl_kernel, dim3(ce_blocks((long)N * HW)), dim3(kBlock), 0, s, s_logits, t_logits, grad,
+                     part, N, C, HW, T);
+}

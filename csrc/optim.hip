@@ -1,0 +1,73 @@
+// Single-launch optimizers and EMA over flat fp32 arenas (all parameters of a model live in one
+// contiguous buffer, so an optimizer step is ONE kernel instead of torch's per-tensor launches).
+// Hyper-parameters are read from DEVICE memory so a hipGraph-captured step picks up the OneCycle
+// lr / momentum values written before each replay.
+//   Adam/AdamW hyper: [lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2, grad_scale]
+//   SGD hyper:        [lr, momentum, weight_decay, grad_scale]
+//   EMA hyper:        [decay]
+// Semantics follow torch.optim.{Adam, AdamW, SGD} (reference utils/optimizer.py:4-21) and
+// ModelEmaV2.update (reference utils/model_ema.py:28-40).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+constexpr int kBlock = 256;
+
+int grid_for(long n) {
+  long b = (n / 4 + kBlock - 1) / kBlock;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, const float* __restrict__ hyper, long n, int adamw) {
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float bc1 = hyper[5], bc2 = hyper[6], gs = hyper[7];
+  const float step = lr / bc1, rbc2 = rsqrtf(bc2);
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) {
+    float pi = p[i];
+    float gi = g[i] * gs;
+    if (!adamw && wd != 0.f) gi += wd * pi;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    if (adamw) pi *= 1.f - lr * wd;
+    const float denom = sqrtf(vi) * rbc2 + eps;
+    p[i] = pi - step * mi / denom;
+  }
+}
+
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                           const float* __restrict__ hyper, long n) {
+  const float lr = hyper[0], mom = hyper[1], wd = hyper[2], gs = hyper[3];
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) {
+    const float pi = p[i];
+    float gi = g[i] * gs + wd * pi;
+    if (mom != 0.f) {
+      gi = mom * buf[i] + gi;
+      buf[i] = gi;
+    }
+    p[i] = pi - lr * gi;
+  }
+}
+
+__global__ void ema_kernel(float* __restrict__ e, const float* __restrict__ m, const float* __restrict__ hyper, long n) {
+  const float d = hyper[0];
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock)
+    e[i] = d * e[i] + (1.f - d) * m[i];
+}
+}  // namespace
+
+void adam_step(float* p, const float* g, float* m, float* v, const float* hyper, long n, int adamw, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, p, g, m, v, hyper, n, adamw);
+}
+
+void sgd_step(float* p, const float* g, float* buf, const float* hyper, long n, hipStream_t s) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, p, g, buf, hyper, n);
+}
+
+void ema_update(float* ema, const float* model, const float* hyper, long n, hipStream_t s) {
+  hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, ema, model, hyper, n);
+}

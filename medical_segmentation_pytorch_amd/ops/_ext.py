@@ -1,0 +1,34 @@
+"""Loader for the in-tree HIP extension ``medical_segmentation_pytorch_amd._C`` (built by
+``csrc/build.py`` / ``__graft_entry__.build()`` for gfx950).
+
+On a GPU box the fused engine REQUIRES the extension: :func:`require` raises instead of silently
+falling back to eager PyTorch, so a missing/stale build can never masquerade as the HIP path.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_C = None
+_ERR = None
+try:
+    from .. import _C  # noqa: F401
+except Exception as e:  # pragma: no cover - depends on build state
+    _ERR = e
+
+
+def available() -> bool:
+    return _C is not None
+
+
+def require():
+    if _C is None:
+        so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_C.so')
+        raise RuntimeError(f'HIP extension not loaded ({so}): {_ERR!r}. Build it with `python csrc/build.py`.')
+    return _C
+
+
+def gpu_ready() -> bool:
+    """True when the fused HIP engine can run (extension built AND a ROCm device present)."""
+    return available() and torch.cuda.is_available()

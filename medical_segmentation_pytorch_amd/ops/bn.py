@@ -1,0 +1,174 @@
+"""BatchNorm(+ReLU) over NHWC bf16 feature maps on the HIP kernels (``csrc/bn.hip``).
+
+``bn_act(xs, bn)`` computes ``act(BN(sum(xs)))`` in training or eval mode with exactly the
+``nn.BatchNorm2d`` semantics of the reference (batch statistics with biased variance for the
+normalisation, running statistics updated with momentum and the unbiased variance; eval uses the
+running statistics).  With a process group it is ``nn.SyncBatchNorm``: the per-channel
+(sum, sum-of-squares) and, in backward, (sum dy, sum dy*xmu) are all-reduced across ranks -- ONE
+RCCL all-reduce of 2*C floats per BN and direction (reference ``utils/parallel.py:37-38`` does an
+all-gather of (mean, invstd, count) per BN via torch's SyncBatchNorm).
+
+Multi-input ``xs`` fuses the residual / branch sums that feed a BN (DUCK's 6-way branch sum,
+``models/ducknet.py:151``; ResidualBlock ``upper + lower``, ``ducknet.py:107``) into the statistics
+pass.  When the producing conv already emitted per-block channel partials (conv stats epilogue),
+the statistics pass is skipped entirely.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ._ext import require
+
+
+@dataclass
+class BNState:
+    C: int
+    weight: Optional[torch.Tensor]
+    bias: Optional[torch.Tensor]
+    running_mean: Optional[torch.Tensor]
+    running_var: Optional[torch.Tensor]
+    momentum: float = 0.1
+    eps: float = 1e-5
+    weight_sink: Optional[torch.Tensor] = None
+    bias_sink: Optional[torch.Tensor] = None
+    group: object = None            # torch.distributed process group for SyncBN (None = local BN)
+    num_batches_tracked: Optional[torch.Tensor] = None
+    count_nbt: bool = True          # False when the engine bumps all counters in one launch
+    ready_hook: Optional[object] = None
+
+    @staticmethod
+    def from_module(bn: torch.nn.modules.batchnorm._BatchNorm, group=None, sinks=None):
+        sinks = sinks or {}
+        return BNState(bn.num_features, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                       bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                       sinks.get(id(bn.weight)) if bn.weight is not None else None,
+                       sinks.get(id(bn.bias)) if bn.bias is not None else None, group,
+                       bn.num_batches_tracked)
+
+
+def _world(group):
+    if group is None or not dist.is_available() or not dist.is_initialized():
+        return 1
+    return dist.get_world_size(group)
+
+
+class _BNAct(torch.autograd.Function):
+    # inputs: st, relu, training, part_info, gamma, beta, *xs  (gamma/beta are inputs so that their
+    # grads reach autograd when the engine gives no grad sink)
+    @staticmethod
+    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, gamma, beta, *xs):
+        C = require()
+        xs = [x.contiguous() for x in xs]
+        y0 = xs[0]
+        Cp = y0.shape[-1]
+        P = y0.numel() // Cp
+        dev = y0.device
+        stats = torch.empty(4, Cp, dtype=torch.float32, device=dev)
+        g_ = gamma.detach() if gamma is not None else None
+        b_ = beta.detach() if beta is not None else None
+        y = torch.empty_like(y0) if len(xs) > 1 else y0
+        if training:
+            sums = torch.empty(2, Cp, dtype=torch.float32, device=dev)
+            if part_info is not None and len(xs) == 1:
+                part, width, col_off = part_info
+                C.bn_reduce_partials(part, part.shape[0], width, col_off, Cp, sums)
+            else:
+                nblk = C.bn_partial_blocks(P, Cp)
+                part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+                C.sum_stats(xs, y if len(xs) > 1 else None, part, P, Cp)
+                C.bn_reduce_partials(part, nblk, Cp, 0, Cp, sums)
+            world = _world(st.group)
+            if world > 1:
+                dist.all_reduce(sums, group=st.group)
+            count = float(P * world)
+            C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
+                          st.eps, True, stats)
+            if st.count_nbt and st.num_batches_tracked is not None:
+                st.num_batches_tracked.add_(1)
+        else:
+            if len(xs) > 1:
+                C.add_n(xs, y)
+            sums = torch.zeros(2, Cp, dtype=torch.float32, device=dev)
+            C.bn_finalize(sums, st.C, Cp, 1.0, g_, b_, st.running_mean, st.running_var, st.momentum,
+                          st.eps, False, stats)
+            count = float(P)
+        z = torch.empty_like(y)
+        C.bn_act_apply(y, stats, z, P, Cp, relu)
+        ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
+        ctx.save_for_backward(y, stats)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        C = require()
+        y, stats = ctx.saved_tensors
+        st: BNState = ctx.st
+        dz = dz.contiguous()
+        Cp = y.shape[-1]
+        P = y.numel() // Cp
+        dev = y.device
+        nblk = C.bn_partial_blocks(P, Cp)
+        part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+        C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
+        sums = torch.empty(2, Cp, dtype=torch.float32, device=dev)
+        C.bn_reduce_partials(part, nblk, Cp, 0, Cp, sums)
+        if ctx.training and _world(st.group) > 1:
+            dist.all_reduce(sums, group=st.group)
+        need_g = ctx.needs_input_grad[4] and st.weight_sink is None
+        need_b = ctx.needs_input_grad[5] and st.bias_sink is None
+        dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
+        dbeta = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_b else None
+        g_t = st.weight_sink if st.weight_sink is not None else dgamma
+        b_t = st.bias_sink if st.bias_sink is not None else dbeta
+        coef = torch.empty(3, Cp, dtype=torch.float32, device=dev)
+        if ctx.training:
+            C.bn_bwd_finalize(sums, st.C, Cp, ctx.count, stats, g_t, b_t, coef)
+        else:
+            # eval-mode BN is a per-channel affine map: dx = dzr * scale
+            coef[0] = stats[0]
+            coef[1:] = 0
+            if g_t is not None:
+                g_t[:st.C] += (sums[1] * stats[3])[:st.C]
+            if b_t is not None:
+                b_t[:st.C] += sums[0][:st.C]
+        dy = torch.empty_like(y)
+        C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+        if st.ready_hook is not None:
+            st.ready_hook([t for t in (st.weight, st.bias) if t is not None])
+        return (None, None, None, None,
+                dgamma[:st.C] if dgamma is not None else None,
+                dbeta[:st.C] if dbeta is not None else None) + (dy,) * ctx.k
+
+
+def bn_act(xs, st: BNState, relu=True, training=True, part_info=None):
+    """act(BN(sum(xs))) for NHWC bf16 feature maps.  ``part_info = (part, width, col_off)`` reuses
+    conv-epilogue channel partials (single input only)."""
+    if isinstance(xs, torch.Tensor):
+        xs = [xs]
+    return _BNAct.apply(st, relu, training, part_info, st.weight, st.bias, *xs)
+
+
+# ------------------------------------------------------------------------------------------------
+def bn_act_reference(xs, st: BNState, relu=True, training=True):
+    """Pure-torch oracle on the same NHWC layout (fp32 math, bf16 output)."""
+    import torch.nn.functional as F
+    if isinstance(xs, torch.Tensor):
+        xs = [xs]
+    y = xs[0].float()
+    for x in xs[1:]:
+        y = y + x.float()
+    if len(xs) > 1:
+        y = y.to(torch.bfloat16).float()
+    Cp = y.shape[-1]
+    yc = y[..., :st.C].reshape(-1, st.C).t().reshape(1, st.C, -1)
+    out = F.batch_norm(yc, st.running_mean, st.running_var, st.weight, st.bias, training, st.momentum, st.eps)
+    if relu:
+        out = torch.relu(out)
+    out = out.reshape(st.C, -1).t().reshape(*y.shape[:-1], st.C)
+    z = torch.zeros(*y.shape[:-1], Cp, dtype=torch.bfloat16, device=y.device)
+    z[..., :st.C] = out.to(torch.bfloat16)
+    return z

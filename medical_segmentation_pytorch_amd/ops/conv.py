@@ -1,0 +1,350 @@
+"""Convolution on the MI355X implicit-GEMM kernels (``csrc/conv.hip``) as an autograd Function.
+
+A :class:`ConvPlan` describes one launch: the tap table (kernel size, stride, padding, dilation),
+the channel grouping of its inputs/outputs, and the list of weight *branches* it multiplies.  One
+branch = one ``nn.Conv2d`` weight.  Several branches that read the same input and share the tap
+grid (the DUCK block's five 3x3 first convs and three 1x1 residual shortcuts,
+reference ``models/ducknet.py:144-149``) are packed into ONE GEMM whose output rows are the
+branches' channels -- each branch's output lands in its own NHWC tensor (``Go`` output groups).
+A 1x1 branch occupies only the centre tap of a 3x3 plan.  Inputs may be a list of tensors that
+are logically channel-concatenated (``Gi`` input groups: UNet's ``torch.cat``).
+
+Weight gradients are written into caller-provided fp32 *sinks* (views into the engine's flat grad
+arena) when given, otherwise returned to autograd as usual.
+
+Reference parity: ``nn.Conv2d`` / ``nn.ConvTranspose2d`` as used in ``models/modules.py:73-108``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ._ext import require
+from .fm import cpad, round_up
+
+
+@dataclass
+class Branch:
+    weight: torch.Tensor            # Conv2d: [co_l, Gi*ci_l, kh_b, kw_b]; ConvTranspose2d: [ci_l, co_l, kh, kw]
+    out_group: int = 0
+    t_base: int = 0
+    T: int = 0
+    sink: Optional[torch.Tensor] = None
+
+
+@dataclass
+class ConvPlan:
+    kh: int
+    kw: int
+    ci_l: int                        # logical channels per input group
+    co_l: int                        # logical channels per output group
+    branches: List[Branch]
+    stride: int = 1
+    padding: tuple = (0, 0)
+    dilation: tuple = (1, 1)
+    Gi: int = 1
+    Go: int = 1
+    transposed: bool = False
+    output_padding: int = 0
+    bias: Optional[torch.Tensor] = None
+    bias_sink: Optional[torch.Tensor] = None
+    ready_hook: Optional[object] = None     # called with the plan's params once their grads are final
+    prepacked: bool = False                 # packed weights kept up to date by a PackProgram
+    wp: Optional[torch.Tensor] = field(default=None, repr=False)
+    wd: Optional[torch.Tensor] = field(default=None, repr=False)
+
+    def __post_init__(self):
+        self.T = self.kh * self.kw
+        self.Cgi = cpad(self.ci_l)
+        self.Cgo = cpad(self.co_l)
+        self.Cip = self.Gi * self.Cgi
+        self.rows = self.Go * self.Cgo
+        self.Kp = round_up(self.T * self.Cip, 32)
+        ph, pw = self.padding
+        dh, dw = self.dilation
+        self.taps_fwd = [(r * dh - ph, s * dw - pw) for r in range(self.kh) for s in range(self.kw)]
+        self.taps_bwd = [(ph - r * dh, pw - s * dw) for r in range(self.kh) for s in range(self.kw)]
+        for b in self.branches:
+            if b.T == 0:
+                b.T = self.T
+        if self.transposed:
+            assert self.Gi == 1 and self.Go == 1 and len(self.branches) == 1
+
+    # -- geometry -------------------------------------------------------------------------------
+    def out_hw(self, ih, iw):
+        ph, pw = self.padding
+        dh, dw = self.dilation
+        s = self.stride
+        if self.transposed:
+            op = self.output_padding
+            return ((ih - 1) * s - 2 * ph + dh * (self.kh - 1) + op + 1,
+                    (iw - 1) * s - 2 * pw + dw * (self.kw - 1) + op + 1)
+        return ((ih + 2 * ph - dh * (self.kh - 1) - 1) // s + 1,
+                (iw + 2 * pw - dw * (self.kw - 1) - 1) // s + 1)
+
+    def fwd_dims(self, n, ih, iw, oh, ow):
+        return [n, ih, iw, self.Gi, self.Cgi, oh, ow, self.Go, self.Cgo, self.co_l, self.T, self.Kp, self.stride]
+
+    def stat_blocks(self, n, ih, iw):
+        oh, ow = self.out_hw(ih, iw)
+        taps = self.taps_bwd if self.transposed else self.taps_fwd
+        return require().conv_stat_blocks(self.fwd_dims(n, ih, iw, oh, ow), [t[0] for t in taps],
+                                          [t[1] for t in taps])
+
+    # -- weight packing ---------------------------------------------------------------------------
+    # A job = (src flat view, dst flat view, nrow, nch, T, Cpk, Kp, t_base, c_base, s_row, s_ch):
+    #   dst[row*Kp + (t_base + t)*Cpk + c_base + c] = bf16(src[row*s_row + c*s_ch + t])
+    def fwd_jobs(self, wp):
+        flat = wp.view(-1)
+        if self.transposed:
+            w = self.branches[0].weight.detach()             # [ci, co, kh, kw]
+            return [(w.reshape(-1), flat, self.co_l, self.ci_l, self.T, self.Cip, self.Kp, 0, 0,
+                     self.T, self.co_l * self.T)]
+        jobs = []
+        cin_tot = self.Gi * self.ci_l
+        for b in self.branches:
+            w = b.weight.detach().reshape(-1)
+            dst = flat[b.out_group * self.Cgo * self.Kp:]
+            for gi in range(self.Gi):
+                jobs.append((w[gi * self.ci_l * b.T:], dst, self.co_l, self.ci_l, b.T, self.Cip, self.Kp,
+                             b.t_base, gi * self.Cgi, cin_tot * b.T, b.T))
+        return jobs
+
+    def dgrad_jobs(self, wd):
+        """Weights of the data-gradient conv: rows = input channels, k = (tap, output channel)."""
+        flat = wd.view(-1)
+        Kp_d = self.Kp_d
+        if self.transposed:
+            w = self.branches[0].weight.detach()             # [ci, co, kh, kw]
+            return [(w.reshape(-1), flat, self.ci_l, self.co_l, self.T, self.rows, Kp_d, 0, 0,
+                     self.co_l * self.T, self.T)]
+        jobs = []
+        cin_tot = self.Gi * self.ci_l
+        for b in self.branches:
+            w = b.weight.detach().reshape(-1)
+            for gi in range(self.Gi):
+                jobs.append((w[gi * self.ci_l * b.T:], flat[gi * self.Cgi * Kp_d:], self.ci_l, self.co_l, b.T,
+                             self.rows, Kp_d, b.t_base, b.out_group * self.Cgo, b.T, cin_tot * b.T))
+        return jobs
+
+    @property
+    def Kp_d(self):
+        return round_up(self.T * self.rows, 32)
+
+    def alloc_fwd(self, device):
+        return torch.zeros(require().conv_rows_alloc(self.rows), self.Kp, dtype=torch.bfloat16, device=device)
+
+    def alloc_dgrad(self, device):
+        return torch.zeros(require().conv_rows_alloc(self.Gi * self.Cgi), self.Kp_d, dtype=torch.bfloat16,
+                           device=device)
+
+    def pack_fwd(self, device):
+        if self.prepacked:
+            return self.wp
+        C = require()
+        wp = self.alloc_fwd(device)
+        for job in self.fwd_jobs(wp):
+            C.pack_weight(*job)
+        return wp
+
+    def pack_dgrad(self, device):
+        if self.prepacked:
+            return self.wd, self.Kp_d
+        C = require()
+        wd = self.alloc_dgrad(device)
+        for job in self.dgrad_jobs(wd):
+            C.pack_weight(*job)
+        return wd, self.Kp_d
+
+
+class PackProgram:
+    """All weight-packing jobs of a set of plans in ONE launch (``pack_batch``); the packed buffers
+    become persistent (zero padding written once) and the plans stop packing per call."""
+
+    def __init__(self, plans, device):
+        C = require()
+        rows, prefix, nblk = [], [], 0
+        per = C.pack_per_block()
+        self.keep = []
+        for p in plans:
+            p.wp = p.alloc_fwd(device)
+            p.wd = p.alloc_dgrad(device)
+            for src, dst, nrow, nch, T, Cpk, Kp, tb, cb, sr, sc in p.fwd_jobs(p.wp) + p.dgrad_jobs(p.wd):
+                n = nrow * nch * T
+                rows.append([src.data_ptr(), dst.data_ptr(), nrow, nch, T, Cpk, Kp, tb, cb, sr, sc, n])
+                prefix.append(nblk)
+                nblk += (n + per - 1) // per
+                self.keep.append(src)
+        self.jobs = torch.tensor(rows, dtype=torch.int64).to(device)
+        self.prefix = torch.tensor(prefix, dtype=torch.int32).to(device)
+        self.blocks = nblk
+        self.plans = list(plans)
+        for p in plans:
+            p.prepacked = True
+
+    def run(self):
+        require().pack_batch(self.jobs, self.prefix, self.blocks)
+
+
+def _taps(tl):
+    return [t[0] for t in tl], [t[1] for t in tl]
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, *args):
+        C = require()
+        xs = [a.contiguous() for a in args[:nx]]
+        n, ih, iw, _ = xs[0].shape
+        oh, ow = plan.out_hw(ih, iw)
+        dev = xs[0].device
+        wp = plan.pack_fwd(dev)
+        ys = [torch.empty(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) for _ in range(plan.Go)]
+        dims = plan.fwd_dims(n, ih, iw, oh, ow)
+        if plan.transposed:
+            dy, dx = _taps(plan.taps_bwd)
+            trans = plan.stride > 1
+        else:
+            dy, dx = _taps(plan.taps_fwd)
+            trans = False
+        part = None
+        if want_stats:
+            nblk = C.conv_stat_blocks(dims, dy, dx)
+            part = torch.empty(nblk, 2, plan.rows, dtype=torch.float32, device=dev)
+        bias = plan.bias.detach().float().contiguous() if plan.bias is not None else None
+        C.conv_fwd(xs, wp, ys, bias, part, dims, dy, dx, trans)
+        ctx.plan = plan
+        ctx.nx = nx
+        ctx.shape = (n, ih, iw, oh, ow)
+        ctx.save_for_backward(*xs)
+        if part is None:
+            part = torch.empty(0, device=dev)
+        ctx.mark_non_differentiable(part)
+        return (*ys, part)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        C = require()
+        plan: ConvPlan = ctx.plan
+        xs = list(ctx.saved_tensors)
+        n, ih, iw, oh, ow = ctx.shape
+        dev = xs[0].device
+        gys = []
+        for g in grads[:plan.Go]:
+            gys.append(torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None
+                       else g.contiguous())
+        dxs = [None] * ctx.nx
+        if any(ctx.needs_input_grad[3:3 + ctx.nx]):
+            wd, Kp_d = plan.pack_dgrad(dev)
+            dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
+            dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
+            if plan.transposed:
+                dy, dx = _taps(plan.taps_fwd)
+                trans = False
+            else:
+                dy, dx = _taps(plan.taps_bwd)
+                trans = plan.stride > 1
+            C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
+        wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev)
+        bgrad = None
+        if plan.bias is not None:
+            bg = gys[0].view(-1, plan.Cgo)[:, :plan.co_l].float().sum(0)
+            if plan.bias_sink is not None:
+                plan.bias_sink.add_(bg)
+            else:
+                bgrad = bg
+        if plan.ready_hook is not None:
+            plan.ready_hook([b.weight for b in plan.branches] + ([plan.bias] if plan.bias is not None else []))
+        # inputs of forward: plan, want_stats, nx, *xs, *weights, bias
+        out = [None, None, None] + dxs + wgrads
+        if plan.bias is not None:
+            out.append(bgrad)
+        return tuple(out)
+
+
+def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
+    C = require()
+    n, ih, iw, oh, ow = shape
+    res = []
+    need = [b.weight.requires_grad for b in plan.branches]
+    if not any(need):
+        return [None] * len(plan.branches)
+    if plan.transposed:
+        b = plan.branches[0]
+        # dW[ci][co][t] = sum_i X[i][ci] * dY[i*S + r*d - p][co]: the X tensor plays the "output" role
+        Kp_w = round_up(plan.T * plan.Cgo, 32)
+        dims = [n, oh, ow, 1, plan.Cgo, ih, iw, 1, plan.Cgi, plan.ci_l, plan.T, Kp_w, plan.stride]
+        dy, dx = _taps(plan.taps_fwd)
+        dwp = torch.empty(plan.Cgi * plan.T * plan.Cgo, dtype=torch.float32, device=dev)
+        C.conv_wgrad(xs, gys, dwp, dims, dy, dx, False)
+        dst = b.sink if b.sink is not None else torch.zeros_like(b.weight, dtype=torch.float32)
+        C.unpack_wgrad(dwp, dst.view(-1), plan.ci_l, plan.co_l, plan.T, plan.Cgo, plan.T * plan.Cgo, 0, 0,
+                       plan.co_l * plan.T, plan.T, True)
+        return [None if b.sink is not None else dst]
+    dims = plan.fwd_dims(n, ih, iw, oh, ow)
+    dy, dx = _taps(plan.taps_fwd)
+    KT = plan.T * plan.Cip
+    dwp = torch.empty(plan.rows * KT, dtype=torch.float32, device=dev)
+    C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False)
+    cin_tot = plan.Gi * plan.ci_l
+    for b, nd in zip(plan.branches, need):
+        if not nd:
+            res.append(None)
+            continue
+        dst = b.sink if b.sink is not None else torch.zeros_like(b.weight, dtype=torch.float32)
+        src = dwp[b.out_group * plan.Cgo * KT:]
+        flat = dst.view(-1)
+        for gi in range(plan.Gi):
+            C.unpack_wgrad(src, flat[gi * plan.ci_l * b.T:], plan.co_l, plan.ci_l, b.T, plan.Cip, KT, b.t_base,
+                           gi * plan.Cgi, cin_tot * b.T, b.T, True)
+        res.append(None if b.sink is not None else dst)
+    return res
+
+
+def conv(plan: ConvPlan, xs, want_stats=False):
+    """Run ``plan`` on input group tensors ``xs``; returns (list of Go output tensors, stat partials)."""
+    if isinstance(xs, torch.Tensor):
+        xs = [xs]
+    assert len(xs) == plan.Gi
+    weights = [b.weight for b in plan.branches]
+    extra = [plan.bias] if plan.bias is not None else []
+    out = _ConvFn.apply(plan, want_stats, len(xs), *xs, *weights, *extra)
+    return list(out[:plan.Go]), (out[plan.Go] if want_stats else None)
+
+
+# ------------------------------------------------------------------------------------------------
+# Pure-PyTorch reference of the same plan (NHWC padded bf16 in/out), used by CPU tests and as the
+# numerics oracle for the GPU kernel tests.
+def conv_reference(plan: ConvPlan, xs, dtype=torch.float32):
+    import torch.nn.functional as F
+    if isinstance(xs, torch.Tensor):
+        xs = [xs]
+    x = torch.cat([t[..., :plan.ci_l] for t in xs], dim=-1).permute(0, 3, 1, 2).to(dtype)
+    outs = []
+    if plan.transposed:
+        w = plan.branches[0].weight.to(dtype)
+        b = plan.bias.to(dtype) if plan.bias is not None else None
+        y = F.conv_transpose2d(x, w, b, plan.stride, plan.padding, plan.output_padding, 1, plan.dilation)
+        outs.append(y)
+    else:
+        by_group = {}
+        for br in plan.branches:
+            w = br.weight.to(dtype)
+            if br.T != plan.T:   # 1x1 branch at the centre tap of a larger grid
+                full = torch.zeros(w.shape[0], w.shape[1], plan.kh, plan.kw, dtype=dtype, device=w.device)
+                r, s = divmod(br.t_base, plan.kw)
+                full[:, :, r, s] = w[:, :, 0, 0]
+                w = full
+            b = plan.bias.to(dtype) if plan.bias is not None else None
+            y = F.conv2d(x, w, b, plan.stride, plan.padding, plan.dilation)
+            by_group[br.out_group] = y
+        outs = [by_group[g] for g in range(plan.Go)]
+    res = []
+    for y in outs:
+        n, c, h, w_ = y.shape
+        o = torch.zeros(n, h, w_, plan.Cgo, dtype=torch.bfloat16, device=y.device)
+        o[..., :c] = y.permute(0, 2, 3, 1).to(torch.bfloat16)
+        res.append(o)
+    return res

@@ -1,0 +1,107 @@
+"""Layout conversion and glue ops on the HIP kernels (``csrc/elementwise.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from ._ext import require
+from .fm import cpad
+
+
+class _ToFM(torch.autograd.Function):
+    """NCHW fp32 -> NHWC bf16 padded (model input boundary)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        C = require()
+        x = x.contiguous().float()
+        n, c, h, w = x.shape
+        y = torch.empty(n, h, w, cpad(c), dtype=torch.bfloat16, device=x.device)
+        C.nchw_to_nhwc(x, y, cpad(c))
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        n, c, h, w = ctx.shape
+        out = torch.empty(n, c, h, w, dtype=torch.float32, device=g.device)
+        C.nhwc_to_nchw(g.contiguous(), out, cpad(c))
+        return out
+
+
+class _FromFM(torch.autograd.Function):
+    """NHWC bf16 padded -> NCHW fp32 with ``c`` logical channels (logits boundary)."""
+
+    @staticmethod
+    def forward(ctx, fm, c):
+        C = require()
+        fm = fm.contiguous()
+        n, h, w, cp = fm.shape
+        out = torch.empty(n, c, h, w, dtype=torch.float32, device=fm.device)
+        C.nhwc_to_nchw(fm, out, cp)
+        ctx.cp = cp
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        g = g.contiguous().float()
+        n, c, h, w = g.shape
+        out = torch.empty(n, h, w, ctx.cp, dtype=torch.bfloat16, device=g.device)
+        C.nchw_to_nhwc(g, out, ctx.cp)
+        return out, None
+
+
+class _Up2Add(torch.autograd.Function):
+    """nearest-2x(low) + skip  (reference models/ducknet.py:82-84)."""
+
+    @staticmethod
+    def forward(ctx, low, skip):
+        C = require()
+        low, skip = low.contiguous(), skip.contiguous()
+        n, h, w, cp = low.shape
+        assert skip.shape == (n, 2 * h, 2 * w, cp), (low.shape, skip.shape)
+        out = torch.empty_like(skip)
+        C.up2_add(low, skip, out, n, h, w, cp)
+        ctx.shape = (n, h, w, cp)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        n, h, w, cp = ctx.shape
+        g = g.contiguous()
+        dlow = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=g.device)
+        C.pool2_sum(g, dlow, n, h, w, cp)
+        return dlow, g
+
+
+class _AddN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        C = require()
+        xs = [x.contiguous() for x in xs]
+        out = torch.empty_like(xs[0])
+        C.add_n(xs, out)
+        ctx.k = len(xs)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g,) * ctx.k
+
+
+def to_fm(x):
+    return _ToFM.apply(x)
+
+
+def from_fm(fm, c):
+    return _FromFM.apply(fm, c)
+
+
+def up2_add(low, skip):
+    return _Up2Add.apply(low, skip)
+
+
+def add_n(*xs):
+    return xs[0] if len(xs) == 1 else _AddN.apply(*xs)

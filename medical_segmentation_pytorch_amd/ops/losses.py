@@ -1,0 +1,101 @@
+"""Fused loss kernels (``csrc/loss.hip``) as autograd Functions over NCHW fp32 logits.
+
+* :func:`cross_entropy` == ``nn.CrossEntropyLoss(weight, ignore_index, reduction='mean')``
+  (reference ``core/loss.py:30-31``): one kernel computes the loss partials and d(loss)/d(logits);
+  backward is a scalar rescale, no second pass over the logits.
+* :func:`ohem_cross_entropy` == reference ``OhemCELoss`` (``core/loss.py:6-20``): the per-pixel
+  losses come from the same fused kernel; selection (threshold, top-k fallback) uses torch.
+* :func:`kd_kl_div` == ``F.kl_div(log_softmax(s/T), softmax(t/T)) * T**2`` with the default
+  elementwise-mean reduction (reference ``core/loss.py:42-46``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._ext import require
+
+
+class _CE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, weight, ignore_index):
+        C = require()
+        logits = logits.contiguous().float()
+        target = target.contiguous().long()
+        n, c, h, w = logits.shape
+        grad = torch.empty_like(logits)
+        part = torch.empty(C.ce_blocks(n * h * w), 2, dtype=torch.float32, device=logits.device)
+        C.ce_fwd_bwd(logits, target, weight, grad, None, part, ignore_index)
+        tot = part.sum(0)
+        ctx.save_for_backward(grad, tot)
+        return tot[0] / tot[1]
+
+    @staticmethod
+    def backward(ctx, g):
+        grad, tot = ctx.saved_tensors
+        return grad * (g / tot[1]), None, None, None
+
+
+def cross_entropy(logits, target, weight=None, ignore_index=255):
+    if weight is not None:
+        weight = weight.to(device=logits.device, dtype=torch.float32).contiguous()
+    return _CE.apply(logits, target, weight, ignore_index)
+
+
+class _OHEM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, thresh, ignore_index):
+        C = require()
+        logits = logits.contiguous().float()
+        target = target.contiguous().long()
+        n, c, h, w = logits.shape
+        grad = torch.empty_like(logits)
+        pix = torch.empty(n * h * w, dtype=torch.float32, device=logits.device)
+        part = torch.empty(C.ce_blocks(n * h * w), 2, dtype=torch.float32, device=logits.device)
+        C.ce_fwd_bwd(logits, target, None, grad, pix, part, ignore_index)
+        n_min = int((target != ignore_index).sum().item()) // 16
+        sel = pix > thresh
+        if int(sel.sum().item()) < n_min:
+            _, idx = pix.topk(n_min)
+            sel = torch.zeros_like(sel)
+            sel[idx] = True
+        cnt = sel.sum().clamp_min(1).float()
+        loss = (pix * sel).sum() / cnt
+        ctx.save_for_backward(grad, sel, cnt)
+        ctx.hw = (n, h * w)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        grad, sel, cnt = ctx.saved_tensors
+        n, hw = ctx.hw
+        mask = sel.view(n, 1, hw).float() * (g / cnt)
+        return grad * mask.view(n, 1, *grad.shape[2:]), None, None, None
+
+
+def ohem_cross_entropy(logits, target, thresh=0.7, ignore_index=255):
+    return _OHEM.apply(logits, target, -math.log(thresh), ignore_index)
+
+
+class _KDKL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t, T):
+        C = require()
+        s = s.contiguous().float()
+        t = t.detach().contiguous().float()
+        grad = torch.empty_like(s)
+        n, c, h, w = s.shape
+        part = torch.empty(C.ce_blocks(n * h * w), dtype=torch.float32, device=s.device)
+        C.kd_kl_fwd_bwd(s, t, grad, part, T)
+        ctx.save_for_backward(grad)
+        return part.sum() * (T * T) / s.numel()
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None, None
+
+
+def kd_kl_div(student, teacher, T=4.0):
+    return _KDKL.apply(student, teacher, float(T))

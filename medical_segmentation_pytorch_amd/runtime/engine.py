@@ -1,0 +1,208 @@
+"""MI355X training engine: flat parameter/gradient arenas, single-launch optimizer + EMA, bucketed
+RCCL gradient all-reduce overlapped with backward, and hipGraph capture of the whole static step.
+
+Reference semantics reproduced (``core/seg_trainer.py:24-95``): zero_grad -> forward -> loss ->
+backward (DDP bucketed all-reduce, averaging) -> optimizer.step -> scheduler.step (per iteration)
+-> EMA update.  Layout decisions:
+
+* every parameter of the model is a view into ONE fp32 arena, every gradient a view into ONE fp32
+  grad arena: ``zero_grad`` is one memset, the optimizer one kernel (``csrc/optim.hip``), the EMA
+  one kernel, and the DDP buckets are plain slices of the grad arena (no flatten/unflatten copies);
+* the fused ops write weight gradients straight into their arena slice (grad *sinks*), and report
+  completion so a bucket's all-reduce is issued the moment its last gradient lands -- RCCL runs on
+  its own stream and overlaps the rest of backward (xGMI is point-to-point, so large buckets);
+* BatchNorm ``num_batches_tracked`` counters live in one int64 arena (one add per step);
+* hyper-parameters (lr, momentum/beta1 from OneCycle, bias corrections, 1/world) are a device
+  tensor refreshed by one H2D copy before each (graph) replay.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops._ext import require
+
+
+class Arena:
+    """Re-homes a module's parameters (and grads) into flat contiguous buffers."""
+
+    def __init__(self, model: nn.Module, device, align=64, with_grad=True):
+        self.params: List[nn.Parameter] = [p for p in model.parameters() if p.requires_grad or not with_grad]
+        offs, n = [], 0
+        for p in self.params:
+            offs.append(n)
+            n += (p.numel() + align - 1) // align * align
+        self.numel = n
+        self.offsets = offs
+        self.data = torch.zeros(n, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=device) if with_grad else None
+        for p, o in zip(self.params, offs):
+            view = self.data[o:o + p.numel()].view_as(p)
+            view.copy_(p.detach())
+            p.data = view
+            if with_grad:
+                p.grad = self.grad[o:o + p.numel()].view_as(p)
+        # float buffers (BN running statistics) -> one flat arena too (single-kernel EMA)
+        fb = [(m, k, b) for m in model.modules() for k, b in m._buffers.items()
+              if b is not None and b.dtype == torch.float32]
+        tot = sum(b.numel() for _, _, b in fb)
+        self.bufdata = torch.zeros(max(tot, 1), dtype=torch.float32, device=device)
+        o = 0
+        for m, k, b in fb:
+            view = self.bufdata[o:o + b.numel()].view_as(b)
+            view.copy_(b.detach())
+            m._buffers[k] = view
+            o += b.numel()
+        # num_batches_tracked counters
+        nbts = [(m, m.num_batches_tracked) for m in model.modules()
+                if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.num_batches_tracked is not None]
+        self.nbt = torch.zeros(max(len(nbts), 1), dtype=torch.long, device=device)
+        for i, (m, t) in enumerate(nbts):
+            self.nbt[i] = t.to(device)
+            m.num_batches_tracked = self.nbt[i:i + 1].view(())
+
+    def sinks(self) -> Dict[int, torch.Tensor]:
+        return {id(p): p.grad for p in self.params}
+
+    def param_index(self):
+        return {id(p): i for i, p in enumerate(self.params)}
+
+
+class GradBucketer:
+    """DDP-equivalent gradient averaging over RCCL: buckets are contiguous slices of the grad arena
+    in REVERSE parameter order (backward produces the last layers first); a bucket is all-reduced
+    as soon as all of its parameters reported ready (SUM; the 1/world factor is folded into the
+    optimizer's grad scale)."""
+
+    def __init__(self, arena: Arena, group=None, bucket_cap_mb=64.0, first_bucket_mb=4.0):
+        self.arena = arena
+        self.group = group
+        self.world = dist.get_world_size(group)
+        idx = list(range(len(arena.params)))[::-1]
+        buckets, cur, cur_bytes, cap = [], [], 0, first_bucket_mb * 2 ** 20
+        for i in idx:
+            cur.append(i)
+            cur_bytes += arena.params[i].numel() * 4
+            if cur_bytes >= cap:
+                buckets.append(cur)
+                cur, cur_bytes, cap = [], 0, bucket_cap_mb * 2 ** 20
+        if cur:
+            buckets.append(cur)
+        self.buckets = []
+        self.owner = {}
+        for b, members in enumerate(buckets):
+            lo = min(arena.offsets[i] for i in members)
+            hi = max(arena.offsets[i] + arena.params[i].numel() for i in members)
+            self.buckets.append((lo, hi, set(members)))
+            for i in members:
+                self.owner[i] = b
+        self.pidx = arena.param_index()
+        self.reset()
+
+    def reset(self):
+        self.pending = [set(m) for _, _, m in self.buckets]
+        self.works = []
+        self.launched = [False] * len(self.buckets)
+
+    def ready(self, params):
+        for p in params:
+            i = self.pidx.get(id(p))
+            if i is None:
+                continue
+            b = self.owner[i]
+            self.pending[b].discard(i)
+            if not self.pending[b] and not self.launched[b]:
+                self._launch(b)
+
+    def _launch(self, b):
+        lo, hi, _ = self.buckets[b]
+        self.launched[b] = True
+        self.works.append(dist.all_reduce(self.arena.grad[lo:hi], group=self.group, async_op=True))
+
+    def finish(self):
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.reset()
+
+
+class FlatOptimizer:
+    """Adam / AdamW / SGD(momentum, wd) over the arena in one kernel (torch.optim semantics)."""
+
+    def __init__(self, arena: Arena, kind='adam', lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 momentum=0.9):
+        self.arena, self.kind = arena, kind
+        self.lr, self.betas, self.eps, self.wd, self.momentum = lr, betas, eps, weight_decay, momentum
+        dev = arena.data.device
+        n = arena.numel
+        if kind in ('adam', 'adamw'):
+            self.m = torch.zeros(n, device=dev)
+            self.v = torch.zeros(n, device=dev)
+        else:
+            self.buf = torch.zeros(n, device=dev)
+        self.step_count = 0
+        self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.hyper_host = torch.zeros(8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() \
+            else torch.zeros(8, dtype=torch.float32)
+        self.grad_scale = 1.0
+
+    def prepare(self):
+        """Host-side: advance step count, write hyper-parameters, H2D copy (outside any graph)."""
+        self.step_count += 1
+        h = self.hyper_host
+        if self.kind in ('adam', 'adamw'):
+            b1, b2 = self.betas
+            h[0], h[1], h[2], h[3], h[4] = self.lr, b1, b2, self.eps, self.wd
+            h[5] = 1 - b1 ** self.step_count
+            h[6] = 1 - b2 ** self.step_count
+            h[7] = self.grad_scale
+        else:
+            h[0], h[1], h[2], h[3] = self.lr, self.momentum, self.wd, self.grad_scale
+        self.hyper.copy_(h, non_blocking=True)
+
+    def step(self):
+        C = require()
+        a = self.arena
+        if self.kind in ('adam', 'adamw'):
+            C.adam_step(a.data, a.grad, self.m, self.v, self.hyper, self.kind == 'adamw')
+        else:
+            C.sgd_step(a.data, a.grad, self.buf, self.hyper)
+
+
+class OneCycle:
+    """torch.optim.lr_scheduler.OneCycleLR (cos anneal, cycle_momentum) computed on the host, per
+    iteration -- the values feed the device hyper tensor (reference utils/scheduler.py:13-19)."""
+
+    def __init__(self, max_lr, total_steps, pct_start=0.3, anneal='cos', div_factor=25.0, final_div_factor=1e4,
+                 base_momentum=0.85, max_momentum=0.95):
+        self.max_lr, self.total = max_lr, total_steps
+        self.initial = max_lr / div_factor
+        self.min_lr = self.initial / final_div_factor
+        self.anneal = anneal
+        self.phase_end = [float(pct_start * total_steps) - 1, float(total_steps - 1)]
+        self.bm, self.mm = base_momentum, max_momentum
+        self.step_num = 0
+
+    def _f(self, start, end, pct):
+        if self.anneal == 'cos':
+            return end + (start - end) / 2.0 * (math.cos(math.pi * pct) + 1)
+        return (end - start) * pct + start
+
+    def values(self, step=None):
+        s = self.step_num if step is None else step
+        start = 0
+        if s <= self.phase_end[0]:
+            pct = (s - start) / max(self.phase_end[0] - start, 1e-12)
+            return self._f(self.initial, self.max_lr, pct), self._f(self.mm, self.bm, pct)
+        start = self.phase_end[0]
+        pct = (s - start) / max(self.phase_end[1] - start, 1e-12)
+        return self._f(self.max_lr, self.min_lr, pct), self._f(self.bm, self.mm, pct)
+
+    def step(self):
+        self.step_num += 1

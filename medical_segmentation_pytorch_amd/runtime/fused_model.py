@@ -1,0 +1,239 @@
+"""Fused MI355X executor for the model families: walks the reference-shaped ``nn.Module`` tree and
+drives the HIP kernels with the modules' own parameters (so ``state_dict`` / checkpoints are the
+reference's), keeping every activation NHWC bf16 on the device.
+
+What is fused relative to the module graph (reference ``models/ducknet.py``, ``models/unet.py``):
+  * every ConvBNAct = 1 implicit-GEMM conv launch whose epilogue emits the BN channel partials,
+    + finalize + one normalize/ReLU pass (no separate statistics read);
+  * DUCK (``ducknet.py:113-154``): the five 3x3 first convs and the three 1x1 residual shortcuts
+    that all read ``in_bn(x)`` are ONE GEMM with 8 output groups (Cout = 8*C), so the input is read
+    once and the data-gradient of all eight is a single launch that sums them for free;
+  * ResidualBlock (``ducknet.py:90-110``): the 1x1 shortcut rides in the first 3x3 conv's launch,
+    and ``bn(upper + lower)`` sums inside the BN statistics pass;
+  * DUCK's 6-way branch sum + ``out_bn`` is one statistics pass over six inputs;
+  * decoder ``interpolate(nearest) + skip`` is one kernel; UNet's ``torch.cat`` is never built (the
+    conv reads both tensors as channel groups).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops.bn import BNState, bn_act
+from ..ops.conv import Branch, ConvPlan, PackProgram, conv
+from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
+
+
+def _is_relu(act_mod):
+    inner = getattr(act_mod, 'activation', act_mod)
+    if isinstance(inner, nn.ReLU):
+        return True
+    if isinstance(inner, nn.Identity):
+        return False
+    raise NotImplementedError(f'fused engine supports ReLU/Identity activations, got {inner}')
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+class FusedExecutor:
+    """Holds per-module plans/BN states; ``forward(model, images)`` returns NCHW fp32 logits."""
+
+    def __init__(self, model: nn.Module, group=None, sinks=None, count_nbt=True, ready_hook=None):
+        self.model = model
+        self.group = group
+        self.sinks = sinks or {}
+        self.count_nbt = count_nbt
+        self.ready_hook = ready_hook
+        self._plans = {}
+        self._bns = {}
+        self.pack_program = None
+
+    def build_pack_program(self, device):
+        """After one forward created every plan: pack all weights in one launch per step."""
+        self.pack_program = PackProgram(list(self._plans.values()), device)
+        return self.pack_program
+
+    def repack(self):
+        if self.pack_program is not None:
+            self.pack_program.run()
+
+    # -- caches -------------------------------------------------------------------------------------
+    def bn(self, m):
+        st = self._bns.get(id(m))
+        if st is None:
+            st = BNState.from_module(m, self.group, self.sinks)
+            st.count_nbt = self.count_nbt
+            st.ready_hook = self.ready_hook
+            self._bns[id(m)] = st
+        return st
+
+    def _branch(self, conv_mod, out_group=0, t_base=0):
+        kh, kw = _pair(conv_mod.kernel_size)
+        return Branch(conv_mod.weight, out_group, t_base, kh * kw, self.sinks.get(id(conv_mod.weight)))
+
+    def plan_conv(self, c: nn.Conv2d, gi=1):
+        key = ('c', id(c), gi)
+        p = self._plans.get(key)
+        if p is None:
+            kh, kw = _pair(c.kernel_size)
+            assert c.groups == 1, 'grouped/depthwise conv not in the fused engine yet'
+            p = ConvPlan(kh, kw, c.in_channels // gi, c.out_channels, [self._branch(c)], stride=_pair(c.stride)[0],
+                         padding=_pair(c.padding), dilation=_pair(c.dilation), Gi=gi, bias=c.bias,
+                         bias_sink=self.sinks.get(id(c.bias)) if c.bias is not None else None,
+                         ready_hook=self.ready_hook)
+            self._plans[key] = p
+        return p
+
+    def plan_deconv(self, c: nn.ConvTranspose2d):
+        key = ('t', id(c))
+        p = self._plans.get(key)
+        if p is None:
+            kh, kw = _pair(c.kernel_size)
+            p = ConvPlan(kh, kw, c.in_channels, c.out_channels,
+                         [Branch(c.weight, 0, 0, kh * kw, self.sinks.get(id(c.weight)))],
+                         stride=_pair(c.stride)[0], padding=_pair(c.padding), dilation=_pair(c.dilation),
+                         transposed=True, output_padding=_pair(c.output_padding)[0], bias=c.bias,
+                         bias_sink=self.sinks.get(id(c.bias)) if c.bias is not None else None,
+                         ready_hook=self.ready_hook)
+            self._plans[key] = p
+        return p
+
+    def plan_fused3x3(self, key, convs3, convs1):
+        """One 3x3/d1/p1 GEMM over sibling convs reading the same input: 3x3 convs first, then 1x1
+        convs at the centre tap.  Output group order = convs3 + convs1."""
+        p = self._plans.get(key)
+        if p is None:
+            c0 = convs3[0]
+            branches = [self._branch(c, g, 0) for g, c in enumerate(convs3)]
+            branches += [self._branch(c, len(convs3) + g, 4) for g, c in enumerate(convs1)]
+            for c in convs3:
+                assert _pair(c.kernel_size) == (3, 3) and _pair(c.dilation) == (1, 1) and _pair(c.stride) == (1, 1)
+            for c in convs1:
+                assert _pair(c.kernel_size) == (1, 1) and c.bias is None
+            p = ConvPlan(3, 3, c0.in_channels, c0.out_channels, branches, stride=1, padding=(1, 1),
+                         dilation=(1, 1), Go=len(branches), ready_hook=self.ready_hook)
+            self._plans[key] = p
+        return p
+
+    # -- blocks -------------------------------------------------------------------------------------
+    def cba(self, m, xs, training):
+        """ConvBNAct: Sequential(conv, BN, act)."""
+        if isinstance(xs, torch.Tensor):
+            xs = [xs]
+        plan = self.plan_conv(m[0], gi=len(xs))
+        (y,), part = conv(plan, xs, want_stats=training)
+        return bn_act([y], self.bn(m[1]), _is_relu(m[2]), training,
+                      (part, plan.rows, 0) if training else None)
+
+    def bn_from_group(self, bn_mod, act, ys, part, plan, g, training):
+        return bn_act([ys[g]], self.bn(bn_mod), _is_relu(act), training,
+                      (part, plan.rows, g * plan.Cgo) if training else None)
+
+    def residual(self, m, x, training):
+        plan = self.plan_fused3x3(('res', id(m)), [m.lower_branch[0][0]], [m.upper_branch])
+        ys, part = conv(plan, [x], want_stats=training)
+        low = self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0, training)
+        low = self.cba(m.lower_branch[1], low, training)
+        return bn_act([ys[1], low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training)
+
+    def _residual_tail(self, m, upper_y, low_z, training):
+        low = self.cba(m.lower_branch[1], low_z, training)
+        return bn_act([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training)
+
+    def duck(self, m, x, training):
+        xb = bn_act([x], self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training)
+        b1, b2, b3, b4, b5, b6 = m.branches()
+        r4, r5 = b4[0], b5[0]
+        convs3 = [b1[0][0], b2[0][0], b3.lower_branch[0][0], r4.lower_branch[0][0], r5.lower_branch[0][0]]
+        convs1 = [b3.upper_branch, r4.upper_branch, r5.upper_branch]
+        plan = self.plan_fused3x3(('duck', id(m)), convs3, convs1)
+        ys, part = conv(plan, [xb], want_stats=training)
+        bnz = lambda seq, g: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training)  # noqa: E731
+        # widescope: d1 -> d2 -> d3 ; midscope: d1 -> d2
+        o1 = bnz(b1[0], 0)
+        o1 = self.cba(b1[1], o1, training)
+        o1 = self.cba(b1[2], o1, training)
+        o2 = bnz(b2[0], 1)
+        o2 = self.cba(b2[1], o2, training)
+        # residual x1 / x2 / x3 (first block's two convs come from the fused launch)
+        o3 = self._residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training)
+        o4 = self._residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training)
+        for blk in list(b4)[1:]:
+            o4 = self.residual(blk, o4, training)
+        o5 = self._residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training)
+        for blk in list(b5)[1:]:
+            o5 = self.residual(blk, o5, training)
+        # separated 1x7 -> 7x1
+        o6 = self.cba(b6[0], xb, training)
+        o6 = self.cba(b6[1], o6, training)
+        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training)
+
+    def head(self, conv_mod, x, num_class):
+        plan = self.plan_conv(conv_mod)
+        (y,), _ = conv(plan, [x], want_stats=False)
+        return from_fm(y, num_class)
+
+    # -- models -------------------------------------------------------------------------------------
+    def ducknet(self, model, images, training):
+        x = to_fm(images)
+        stages = model.down_stages()
+        s1 = stages[0]
+        shortcut = self.cba(s1.conv2, x, training)
+        skip = self.duck(s1.duck, x, training)
+        down = self.cba(s1.conv1, skip, training)
+        skips = [skip]
+        for st in stages[1:]:
+            x1 = add_n(down, shortcut)
+            shortcut = self.cba(st.conv2, shortcut, training)
+            skip = self.duck(st.duck, x1, training)
+            down = self.cba(st.conv1, skip, training)
+            skips.append(skip)
+        x = add_n(down, shortcut)
+        for blk in model.mid_stage:
+            x = self.residual(blk, x, training)
+        for st, skip in zip(model.up_stages(), reversed(skips)):
+            x = up2_add(x, skip)
+            x = self.duck(st.duck, x, training)
+        return self.head(model.seg_head, x, model.num_class)
+
+    def unet(self, model, images, training):
+        import torch.nn.functional as F
+        x = to_fm(images)
+        skips = []
+        for i in range(1, 5):
+            st = getattr(model, f'down_stage{i}')
+            f = self.cba(st.conv[0], x, training)
+            f = self.cba(st.conv[1], f, training)
+            skips.append(f)
+            p = st.pool
+            x = F.max_pool2d(f.permute(0, 3, 1, 2), p.kernel_size, p.stride, p.padding).permute(0, 2, 3, 1)
+            x = x.contiguous()
+        x = self.cba(model.mid_stage[0], x, training)
+        x = self.cba(model.mid_stage[1], x, training)
+        for i in range(4, 0, -1):
+            st = getattr(model, f'up_stage{i}')
+            dc = st.up.up_conv
+            plan = self.plan_deconv(dc[0])
+            (u,), part = conv(plan, [x], want_stats=training)
+            u = bn_act([u], self.bn(dc[1]), _is_relu(dc[2]), training, (part, plan.rows, 0) if training else None)
+            x = self.cba(st.conv[0], [u, skips[i - 1]], training)
+            x = self.cba(st.conv[1], x, training)
+        return self.head(model.seg_head, x, model.num_class)
+
+    def forward(self, images, training=None):
+        model = self.model
+        training = model.training if training is None else training
+        name = type(model).__name__
+        if name == 'DuckNet':
+            return self.ducknet(model, images, training)
+        if name == 'UNet':
+            return self.unet(model, images, training)
+        raise NotImplementedError(f'no fused executor for {name}')
+
+    __call__ = forward
+
+
+def supports(model) -> bool:
+    return type(model).__name__ in ('DuckNet', 'UNet')

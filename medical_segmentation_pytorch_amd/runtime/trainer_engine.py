@@ -1,0 +1,122 @@
+"""The fused MI355X training step used by ``bench.py`` (and, in full, by ``core.SegTrainer``).
+
+One step = reference ``core/seg_trainer.py:24-95`` semantics: zero_grad, forward, CE loss,
+backward with DDP-style averaged gradients (RCCL buckets overlapped with backward) and SyncBN,
+optimizer step, OneCycle lr/momentum step, EMA update -- nothing skipped.  The whole step is
+captured once into a hipGraph (``torch.cuda.CUDAGraph`` is HIP graphs on ROCm) and replayed; the
+only per-step host work is writing the OneCycle values into the hyper-parameter tensor.
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.distributed as dist
+
+from ..ops._ext import require
+from ..ops.losses import cross_entropy
+from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle
+from .fused_model import FusedExecutor
+
+
+class FusedStep:
+    def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
+                 total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
+                 syncbn=True, bucket_cap_mb=64.0, ignore_index=255):
+        require()
+        dev = images.device
+        self.model = model
+        self.images, self.masks = images, masks
+        self.ignore_index = ignore_index
+        self.world = dist.get_world_size() if distributed else 1
+        group = dist.group.WORLD if distributed else None
+        self.ema_model = copy.deepcopy(model).eval()
+        self.arena = Arena(model, dev)
+        self.bucketer = GradBucketer(self.arena, group, bucket_cap_mb) if distributed else None
+        self.ex = FusedExecutor(model, group=group if syncbn else None, sinks=self.arena.sinks(), count_nbt=False,
+                                ready_hook=self.bucketer.ready if self.bucketer else None)
+        kind = optimizer
+        self.opt = FlatOptimizer(self.arena, kind, lr=lr, weight_decay=weight_decay, momentum=momentum)
+        self.opt.grad_scale = 1.0 / self.world
+        self.sched = OneCycle(lr, total_steps, pct_start)
+        # EMA: flat copy of the parameter arena + running statistics (reference ModelEmaV2)
+        self.ema_arena = Arena(self.ema_model, dev, with_grad=False)
+        self.use_ema = use_ema
+        self.ema_hyper = torch.zeros(1, device=dev)
+        self.ema_hyper_host = torch.zeros(1).pin_memory()
+        self.total_steps = total_steps
+        self.itrs = 0
+        self.use_graph = use_graph
+        self.graph = None
+        self.loss = None
+
+    def _body(self):
+        C = require()
+        self.arena.grad.zero_()
+        self.ex.repack()
+        out = self.ex(self.images, training=True)
+        loss = cross_entropy(out, self.masks, None, self.ignore_index)
+        loss.backward()
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        self.opt.step()
+        self.arena.nbt.add_(1)
+        C.ema_update(self.ema_arena.data, self.arena.data, self.ema_hyper)
+        C.ema_update(self.ema_arena.bufdata, self.arena.bufdata, self.ema_hyper)
+        return loss
+
+    def _prepare(self):
+        lr, mom = self.sched.values()
+        self.opt.lr = lr
+        if self.opt.kind in ('adam', 'adamw'):
+            self.opt.betas = (mom, self.opt.betas[1])
+        else:
+            self.opt.momentum = mom
+        self.opt.prepare()
+        self.itrs += 1
+        d = min(max(self.itrs / self.total_steps, 0.0), 1.0) if self.use_ema else 0.0
+        self.ema_hyper_host[0] = d
+        self.ema_hyper.copy_(self.ema_hyper_host, non_blocking=True)
+        self.sched.step()
+
+    def __call__(self):
+        self._prepare()
+        if self.ex.pack_program is None and self.itrs > 1:
+            self.ex.build_pack_program(self.images.device)
+        if not self.use_graph:
+            self.loss = self._body()
+            return self.loss
+        if self.graph is None:
+            # warm up on a side stream (allocator + autograd state), then capture
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._body()
+                if self.ex.pack_program is None:
+                    self.ex.build_pack_program(self.images.device)
+                self._body()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.loss = self._body()
+        self.graph.replay()
+        return self.loss
+
+
+def build_fused_step(batch, size, base_channel, device, use_graph=True, distributed=False, optimizer='adam',
+                     lr=1e-3, model_name='ducknet', syncbn=True):
+    from ..models.ducknet import DuckNet
+    from ..models.unet import UNet
+    from .bench_step import synthetic_batch
+    torch.manual_seed(1)
+    if model_name == 'ducknet':
+        model = DuckNet(num_class=2, n_channel=3, base_channel=base_channel)
+    else:
+        model = UNet(num_class=2, n_channel=3, base_channel=base_channel)
+    model = model.to(device).train()
+    if distributed:   # identical initial weights on every rank (DDP broadcast semantics)
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, 0)
+    images, masks = synthetic_batch(batch, size, device, seed=dist.get_rank() if distributed else 0)
+    return FusedStep(model, images, masks, optimizer=optimizer, lr=lr, use_graph=use_graph, distributed=distributed,
+                     syncbn=syncbn)

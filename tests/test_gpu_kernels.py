@@ -1,0 +1,287 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (MI355X only)."""
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from medical_segmentation_pytorch_amd.ops.bn import BNState, bn_act, bn_act_reference
+from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, conv, conv_reference
+from medical_segmentation_pytorch_amd.ops.fm import cpad, from_fm_reference, to_fm_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, (kh, kw), stride, pad, dil
+    (2, 16, 16, 17, 17, (3, 3), 1, (1, 1), (1, 1)),
+    (2, 16, 16, 17, 34, (3, 3), 1, (2, 2), (2, 2)),
+    (2, 16, 16, 34, 34, (3, 3), 1, (3, 3), (3, 3)),
+    (2, 12, 20, 3, 17, (1, 7), 1, (0, 3), (1, 1)),
+    (2, 12, 20, 17, 17, (7, 1), 1, (3, 0), (1, 1)),
+    (2, 16, 16, 17, 34, (2, 2), 2, (0, 0), (1, 1)),
+    (2, 16, 16, 17, 34, (3, 3), 2, (1, 1), (1, 1)),
+    (2, 8, 8, 136, 68, (1, 1), 1, (0, 0), (1, 1)),
+    (1, 11, 11, 272, 544, (3, 3), 1, (1, 1), (1, 1)),
+    (3, 9, 7, 40, 72, (3, 3), 1, (1, 1), (1, 1)),
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv_fwd_bwd(gpu, case):
+    n, h, w, ci, co, (kh, kw), s, pad, dil = case
+    torch.manual_seed(0)
+    m = nn.Conv2d(ci, co, (kh, kw), s, pad, dil, bias=False).to(gpu)
+    plan = ConvPlan(kh, kw, ci, co, [Branch(m.weight)], stride=s, padding=pad, dilation=dil)
+    x = _bf(torch.randn(n, ci, h, w, device=gpu))
+    xf = to_fm_reference(x).requires_grad_(True)
+    (y,), part = conv(plan, [xf], want_stats=True)
+    # reference with the same bf16-rounded operands
+    xr = x.clone().requires_grad_(True)
+    wr = _bf(m.weight.detach()).requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, pad, dil)
+    assert y.shape == (n, yr.shape[2], yr.shape[3], cpad(co))
+    assert _rel(from_fm_reference(y, co), yr) < 1e-2
+    if co < cpad(co):
+        assert y[..., co:].abs().max().item() == 0.0      # padded channels stay zero
+    # conv-epilogue BN partials == channel sums of the stored output
+    tot = part.sum(0)
+    yv = y.float().reshape(-1, cpad(co))
+    assert _rel(tot[0], yv.sum(0)) < 1e-3
+    assert _rel(tot[1], (yv * yv).sum(0)) < 1e-3
+    # backward
+    g = _bf(torch.randn_like(yr))
+    yr.backward(g)
+    gf = to_fm_reference(g)
+    y.backward(gf)
+    assert _rel(from_fm_reference(xf.grad, ci), xr.grad) < 2e-2
+    assert _rel(m.weight.grad, wr.grad) < 2e-2
+
+
+def test_conv_groups_fused_siblings(gpu):
+    """DUCK-style horizontal fusion: 3x3 convs + 1x1 convs (centre tap) in one launch."""
+    torch.manual_seed(1)
+    n, h, w, ci, co = 2, 16, 16, 17, 17
+    c3 = [nn.Conv2d(ci, co, 3, 1, 1, bias=False).to(gpu) for _ in range(2)]
+    c1 = [nn.Conv2d(ci, co, 1, bias=False).to(gpu) for _ in range(2)]
+    br = [Branch(c.weight, g, 0, 9) for g, c in enumerate(c3)] + [Branch(c.weight, 2 + g, 4, 1) for g, c in enumerate(c1)]
+    plan = ConvPlan(3, 3, ci, co, br, padding=(1, 1), Go=4)
+    x = _bf(torch.randn(n, ci, h, w, device=gpu))
+    xf = to_fm_reference(x).requires_grad_(True)
+    ys, part = conv(plan, [xf], want_stats=True)
+    refs = [F.conv2d(x, _bf(c.weight.detach()), None, 1, 1) for c in c3] + [F.conv2d(x, _bf(c.weight.detach())) for c in c1]
+    for y, r in zip(ys, refs):
+        assert _rel(from_fm_reference(y, co), r) < 1e-2
+    # backward: input grad = sum of the four branches' dgrads
+    gs = [_bf(torch.randn_like(r)) for r in refs]
+    xr = x.clone().requires_grad_(True)
+    ws = [_bf(c.weight.detach()).requires_grad_(True) for c in c3 + c1]
+    out = sum((F.conv2d(xr, wv, None, 1, 1 if i < 2 else 0) * gg).sum() for i, (wv, gg) in enumerate(zip(ws, gs)))
+    out.backward()
+    torch.autograd.backward(ys, [to_fm_reference(gg) for gg in gs])
+    assert _rel(from_fm_reference(xf.grad, ci), xr.grad) < 2e-2
+    for c, wv in zip(c3 + c1, ws):
+        assert _rel(c.weight.grad, wv.grad) < 2e-2
+
+
+def test_conv_group_inputs(gpu):
+    """UNet concat: conv over two input tensors without materialising torch.cat."""
+    torch.manual_seed(2)
+    n, h, w, ci, co = 2, 12, 12, 32, 32
+    m = nn.Conv2d(2 * ci, co, 3, 1, 1, bias=False).to(gpu)
+    plan = ConvPlan(3, 3, ci, co, [Branch(m.weight)], padding=(1, 1), Gi=2)
+    a = _bf(torch.randn(n, ci, h, w, device=gpu))
+    b = _bf(torch.randn(n, ci, h, w, device=gpu))
+    af, bf_ = to_fm_reference(a).requires_grad_(True), to_fm_reference(b).requires_grad_(True)
+    (y,), _ = conv(plan, [af, bf_])
+    xr = torch.cat([a, b], 1).requires_grad_(True)
+    wr = _bf(m.weight.detach()).requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 1, 1)
+    assert _rel(from_fm_reference(y, co), yr) < 1e-2
+    g = _bf(torch.randn_like(yr))
+    yr.backward(g)
+    y.backward(to_fm_reference(g))
+    assert _rel(from_fm_reference(af.grad, ci), xr.grad[:, :ci]) < 2e-2
+    assert _rel(from_fm_reference(bf_.grad, ci), xr.grad[:, ci:]) < 2e-2
+    assert _rel(m.weight.grad, wr.grad) < 2e-2
+
+
+def test_conv_transpose(gpu):
+    torch.manual_seed(3)
+    n, h, w, ci, co = 2, 8, 8, 64, 32
+    m = nn.ConvTranspose2d(ci, co, 3, 2, 1, output_padding=1).to(gpu)
+    plan = ConvPlan(3, 3, ci, co, [Branch(m.weight)], stride=2, padding=(1, 1), transposed=True, output_padding=1,
+                    bias=m.bias)
+    x = _bf(torch.randn(n, ci, h, w, device=gpu))
+    xf = to_fm_reference(x).requires_grad_(True)
+    (y,), _ = conv(plan, [xf])
+    xr = x.clone().requires_grad_(True)
+    wr = _bf(m.weight.detach()).requires_grad_(True)
+    br = m.bias.detach().clone().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, br, 2, 1, 1)
+    assert y.shape[1:3] == yr.shape[2:]
+    assert _rel(from_fm_reference(y, co), yr) < 1e-2
+    g = _bf(torch.randn_like(yr))
+    yr.backward(g)
+    y.backward(to_fm_reference(g))
+    assert _rel(from_fm_reference(xf.grad, ci), xr.grad) < 2e-2
+    assert _rel(m.weight.grad, wr.grad) < 2e-2
+    assert _rel(m.bias.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize('C,k', [(17, 1), (34, 2), (136, 6), (3, 1)])
+def test_bn_act(gpu, C, k):
+    torch.manual_seed(4)
+    n, h, w = 4, 16, 16
+    bn = nn.BatchNorm2d(C).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_ref = nn.BatchNorm2d(C).to(gpu)
+    bn_ref.load_state_dict(bn.state_dict())
+    xs = [_bf(torch.randn(n, C, h, w, device=gpu) * 2 + 0.3) for _ in range(k)]
+    xfs = [to_fm_reference(x).requires_grad_(True) for x in xs]
+    st = BNState.from_module(bn)
+    z = bn_act(xfs, st, relu=True, training=True)
+    xrs = [x.clone().requires_grad_(True) for x in xs]
+    s = xrs[0]
+    for x in xrs[1:]:
+        s = s + x
+    if k > 1:
+        s = s + (_bf(s.detach()) - s.detach())  # the fused sum is stored in bf16
+    zr = F.relu(bn_ref(s))
+    assert _rel(from_fm_reference(z, C), zr) < 1e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, atol=1e-4, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+    g = _bf(torch.randn_like(zr))
+    zr.backward(g)
+    z.backward(to_fm_reference(g))
+    for xf, xr in zip(xfs, xrs):
+        assert _rel(from_fm_reference(xf.grad, C), xr.grad) < 2e-2
+    assert _rel(bn.weight.grad, bn_ref.weight.grad) < 1e-2
+    assert _rel(bn.bias.grad, bn_ref.bias.grad) < 1e-2
+    # eval mode uses running stats
+    bn.eval(); bn_ref.eval()
+    ze = bn_act([xfs[0].detach()], BNState.from_module(bn), relu=True, training=False)
+    assert _rel(from_fm_reference(ze, C), F.relu(bn_ref(xs[0]))) < 1e-2
+
+
+def test_elementwise(gpu):
+    from medical_segmentation_pytorch_amd.ops.elementwise import add_n, from_fm, to_fm, up2_add
+    torch.manual_seed(5)
+    x = torch.randn(2, 3, 16, 16, device=gpu)
+    fm = to_fm(x)
+    assert torch.equal(fm, to_fm_reference(x))
+    back = from_fm(fm, 3)
+    assert torch.equal(back, from_fm_reference(fm, 3))
+    low = to_fm_reference(torch.randn(2, 34, 8, 8, device=gpu)).requires_grad_(True)
+    skip = to_fm_reference(torch.randn(2, 34, 16, 16, device=gpu)).requires_grad_(True)
+    out = up2_add(low, skip)
+    ref = F.interpolate(from_fm_reference(low, 34), size=(16, 16), mode='nearest') + from_fm_reference(skip, 34)
+    assert _rel(from_fm_reference(out, 34), ref) < 1e-2
+    g = to_fm_reference(torch.randn(2, 34, 16, 16, device=gpu))
+    out.backward(g)
+    gl = F.avg_pool2d(from_fm_reference(g, 34), 2) * 4
+    assert _rel(from_fm_reference(low.grad, 34), gl) < 1e-2
+    a, b, c = [to_fm_reference(torch.randn(2, 5, 4, 4, device=gpu)) for _ in range(3)]
+    s = add_n(a, b, c)
+    assert _rel(s.float(), a.float() + b.float() + c.float()) < 1e-2
+
+
+@pytest.mark.parametrize('weighted', [False, True])
+def test_cross_entropy(gpu, weighted):
+    from medical_segmentation_pytorch_amd.ops.losses import cross_entropy
+    torch.manual_seed(6)
+    logits = torch.randn(3, 4, 10, 12, device=gpu, requires_grad=True)
+    tgt = torch.randint(0, 4, (3, 10, 12), device=gpu)
+    tgt[0, :2] = 255
+    w = torch.tensor([1.0, 2.0, 0.5, 1.5], device=gpu) if weighted else None
+    loss = cross_entropy(logits, tgt, w, 255)
+    lr = logits.detach().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, tgt, weight=w, ignore_index=255)
+    assert abs(loss.item() - ref.item()) < 1e-4
+    loss.backward(); ref.backward()
+    assert _rel(logits.grad, lr.grad) < 1e-4
+
+
+def test_ohem_and_kd(gpu):
+    from medical_segmentation_pytorch_amd.ops.losses import kd_kl_div, ohem_cross_entropy
+    torch.manual_seed(7)
+    logits = torch.randn(2, 2, 16, 16, device=gpu, requires_grad=True)
+    tgt = torch.randint(0, 2, (2, 16, 16), device=gpu)
+    loss = ohem_cross_entropy(logits, tgt, 0.7, 255)
+    lr = logits.detach().clone().requires_grad_(True)
+    px = F.cross_entropy(lr, tgt, ignore_index=255, reduction='none').view(-1)
+    hard = px[px > -math.log(0.7)]
+    n_min = tgt.numel() // 16
+    if hard.numel() < n_min:
+        hard, _ = px.topk(n_min)
+    ref = hard.mean()
+    assert abs(loss.item() - ref.item()) < 1e-4
+    loss.backward(); ref.backward()
+    assert _rel(logits.grad, lr.grad) < 1e-4
+    s = torch.randn(2, 3, 8, 8, device=gpu, requires_grad=True)
+    t = torch.randn(2, 3, 8, 8, device=gpu)
+    kd = kd_kl_div(s, t, 4.0)
+    sr = s.detach().clone().requires_grad_(True)
+    kr = F.kl_div(F.log_softmax(sr / 4, 1), F.softmax(t / 4, 1), reduction='mean') * 16
+    assert abs(kd.item() - kr.item()) < 1e-5
+    kd.backward(); kr.backward()
+    assert _rel(s.grad, sr.grad) < 1e-4
+
+
+def test_optim_and_ema(gpu):
+    from medical_segmentation_pytorch_amd import _C
+    torch.manual_seed(8)
+    n = 1000
+    for adamw in (False, True):
+        p = torch.randn(n, device=gpu)
+        pr = p.clone().requires_grad_(True)
+        opt = (torch.optim.AdamW if adamw else torch.optim.Adam)([pr], lr=1e-2, weight_decay=0.1)
+        m = torch.zeros(n, device=gpu); v = torch.zeros(n, device=gpu)
+        for step in range(1, 4):
+            g = torch.randn(n, device=gpu)
+            pr.grad = g.clone()
+            opt.step()
+            hyper = torch.tensor([1e-2, 0.9, 0.999, 1e-8, 0.1, 1 - 0.9 ** step, 1 - 0.999 ** step, 1.0], device=gpu)
+            _C.adam_step(p, g, m, v, hyper, adamw)
+        assert _rel(p, pr.detach()) < 1e-5
+    p = torch.randn(n, device=gpu)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.SGD([pr], lr=1e-2, momentum=0.9, weight_decay=1e-4)
+    buf = torch.zeros(n, device=gpu)
+    for _ in range(3):
+        g = torch.randn(n, device=gpu)
+        pr.grad = g.clone()
+        opt.step()
+        _C.sgd_step(p, g, buf, torch.tensor([1e-2, 0.9, 1e-4, 1.0], device=gpu))
+    assert _rel(p, pr.detach()) < 1e-5
+    e = torch.randn(n, device=gpu); mm = torch.randn(n, device=gpu)
+    ref = 0.3 * e + 0.7 * mm
+    _C.ema_update(e, mm, torch.tensor([0.3], device=gpu))
+    assert _rel(e, ref) < 1e-6
+
+
+def test_confmat(gpu):
+    from medical_segmentation_pytorch_amd import _C
+    torch.manual_seed(9)
+    logits = torch.randn(2, 3, 9, 9, device=gpu)
+    tgt = torch.randint(0, 3, (2, 9, 9), device=gpu)
+    tgt[0, 0] = 255
+    cm = torch.zeros(3, 3, dtype=torch.long, device=gpu)
+    _C.confmat_update(logits, tgt, cm, 255)
+    pred = logits.argmax(1)
+    valid = tgt != 255
+    ref = torch.bincount(tgt[valid] * 3 + pred[valid], minlength=9).view(3, 3)
+    assert torch.equal(cm, ref)

@@ -1,0 +1,103 @@
+"""End-to-end fused executor vs eager fp32 PyTorch on the same module tree (MI355X only)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from medical_segmentation_pytorch_amd.models.ducknet import DuckNet
+from medical_segmentation_pytorch_amd.models.unet import UNet
+from medical_segmentation_pytorch_amd.runtime.fused_model import FusedExecutor
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    return F.cosine_similarity(a.flatten().float(), b.flatten().float(), dim=0).item()
+
+
+def _eager_bf16(model, x):
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        return model(x).float()
+
+
+@pytest.mark.parametrize('model_fn,size,batch', [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64, 2)])
+def test_fused_matches_eager(gpu, model_fn, size, batch):
+    """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is."""
+    torch.manual_seed(0)
+    model = model_fn().to(gpu).train()
+    ref = copy.deepcopy(model)
+    ref16 = copy.deepcopy(model)
+    x = torch.randn(batch, 3, size, size, device=gpu)
+    tgt = torch.randint(0, 2, (batch, size, size), device=gpu)
+    ex = FusedExecutor(model)
+    out = ex(x, training=True)
+    out_ref = ref(x)
+    out16 = _eager_bf16(ref16, x)
+    base = _cos(out16, out_ref)
+    got = _cos(out, out_ref)
+    print(f'logits cos: fused {got:.4f}  autocast-bf16 {base:.4f}')
+    assert out.shape == out_ref.shape
+    assert got > min(0.99, base - 0.05)
+    F.cross_entropy(out, tgt).backward()
+    F.cross_entropy(out_ref, tgt).backward()
+    F.cross_entropy(out16, tgt).backward()
+    cf, cb = [], []
+    for p, q, r in zip(model.parameters(), ref.parameters(), ref16.parameters()):
+        assert p.grad is not None
+        if q.grad.abs().sum() > 0:
+            cf.append(_cos(p.grad, q.grad))
+            cb.append(_cos(r.grad, q.grad))
+    mf = sum(cf) / len(cf)
+    mb = sum(cb) / len(cb)
+    print(f'grad cos mean: fused {mf:.4f} autocast-bf16 {mb:.4f}; min fused {min(cf):.4f} bf16 {min(cb):.4f}')
+    assert mf > mb - 0.05
+    for (k, a), (_, b) in zip(model.state_dict().items(), ref.state_dict().items()):
+        if 'num_batches_tracked' in k:
+            assert int(a) == int(b), k
+    model.eval(); ref.eval()
+    with torch.no_grad():
+        assert _cos(ex(x, training=False), ref(x)) > 0.95
+
+
+def _block_check(gpu, mod, fused_fn, shape, tol=0.99):
+    torch.manual_seed(0)
+    mod = mod.to(gpu).train()
+    ref = copy.deepcopy(mod)
+    from medical_segmentation_pytorch_amd.ops.fm import from_fm_reference, to_fm_reference
+    x = torch.randn(*shape, device=gpu).to(torch.bfloat16).float()
+    xf = to_fm_reference(x).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    ref16 = copy.deepcopy(mod)
+    y = fused_fn(FusedExecutor(mod), mod, xf)
+    yr = ref(xr)
+    x16 = x.clone().requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y16 = ref16(x16)
+    c = yr.shape[1]
+    assert _cos(from_fm_reference(y, c), yr) > tol
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    y16.float().backward(g)
+    y.backward(to_fm_reference(g))
+    assert _cos(from_fm_reference(xf.grad, shape[1]), xr.grad) > tol - 0.02
+    for (n, p), q, r in zip(mod.named_parameters(), ref.parameters(), ref16.parameters()):
+        base = _cos(r.grad, q.grad)
+        assert _cos(p.grad, q.grad) > min(tol - 0.04, base - 0.05), (n, _cos(p.grad, q.grad), base)
+
+
+def test_block_residual(gpu):
+    from medical_segmentation_pytorch_amd.models.ducknet import ResidualBlock
+    _block_check(gpu, ResidualBlock(17, 34), lambda ex, m, x: ex.residual(m, x, True), (4, 17, 32, 32))
+
+
+def test_block_duck(gpu):
+    from medical_segmentation_pytorch_amd.models.ducknet import DUCK
+    _block_check(gpu, DUCK(17, 17), lambda ex, m, x: ex.duck(m, x, True), (4, 17, 32, 32))
+
+
+def test_block_cba(gpu):
+    from medical_segmentation_pytorch_amd.models.layers import ConvBNAct
+    _block_check(gpu, ConvBNAct(17, 34, 3, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
+    _block_check(gpu, ConvBNAct(17, 34, 2, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
+    _block_check(gpu, ConvBNAct(17, 17, (1, 7)), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
