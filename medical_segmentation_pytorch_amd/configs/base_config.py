@@ -128,33 +128,39 @@ class BaseConfig:
         self.synthetic_data = False    # generate a synthetic polyp set when data_root is missing
         self.synthetic_num = (64, 16, 16)
         self.synthetic_size = 352
+        self.cap_workers = True        # cap DataLoader workers at the host CPU count (ref: gpu_num*base_workers)
+        self.teacher_base_channel = None
+        self.graph_warmup = 3          # eager iterations before the hipGraph capture
+        self.graph_ddp = False         # also capture multi-GPU steps (RCCL inside the graph)
+        self.progress_bar = True
 
     # ------------------------------------------------------------------
     def init_dependent_config(self):
+        """Derive dependent fields (reference base_config.py:106-123).  Fields this pass derived
+        itself are re-derived on a later call (after CLI overrides); user-set values are kept."""
         assert len(self.metrics) > 0
+        auto = getattr(self, '_auto_derived', set())
 
-        if self.load_ckpt_path is None and not self.is_testing:
-            self.load_ckpt_path = f'{self.save_dir}/last.pth'
+        def derive(name, value, cond):
+            if getattr(self, name) is None or name in auto:
+                if cond:
+                    setattr(self, name, value)
+                    auto.add(name)
 
-        if self.tb_log_dir is None:
-            self.tb_log_dir = f'{self.save_dir}/tb_logs/'
-
-        if self.crop_h is None:
-            self.crop_h = self.crop_size
-        if self.crop_w is None:
-            self.crop_w = self.crop_size
-
+        derive('load_ckpt_path', f'{self.save_dir}/last.pth', not self.is_testing)
+        derive('tb_log_dir', f'{self.save_dir}/tb_logs/', True)
+        derive('crop_h', self.crop_size, True)
+        derive('crop_w', self.crop_size, True)
         if self.data_root is None and self.dataroot is not None:
             self.data_root = self.dataroot
         if self.dataroot is None and self.data_root is not None:
             self.dataroot = self.data_root
-
         if self.logger_name is None:
             self.logger_name = 'seg_trainer'
-
-        if self.dataset == 'polyp':
+        if self.dataset in ('polyp', 'synthetic'):
             self.num_class = 2 if self.num_class == -1 else self.num_class
             self.num_channel = 3 if self.num_channel is None else self.num_channel
+        self._auto_derived = auto
         return self
 
     def to_dict(self):

@@ -111,6 +111,14 @@ def get_parser():
     _flag(p, 'bucket_cap_mb', type=float)
     _flag(p, 'grad_compress', type=str, choices=['bf16'])
     _flag(p, 'synthetic_data', action='store_true')
+    _flag(p, 'synthetic_num', type=int, nargs=3)
+    _flag(p, 'synthetic_size', type=int)
+    _flag(p, 'graph_ddp', action='store_true')
+    _flag(p, 'graph_warmup', type=int)
+    _flag(p, 'log_interval', type=int)
+    _flag(p, 'no_progress_bar', action='store_true')
+    _flag(p, 'dist_backend', type=str, choices=['nccl', 'gloo'])
+    _flag(p, 'num_workers_cap', action='store_false', dest='cap_workers')
     return p
 
 
@@ -126,6 +134,10 @@ def load_parser(config, argv=None):
             config.data_root = value
         if key == 'crop_size':
             config.crop_h = config.crop_w = value
+        if key == 'no_progress_bar':
+            config.progress_bar = not value
+        if key == 'synthetic_num':
+            config.synthetic_num = tuple(value)
     if getattr(config, 'dataset', None) == 'synthetic':
         config.dataset, config.synthetic_data = 'polyp', True
     return config.init_dependent_config()

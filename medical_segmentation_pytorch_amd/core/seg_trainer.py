@@ -1,0 +1,247 @@
+"""Segmentation trainer -- reference ``core/seg_trainer.py:15-181``.
+
+Hot loop (``train_one_epoch``) keeps the reference's step semantics: zero_grad -> forward (autocast
+for the eager engine; the fused engine is bf16 by construction) -> loss (+ KD term) -> backward ->
+scaler.step(optimizer) -> scaler.update -> scheduler.step (per iteration) -> EMA update.
+
+MI355X changes:
+  * no per-iteration host sync: losses stay on the device and are flushed to TensorBoard / the
+    progress bar every ``config.log_interval`` iterations (the reference syncs twice per step);
+  * fused engine + static shapes: after ``graph_warmup`` eager iterations the whole step
+    (weight repack, forward, loss, backward, all-reduce, optimizer) is captured into ONE hipGraph
+    and replayed; the scheduler writes lr/momentum through the optimizer's device hyper tensor;
+  * validation metrics accumulate a device confusion matrix (HIP kernel) and all-reduce it once.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from PIL import Image
+
+from ..models import get_teacher_model
+from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
+from .base_trainer import BaseTrainer
+from .loss import kd_loss_fn
+
+
+def _tqdm(it, enable):
+    if not enable:
+        return it
+    try:
+        from tqdm import tqdm
+        return tqdm(it)
+    except Exception:   # pragma: no cover
+        return it
+
+
+class GraphedStep:
+    """hipGraph capture of one fused training step (``torch.cuda.CUDAGraph`` = HIP graph on ROCm)."""
+
+    def __init__(self, trainer, config):
+        self.t, self.config = trainer, config
+        self.graph = None
+        self.images = self.masks = self.loss = None
+        self.calls = 0
+
+    def _body(self):
+        t = self.t
+        t.optimizer.zero_grad()
+        ex = t.model.executor
+        ex.repack()
+        preds = t.model(self.images)
+        loss = t.loss_fn(preds, self.masks)
+        loss.backward()
+        t.optimizer.launch()
+        return loss.detach()
+
+    def __call__(self, images, masks):
+        t = self.t
+        self.calls += 1
+        if self.images is None:
+            self.images = torch.empty_like(images)
+            self.masks = torch.empty_like(masks)
+        if images.shape != self.images.shape or masks.shape != self.masks.shape:
+            return t.eager_step(images, masks)        # ragged batch: not capturable, run eagerly
+        self.images.copy_(images, non_blocking=True)
+        self.masks.copy_(masks, non_blocking=True)
+        ex = t.model.executor
+        if self.calls <= max(1, self.config.graph_warmup):
+            loss = t.eager_step(self.images, self.masks)
+            if ex.pack_program is None:
+                ex.build_pack_program(self.images.device)
+            return loss
+        t.optimizer.prepare()
+        if self.graph is None:
+            torch.cuda.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.loss = self._body()
+        self.graph.replay()
+        return self.loss
+
+
+class SegTrainer(BaseTrainer):
+    def __init__(self, config):
+        super().__init__(config)
+        if config.is_testing:
+            self.colormap = torch.tensor(get_colormap(config)).to(self.device)
+        else:
+            self.teacher_model = get_teacher_model(config, self.device)
+            self.metrics = [get_seg_metrics(config, m).to(self.device) for m in config.metrics]
+        self.graph_step = None
+        self._ema_exec = (None, None)
+        self._loss_hist = []
+
+    # ------------------------------------------------------------------------------------------------
+    def eager_step(self, images, masks):
+        config = self.config_ref
+        self.optimizer.zero_grad()
+        amp = config.amp_training and not self.fused and self.device.type == 'cuda'
+        dtype = torch.float16 if config.amp_dtype == 'fp16' else torch.bfloat16
+        with torch.autocast('cuda', dtype=dtype, enabled=amp):
+            preds = self.model(images)
+            loss = self.loss_fn(preds, masks)
+        if config.kd_training:
+            with torch.autocast('cuda', dtype=dtype, enabled=self.device.type == 'cuda'):
+                with torch.no_grad():
+                    teacher_preds = self.teacher_model(images)
+            loss_kd = kd_loss_fn(config, preds.float(), teacher_preds.detach().float())
+            loss = loss + config.kd_loss_coefficient * loss_kd
+            self._last_kd = loss_kd.detach()
+        self.scaler.scale(loss).backward()
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        return loss.detach()
+
+    def _use_graph(self, config):
+        return (self.fused and config.use_graph and not config.kd_training and not config.use_aux
+                and config.loss_type == 'ce' and not self.scaler.is_enabled()
+                and (not config.DDP or config.gpu_num == 1 or config.graph_ddp))
+
+    def _flush_logs(self, config, pbar=None):
+        if not self._loss_hist:
+            return
+        vals = torch.stack([v for _, v, _ in self._loss_hist]).float().cpu().tolist()
+        kds = [k for _, _, k in self._loss_hist]
+        kdv = torch.stack(kds).float().cpu().tolist() if all(k is not None for k in kds) else None
+        if config.use_tb and self.main_rank and self.writer is not None:
+            for (itr, _, _), v in zip(self._loss_hist, vals):
+                self.writer.add_scalar('train/loss', v, itr)
+            if kdv is not None:
+                for (itr, _, _), v, tot in zip(self._loss_hist, kdv, vals):
+                    self.writer.add_scalar('train/loss_kd', v, itr)
+                    self.writer.add_scalar('train/loss_total', tot, itr)
+        if pbar is not None and hasattr(pbar, 'set_description'):
+            pbar.set_description(f'Epoch:{self.cur_epoch}/{config.total_epoch}    |Loss:{vals[-1]:4.4g}    |')
+        self.last_loss = vals[-1]
+        self._loss_hist = []
+
+    def train_one_epoch(self, config):
+        self.config_ref = config
+        self.model.train()
+        sampler_set_epoch(config, self.train_loader, self.cur_epoch)
+        if self.graph_step is None and self._use_graph(config) and isinstance(self.model, FusedModel):
+            self.graph_step = GraphedStep(self, config)
+        pbar = _tqdm(self.train_loader, self.main_rank and config.progress_bar)
+        for cur_itrs, (images, masks) in enumerate(pbar):
+            self.cur_itrs = cur_itrs
+            self.train_itrs += 1
+            images = images.to(self.device, dtype=torch.float32, non_blocking=True)
+            masks = masks.to(self.device, dtype=torch.float32 if config.num_class == 1 else torch.long,
+                             non_blocking=True)
+            self._last_kd = None
+            if self.graph_step is not None:
+                loss = self.graph_step(images, masks)
+            else:
+                loss = self.eager_step(images, masks)
+            self.scheduler.step()
+            self.ema_model.update(self.model, self.train_itrs)
+            self._loss_hist.append((self.train_itrs, loss.clone(), self._last_kd))
+            if len(self._loss_hist) >= config.log_interval:
+                self._flush_logs(config, pbar)
+        self._flush_logs(config, pbar)
+
+    # ------------------------------------------------------------------------------------------------
+    def _ema_forward(self, images):
+        ema = self.ema_model.ema
+        if not self.fused:
+            return ema(images)
+        owner, ex = self._ema_exec
+        if owner is not ema:
+            ex = FusedModel(ema).eval()
+            self._ema_exec = (ema, ex)
+        return ex(images)
+
+    @torch.no_grad()
+    def validate(self, config, loader, val_best=False):
+        pbar = _tqdm(loader, self.main_rank and config.progress_bar)
+        for images, masks in pbar:
+            images = images.to(self.device, dtype=torch.float32)
+            _, _, H, W = images.shape
+            stride = config.val_img_stride
+            resized = H % stride != 0 or W % stride != 0
+            if resized:
+                images = F.interpolate(images, (H // stride * stride, W // stride * stride), mode='bilinear')
+            masks = masks.to(self.device, dtype=torch.long)
+            preds = self._ema_forward(images)
+            if resized:
+                preds = F.interpolate(preds, masks.size()[1:], mode='bilinear', align_corners=True)
+            if preds.shape[1] == 1:   # binary (sigmoid) path -> two-class logits for the confmat
+                preds = torch.cat([torch.zeros_like(preds), preds], 1)
+            for metric in self.metrics:
+                metric.update(preds.detach().float(), masks)
+        scores = [metric.compute() for metric in self.metrics]
+        score = scores[0].mean()
+        if self.main_rank and self.logger:
+            for i in range(len(config.metrics)):
+                if val_best:
+                    self.logger.info(f'\n\nTrain {config.total_epoch} epochs finished.' +
+                                     f'\n\nBest m{config.metrics[i]} is: {scores[i].mean():.4f}\n')
+                else:
+                    infos = f' Epoch{self.cur_epoch} m{config.metrics[i]}: {scores[i].mean():.4f} \t| ' + \
+                            f'best m{config.metrics[0]} so far: {self.best_score:.4f}\n'
+                    if len(config.metrics) > 1 and i != len(config.metrics) - 1:
+                        infos = infos[:-1]
+                    self.logger.info(infos)
+                if config.use_tb and self.writer is not None and self.cur_epoch < config.total_epoch:
+                    self.writer.add_scalar(f'val/m{config.metrics[i]}', scores[i].mean().item(), self.cur_epoch + 1)
+                    if config.metrics[i] == 'iou':
+                        for j in range(scores[i].numel()):
+                            self.writer.add_scalar(f'val/IoU_cls{j:02d}', scores[i][j].item(), self.cur_epoch + 1)
+        self.last_scores = {m: s.detach().cpu() for m, s in zip(config.metrics, scores)}
+        for metric in self.metrics:
+            metric.reset()
+        return score
+
+    @torch.no_grad()
+    def predict(self, config):
+        if config.DDP:
+            raise ValueError('Predict mode currently does not support DDP.')
+        if self.logger:
+            self.logger.info('\nStart predicting...\n')
+        model = de_parallel(self.model).eval()
+        fwd = FusedModel(model).eval() if self.fused else model
+        for images, images_aug, img_names in _tqdm(self.test_loader, config.progress_bar):
+            images_aug = images_aug.to(self.device, dtype=torch.float32)
+            preds = fwd(images_aug)
+            if preds.shape[1] == 1:
+                idx = (preds[:, 0] > 0).long()
+            else:
+                idx = preds.max(dim=1)[1]
+            preds = self.colormap[idx].cpu().numpy()
+            images = images.cpu().numpy()
+            for i in range(preds.shape[0]):
+                save_path = os.path.join(config.save_dir, img_names[i])
+                suffix = img_names[i].split('.')[-1]
+                pred = Image.fromarray(preds[i].astype(np.uint8))
+                if config.save_mask:
+                    pred.save(save_path)
+                if config.blend_prediction:
+                    blend_path = save_path.replace(f'.{suffix}', f'_blend.{suffix}')
+                    image = Image.fromarray(images[i].astype(np.uint8))
+                    if image.size != pred.size:
+                        image = image.resize(pred.size, Image.BILINEAR)
+                    Image.blend(image, pred, config.blend_alpha).save(blend_path)

@@ -1,0 +1,69 @@
+"""Datasets and loaders -- reference ``datasets/__init__.py:7-59``.
+
+Differences: the DistributedSampler uses the GLOBAL rank (the reference passes
+LOCAL_RANK, i.e. single-node only); ``dataset='synthetic'`` (or ``synthetic_data=True`` with a
+missing ``data_root``) generates a polyp-like set in the reference layout first.
+"""
+from __future__ import annotations
+
+import os
+
+import torch.distributed as dist
+from torch.utils.data import DataLoader
+
+from .polyp import PolypDataset, seed_worker
+from .synthetic import make_synthetic_polyp, synthetic_tensors  # noqa: F401
+
+dataset_hub = {'polyp': PolypDataset, 'synthetic': PolypDataset}
+
+
+def _ensure_data(config):
+    want = config.dataset == 'synthetic' or (config.synthetic_data and not os.path.isdir(str(config.data_root)))
+    if want:
+        root = config.data_root if config.data_root and config.data_root != '/path/to/your/dataset' \
+            else os.path.join(config.save_dir, 'synthetic_polyp')
+        rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+        if rank0:
+            make_synthetic_polyp(root, config.synthetic_num, config.synthetic_size, config.random_seed)
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+        config.data_root = root
+
+
+def get_dataset(config, mode):
+    _ensure_data(config)
+    if config.dataset in dataset_hub:
+        return dataset_hub[config.dataset](config=config, mode=mode)
+    raise NotImplementedError('Unsupported dataset!')
+
+
+def get_loader(config, rank, mode, pin_memory=True, drop_last=True):
+    dataset = get_dataset(config, mode)
+    if mode == 'train':
+        config.train_num = int(len(dataset) // config.train_bs * config.train_bs)
+    elif mode == 'val':
+        config.val_num = len(dataset)
+    elif mode == 'test':
+        config.test_num = len(dataset)
+    shuffle = mode == 'train'
+    bs = config.train_bs if mode == 'train' else config.val_bs
+    workers = config.num_workers
+    common = dict(num_workers=workers, worker_init_fn=seed_worker, persistent_workers=workers > 0)
+    if config.DDP:
+        from torch.utils.data.distributed import DistributedSampler
+        grank = dist.get_rank() if dist.is_initialized() else max(rank, 0)
+        sampler = DistributedSampler(dataset, num_replicas=config.gpu_num, rank=grank, shuffle=shuffle,
+                                     seed=config.random_seed)
+        return DataLoader(dataset, batch_size=bs, shuffle=False, pin_memory=pin_memory, sampler=sampler,
+                          drop_last=drop_last and mode == 'train', **common)
+    return DataLoader(dataset, batch_size=bs, shuffle=shuffle, pin_memory=pin_memory,
+                      drop_last=drop_last and mode == 'train', **common)
+
+
+def get_test_loader(config):
+    from .test_dataset import TestDataset
+    dataset = TestDataset(config)
+    config.test_num = len(dataset)
+    if config.DDP:
+        raise NotImplementedError('predict mode does not support DDP (reference datasets/__init__.py:54)')
+    return DataLoader(dataset, batch_size=config.test_bs, shuffle=False, num_workers=config.num_workers)

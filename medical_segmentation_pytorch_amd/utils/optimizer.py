@@ -1,0 +1,131 @@
+"""Optimizers -- reference ``utils/optimizer.py:4-21`` (same lr scaling rules).
+
+Eager engine: ``torch.optim.{SGD, Adam, AdamW}``.  Fused MI355X engine: :class:`FusedOptimizer`,
+a real ``torch.optim.Optimizer`` (so ``OneCycleLR`` drives its param_groups and its
+``state_dict`` has torch's format: 'momentum_buffer' / 'exp_avg' / 'exp_avg_sq' / 'step') whose
+parameters, gradients and states are views into flat arenas; ``step`` is ONE HIP kernel launch.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import SGD, Adam, AdamW
+
+
+class FusedOptimizer(torch.optim.Optimizer):
+    def __init__(self, model, kind='adam', lr=1e-3, momentum=0.9, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
+                 device=None):
+        from ..runtime.engine import Arena
+        device = device or next(model.parameters()).device
+        self.kind = kind
+        self.arena = Arena(model, device)
+        params = self.arena.params
+        if kind == 'sgd':
+            defaults = dict(lr=lr, momentum=momentum, dampening=0, weight_decay=weight_decay, nesterov=False,
+                            maximize=False, foreach=None, differentiable=False, fused=None)
+        else:
+            defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                            foreach=None, capturable=False, differentiable=False, fused=None)
+            if kind == 'adamw' and weight_decay == 0.0:
+                defaults['weight_decay'] = 1e-2     # torch.optim.AdamW default
+        super().__init__(params, defaults)
+        n = self.arena.numel
+        if kind == 'sgd':
+            self.buf = torch.zeros(n, device=device)
+        else:
+            self.m = torch.zeros(n, device=device)
+            self.v = torch.zeros(n, device=device)
+        for i, p in enumerate(params):
+            o, k = self.arena.offsets[i], p.numel()
+            if kind == 'sgd':
+                self.state[p] = {'momentum_buffer': self.buf[o:o + k].view_as(p)}
+            else:
+                self.state[p] = {'step': torch.tensor(0.0), 'exp_avg': self.m[o:o + k].view_as(p),
+                                 'exp_avg_sq': self.v[o:o + k].view_as(p)}
+        self.step_count = 0
+        self.hyper = torch.zeros(8, dtype=torch.float32, device=device)
+        self.hyper_host = torch.zeros(8, dtype=torch.float32)
+        if device.type == 'cuda':
+            self.hyper_host = self.hyper_host.pin_memory()
+        self.bucketer = None
+        self.grad_scale = 1.0
+
+    def attach_bucketer(self, bucketer):
+        self.bucketer = bucketer
+        self.grad_scale = 1.0 / bucketer.world
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.arena.grad.zero_()
+
+    def prepare(self):
+        """Write this step's hyper-parameters to the device (host work, outside any hipGraph)."""
+        self.step_count += 1
+        g = self.param_groups[0]
+        h = self.hyper_host
+        if self.kind == 'sgd':
+            h[0], h[1], h[2], h[3] = g['lr'], g['momentum'], g['weight_decay'], self.grad_scale
+        else:
+            b1, b2 = g['betas']
+            h[0], h[1], h[2], h[3], h[4] = g['lr'], b1, b2, g['eps'], g['weight_decay']
+            h[5] = 1 - b1 ** self.step_count
+            h[6] = 1 - b2 ** self.step_count
+            h[7] = self.grad_scale
+        self.hyper.copy_(h, non_blocking=True)
+
+    def launch(self):
+        """Device work of a step (capturable): all-reduce wait + one optimizer kernel."""
+        from ..ops._ext import require
+        C = require()
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        a = self.arena
+        if self.kind == 'sgd':
+            C.sgd_step(a.data, a.grad, self.buf, self.hyper)
+        else:
+            C.adam_step(a.data, a.grad, self.m, self.v, self.hyper, self.kind == 'adamw')
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.prepare()
+        self.launch()
+        return loss
+
+    def state_dict(self):
+        if self.kind != 'sgd':
+            for p in self.arena.params:
+                self.state[p]['step'] = torch.tensor(float(self.step_count))
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        groups = state_dict['param_groups']
+        for g, sg in zip(self.param_groups, groups):
+            for k, v in sg.items():
+                if k != 'params':
+                    g[k] = v
+        params = self.arena.params
+        for idx, st in state_dict['state'].items():
+            p = params[int(idx)]
+            for k, v in st.items():
+                if k == 'step':
+                    self.step_count = int(float(v))
+                    if 'step' in self.state[p]:
+                        self.state[p]['step'] = torch.tensor(float(v))
+                elif k in self.state[p] and v is not None:
+                    self.state[p][k].copy_(v)
+
+
+def get_optimizer(config, model):
+    fused = getattr(config, '_fused', False)
+    if config.optimizer_type == 'sgd':
+        config.lr = config.base_lr * config.gpu_num
+        if fused:
+            return FusedOptimizer(model, 'sgd', lr=config.lr, momentum=config.momentum,
+                                  weight_decay=config.weight_decay)
+        return SGD(model.parameters(), lr=config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
+    if config.optimizer_type in ['adam', 'adamw']:
+        config.lr = 0.1 * config.base_lr * config.gpu_num
+        if fused:
+            return FusedOptimizer(model, config.optimizer_type, lr=config.lr)
+        cls = Adam if config.optimizer_type == 'adam' else AdamW
+        return cls(model.parameters(), lr=config.lr)
+    raise NotImplementedError(f'Unsupported optimizer type: {config.optimizer_type}')

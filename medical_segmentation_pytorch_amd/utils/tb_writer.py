@@ -78,11 +78,20 @@ class SummaryWriter:
         os.makedirs(log_dir, exist_ok=True)
         self.log_dir = log_dir
         name = f'events.out.tfevents.{int(time.time())}.{socket.gethostname()}.{os.getpid()}'
-        self._f = open(os.path.join(log_dir, name), 'wb')
+        self._path = os.path.join(log_dir, name)
+        self._f = open(self._path, 'wb')
         self._jsonl = open(os.path.join(log_dir, 'scalars.jsonl'), 'a')
         self._write(_event(time.time(), 0, file_version='brain.Event:2'))
 
+    def _reopen(self):
+        # torch's SummaryWriter silently re-creates its file writer after close(); the reference
+        # relies on that (val_best logs after writer.close(), core/base_trainer.py:108-118)
+        if self._f.closed:
+            self._f = open(self._path, 'ab')
+            self._jsonl = open(os.path.join(self.log_dir, 'scalars.jsonl'), 'a')
+
     def _write(self, data: bytes):
+        self._reopen()
         header = struct.pack('<Q', len(data))
         self._f.write(header + struct.pack('<I', _masked_crc(header)) + data +
                       struct.pack('<I', _masked_crc(data)))

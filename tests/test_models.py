@@ -1,0 +1,90 @@
+import warnings
+
+import pytest
+import torch
+
+from medical_segmentation_pytorch_amd.models import DuckNet, UNet, count_params, decoder_hub, get_model
+from medical_segmentation_pytorch_amd.models.layers import Activation
+from medical_segmentation_pytorch_amd.configs import MyConfig
+
+
+@pytest.mark.parametrize('ctor,params,keys', [
+    (lambda: DuckNet(2, 3, 17), 40_101_544, 1733),
+    (lambda: UNet(2, 3, 32), 8_634_432, 137),
+])
+def test_param_count_and_keys(ctor, params, keys):
+    m = ctor()
+    assert count_params(m) == params
+    assert len(m.state_dict()) == keys
+
+
+def test_ducknet34_param_count():
+    assert round(count_params(DuckNet(2, 3, 34)) / 1e6, 2) == 160.28
+
+
+def test_reference_key_names():
+    k = set(DuckNet(2, 3, 17).state_dict())
+    for key in ['down_stage1.duck.branch1.0.0.weight', 'down_stage1.duck.in_bn.0.running_var',
+                'down_stage3.duck.branch3.upper_branch.weight', 'down_stage3.duck.branch4.1.lower_branch.1.1.bias',
+                'down_stage5.conv2.1.num_batches_tracked', 'mid_stage.3.bn.0.weight',
+                'up_stage1.duck.branch6.1.0.weight', 'up_stage1.duck.out_bn.0.weight', 'seg_head.weight']:
+        assert key in k, key
+    u = set(UNet(2, 3, 32).state_dict())
+    for key in ['down_stage1.conv.0.0.weight', 'mid_stage.1.1.running_mean', 'up_stage4.up.up_conv.0.bias',
+                'up_stage1.conv.1.1.weight', 'seg_head.weight']:
+        assert key in u, key
+
+
+@pytest.mark.parametrize('size,ok', [(64, True), (96, True), (80, False)])
+def test_ducknet_divisibility(size, ok):
+    m = DuckNet(2, 3, 8).eval()
+    x = torch.randn(1, 3, size, size)
+    if ok:
+        assert m(x).shape == (1, 2, size, size)
+    else:
+        with pytest.raises(Exception):
+            m(x)
+
+
+def test_unet_forward():
+    m = UNet(2, 3, 8).eval()
+    assert m(torch.randn(2, 3, 48, 64)).shape == (2, 2, 48, 64)
+
+
+def test_smp_unet_parity_counts():
+    warnings.simplefilter('ignore')
+    r18 = decoder_hub['unet'](encoder_name='resnet18', encoder_weights=None, in_channels=3, classes=1)
+    assert count_params(r18) == 14_328_209              # README.md:113 "14.33M"
+    r101 = decoder_hub['unet'](encoder_name='resnet101', encoder_weights=None, in_channels=3, classes=2)
+    assert round(count_params(r101) / 1e6, 2) == 51.51
+    sd = r18.state_dict()
+    assert 'segmentation_head.0.weight' in sd and 'decoder.blocks.0.conv1.0.weight' in sd
+    assert 'encoder.layer4.1.bn2.running_var' in sd
+
+
+@pytest.mark.parametrize('dec', sorted(decoder_hub))
+def test_all_decoders_forward(dec):
+    warnings.simplefilter('ignore')
+    m = decoder_hub[dec](encoder_name='resnet18', encoder_weights=None, in_channels=3, classes=2).eval()
+    with torch.no_grad():
+        assert m(torch.randn(1, 3, 128, 128)).shape == (1, 2, 128, 128)
+
+
+def test_get_model_factory():
+    c = MyConfig().init_dependent_config()
+    c.model, c.base_channel = 'ducknet', 17
+    assert isinstance(get_model(c), DuckNet)
+    c.model, c.decoder, c.encoder, c.encoder_weights = 'smp', 'fpn', 'resnet34', None
+    m = get_model(c)
+    assert m.segmentation_head[0].out_channels == 2
+    c.model, c.use_aux = 'unet', True
+    with pytest.raises(ValueError):
+        get_model(c)
+
+
+def test_activation_hub():
+    for name in ['relu', 'relu6', 'leakyrelu', 'prelu', 'celu', 'elu', 'hardswish', 'hardtanh', 'gelu', 'selu',
+                 'silu', 'sigmoid', 'tanh', 'none']:
+        assert Activation(name)(torch.randn(2, 4)).shape == (2, 4)
+    with pytest.raises(NotImplementedError):
+        Activation('nope')
