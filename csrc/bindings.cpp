@@ -124,24 +124,35 @@ void sum_stats_t(std::vector<at::Tensor> inputs, const c10::optional<at::Tensor>
   sum_stats(ptrs.data(), (int)ptrs.size(), o, f32(part), P, Cp, cur_stream());
 }
 
+#define CHECK_F64(t) CHECK_DEV(t); TORCH_CHECK((t).scalar_type() == at::kDouble, #t " must be fp64")
+
+// tmp: fp64 [S, 2*Cp] with S = bn_reduce_splits(nblk)
 void bn_reduce_partials_t(const at::Tensor& part, int64_t nblk, int64_t width, int64_t col_off, int64_t Cp,
-                          const at::Tensor& sums) {
-  CHECK_F32(part); CHECK_F32(sums);
-  TORCH_CHECK(part.numel() == nblk * 2 * width && col_off + Cp <= width && sums.numel() == 2 * Cp, "size mismatch");
-  auto tmp = at::empty({(int64_t)bn_reduce_splits(nblk) * 2 * Cp}, sums.options().dtype(at::kDouble));
-  bn_reduce_partials(f32(part), nblk, width, col_off, Cp, f32(sums), tmp.data_ptr<double>(), cur_stream());
+                          const at::Tensor& tmp) {
+  CHECK_F32(part); CHECK_F64(tmp);
+  TORCH_CHECK(part.numel() == nblk * 2 * width && col_off + Cp <= width, "partials size mismatch");
+  TORCH_CHECK(tmp.numel() == (int64_t)bn_reduce_splits(nblk) * 2 * Cp, "tmp must be [bn_reduce_splits(nblk), 2*Cp]");
+  bn_reduce_partials(f32(part), nblk, width, col_off, Cp, tmp.data_ptr<double>(), cur_stream());
 }
 
-void bn_finalize_t(const at::Tensor& sums, int64_t C, int64_t Cp, double count, const c10::optional<at::Tensor>& gamma,
+void bn_collapse_t(const at::Tensor& tmp, int64_t Cp, const at::Tensor& out) {
+  CHECK_F64(tmp); CHECK_F64(out);
+  TORCH_CHECK(tmp.numel() % (2 * Cp) == 0 && out.numel() == 2 * Cp);
+  bn_collapse(tmp.data_ptr<double>(), (int)(tmp.numel() / (2 * Cp)), Cp, out.data_ptr<double>(), cur_stream());
+}
+
+void bn_finalize_t(const at::Tensor& tmp, int64_t C, int64_t Cp, double count, const c10::optional<at::Tensor>& gamma,
                    const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& rmean,
                    const c10::optional<at::Tensor>& rvar, double momentum, double eps, bool training,
                    const at::Tensor& stats) {
-  CHECK_F32(sums); CHECK_F32(stats);
+  CHECK_F64(tmp); CHECK_F32(stats);
   TORCH_CHECK(stats.numel() == 4 * Cp, "stats = [scale, shift, mean, invstd] x Cp");
+  TORCH_CHECK(tmp.numel() % (2 * Cp) == 0, "tmp must be [S, 2*Cp]");
   TORCH_CHECK(training || (rmean.has_value() && rvar.has_value()), "eval BN needs running stats");
   float* st = f32(stats);
-  bn_finalize(f32(sums), C, Cp, (float)count, f32_opt(gamma), f32_opt(beta), f32_opt_mut(rmean), f32_opt_mut(rvar),
-              (float)momentum, (float)eps, training ? 1 : 0, st, st + Cp, st + 2 * Cp, st + 3 * Cp, cur_stream());
+  bn_finalize(tmp.data_ptr<double>(), (int)(tmp.numel() / (2 * Cp)), C, Cp, (float)count, f32_opt(gamma),
+              f32_opt(beta), f32_opt_mut(rmean), f32_opt_mut(rvar), (float)momentum, (float)eps, training ? 1 : 0,
+              st, st + Cp, st + 2 * Cp, st + 3 * Cp, cur_stream());
 }
 
 void bn_act_apply_t(const at::Tensor& y, const at::Tensor& stats, const at::Tensor& z, int64_t P, int64_t Cp, bool relu) {
@@ -160,14 +171,14 @@ void bn_act_bwd_partial_t(const at::Tensor& dz, const at::Tensor& y, const at::T
   bn_act_bwd_partial(bf(dz), bf(y), st, st + Cp, st + 2 * Cp, f32(part), P, Cp, relu ? 1 : 0, cur_stream());
 }
 
-void bn_bwd_finalize_t(const at::Tensor& sums, int64_t C, int64_t Cp, double count, const at::Tensor& stats,
+void bn_bwd_finalize_t(const at::Tensor& tmp, int64_t C, int64_t Cp, double count, const at::Tensor& stats,
                        const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
                        const at::Tensor& coef) {
-  CHECK_F32(sums); CHECK_F32(stats); CHECK_F32(coef);
-  TORCH_CHECK(coef.numel() == 3 * Cp && stats.numel() == 4 * Cp && sums.numel() == 2 * Cp);
+  CHECK_F64(tmp); CHECK_F32(stats); CHECK_F32(coef);
+  TORCH_CHECK(coef.numel() == 3 * Cp && stats.numel() == 4 * Cp && tmp.numel() % (2 * Cp) == 0);
   const float* st = f32(stats);
-  bn_bwd_finalize(f32(sums), C, Cp, (float)count, st, st + 3 * Cp, st + 2 * Cp, f32_opt_mut(dgamma),
-                  f32_opt_mut(dbeta), f32(coef), cur_stream());
+  bn_bwd_finalize(tmp.data_ptr<double>(), (int)(tmp.numel() / (2 * Cp)), C, Cp, (float)count, st, st + 3 * Cp,
+                  st + 2 * Cp, f32_opt_mut(dgamma), f32_opt_mut(dbeta), f32(coef), cur_stream());
 }
 
 void bn_act_bwd_apply_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& coef,
@@ -294,6 +305,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });
   m.def("sum_stats", &sum_stats_t);
   m.def("bn_reduce_partials", &bn_reduce_partials_t);
+  m.def("bn_reduce_splits", [](int64_t nblk) { return bn_reduce_splits(nblk); });
+  m.def("bn_collapse", &bn_collapse_t);
   m.def("bn_finalize", &bn_finalize_t);
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);

@@ -89,15 +89,22 @@ __global__ __launch_bounds__(256) void reduce_partials_stage1(const float* __res
   }
 }
 
-__global__ void reduce_partials_stage2(const double* __restrict__ tmp, int splits, int ncol, float* __restrict__ sums) {
+__global__ void reduce_partials_stage2(const double* __restrict__ tmp, int splits, int ncol, double* __restrict__ sums) {
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= ncol) return;
   double s = 0.0;
   for (int i = 0; i < splits; ++i) s += tmp[(long)i * ncol + col];
-  sums[col] = (float)s;
+  sums[col] = s;
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ sums, int C, int Cp, float count,
+// sum of the S split rows of column i (fixed order -> deterministic)
+DEVI double split_sum(const double* __restrict__ tmp, int S, int ncol, int i) {
+  double s = 0.0;
+  for (int k = 0; k < S; ++k) s += tmp[(long)k * ncol + i];
+  return s;
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ tmp, int S, int C, int Cp, float count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
                                    float eps, int training, float* __restrict__ scale,
@@ -108,8 +115,8 @@ __global__ void bn_finalize_kernel(const float* __restrict__ sums, int C, int Cp
   if (c >= C) { scale[c] = 0.f; shift[c] = 0.f; mean_out[c] = 0.f; invstd_out[c] = 0.f; return; }
   float mean, var;
   if (training) {
-    const double m = (double)sums[c] / count;
-    double v = (double)sums[Cp + c] / count - m * m;
+    const double m = split_sum(tmp, S, 2 * Cp, c) / count;
+    double v = split_sum(tmp, S, 2 * Cp, Cp + c) / count - m * m;
     if (v < 0) v = 0;
     mean = (float)m; var = (float)v;
     if (rmean != nullptr) {
@@ -199,14 +206,14 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
 
 // coef[3][Cp]: dy = k1*dzr + k2*y + k3  (k1 = gamma*invstd, k2 = -k1*invstd*sum(dzr*xmu)/M,
 // k3 = -k1*sum(dzr)/M - k2*mean).  dgamma/dbeta are ACCUMULATED into the fp32 parameter grads.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ sums, int C, int Cp, float count,
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ tmp, int S, int C, int Cp, float count,
                                        const float* __restrict__ scale, const float* __restrict__ invstd,
                                        const float* __restrict__ mean, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= Cp) return;
   if (c >= C) { coef[c] = 0.f; coef[Cp + c] = 0.f; coef[2 * Cp + c] = 0.f; return; }
-  const float sd = sums[c], sdx = sums[Cp + c];
+  const float sd = (float)split_sum(tmp, S, 2 * Cp, c), sdx = (float)split_sum(tmp, S, 2 * Cp, Cp + c);
   if (dgamma != nullptr) dgamma[c] += sdx * invstd[c];
   if (dbeta != nullptr) dbeta[c] += sd;
   const float k1 = scale[c];
@@ -267,18 +274,20 @@ int bn_reduce_splits(long nblk) {
   return (int)sp;
 }
 
-void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, float* sums, double* tmp,
-                        hipStream_t s) {
+void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, double* tmp, hipStream_t s) {
   const int splits = bn_reduce_splits(nblk);
   hipLaunchKernelGGL(reduce_partials_stage1, dim3(cdiv(2 * Cp, kRedCols), splits), dim3(256), 0, s, part, nblk, width,
                      col_off, Cp, tmp);
-  hipLaunchKernelGGL(reduce_partials_stage2, dim3(cdiv(2 * Cp, 256)), dim3(256), 0, s, tmp, splits, 2 * Cp, sums);
 }
 
-void bn_finalize(const float* sums, int C, int Cp, float count, const float* gamma, const float* beta,
+void bn_collapse(const double* tmp, int S, int Cp, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_stage2, dim3(cdiv(2 * Cp, 256)), dim3(256), 0, s, tmp, S, 2 * Cp, out);
+}
+
+void bn_finalize(const double* tmp, int S, int C, int Cp, float count, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, int training,
                  float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, sums, C, Cp, count, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, tmp, S, C, Cp, count, gamma, beta,
                      running_mean, running_var, momentum, eps, training, scale, shift, mean, invstd);
 }
 
@@ -295,9 +304,9 @@ void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scal
                      shift, mean, part, P, Cp, relu);
 }
 
-void bn_bwd_finalize(const float* sums, int C, int Cp, float count, const float* scale, const float* invstd,
+void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale, const float* invstd,
                      const float* mean, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, sums, C, Cp, count, scale,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, tmp, S, C, Cp, count, scale,
                      invstd, mean, dgamma, dbeta, coef);
 }
 

@@ -20,6 +20,8 @@
 // of a stride-s conv, and the forward of ConvTranspose2d.
 // Channel GROUPS (launchers.h): the logical input/output channel dims may be split over up to 8
 // separate NHWC tensors; group pointers are staged in LDS and selected per lane per k-step.
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -345,6 +347,129 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
   }
 }
 
+// Halo-tiled weight gradient for stride-1 convs ("direct wgrad").  The gather kernel above reads
+// every input pixel once per tap (a 9x im2col expansion through L2 for a 3x3); here a block stages an
+// output tile of dY [TH x TW px][32 co] and the matching input HALO [(TH+eh) x (TW+ew) px][32 ci]
+// in LDS ONCE, and every tap reads its shifted window of the halo with ds_read_b64_tr_b16 (each lane
+// supplies its own pixel row address, so the shift is free).  Block output = dW[32 co][T taps][32 ci];
+// the 4 waves own disjoint (tap, ci16) pairs, so no cross-wave reduction.  Blocks loop over pixel
+// tiles (accumulating in registers) and finish with one fp32 atomic per output element.
+constexpr int DW_CH = 32;               // co rows and ci channels per block
+constexpr int DW_LD = DW_CH + 4;        // LDS pixel pitch (bf16 elems): 72 B, 8-B aligned
+
+struct DwTile { int TH, TW, ey0, ex0, HH, HWd, tiles_y, tiles_x; };
+
+template <int NPW>
+__global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
+                                                              DwTile tl, int KT, long ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
+  const int npx = tl.TH * tl.TW;
+  const int nslice = (npx + 31) / 32;
+  uint16_t* sY = dsm;                                    // [nslice*32 + 1][DW_LD] (last row = zeros)
+  uint16_t* sX = dsm + (nslice * 32 + 1) * DW_LD;        // [HH*HWd][DW_LD]
+  __shared__ int2 s_tap[kMaxTaps];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, p4 = lr & 3;
+  const int co0 = blockIdx.y * DW_CH, ci0 = blockIdx.z * DW_CH;
+  const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
+  if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
+  // zero row for out-of-tile pixels
+  if (tid < DW_LD) sY[nslice * 32 * DW_LD + tid] = 0;
+
+  // per-thread loader roles: vector v = tid & 3 (8 channels), pixel = tid >> 2 (+ 64*i)
+  const int vv = tid & 3, vp = tid >> 2;
+  const int yco = co0 + 8 * vv;
+  const bool y_ok = yco < rows;
+  const int y_g = y_ok ? yco / g.Cgo : 0;
+  const uint16_t* y_base = P.dy[y_g] + (yco - y_g * g.Cgo);
+  const int xci = ci0 + 8 * vv;
+  const bool x_ok = xci < Cip;
+  const int x_g = x_ok ? xci / g.Cgi : 0;
+  const uint16_t* x_base = P.x[x_g] + (xci - x_g * g.Cgi);
+
+  f32x4_t acc[2][NPW];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int npairs = 2 * g.T;
+
+  for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
+    const int per_img = tl.tiles_y * tl.tiles_x;
+    const int n = (int)(tix / per_img);
+    const int rem = (int)(tix - (long)n * per_img);
+    const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
+    __syncthreads();   // previous tile's LDS reads are done
+    // ---- stage dY tile (pixels beyond the image -> 0)
+    for (int px = vp; px < nslice * 32; px += 64) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int ty = px / tl.TW, tx = px - (px / tl.TW) * tl.TW;
+      const int oy = y0 + ty, ox = x0 + tx;
+      if (px < npx && y_ok && oy < g.OH && ox < g.OW)
+        v = *reinterpret_cast<const uint4*>(y_base + ((long)n * g.OH * g.OW + (long)oy * g.OW + ox) * g.Cgo);
+      *reinterpret_cast<uint2*>(&sY[px * DW_LD + 8 * vv]) = make_uint2(v.x, v.y);
+      *reinterpret_cast<uint2*>(&sY[px * DW_LD + 8 * vv + 4]) = make_uint2(v.z, v.w);
+    }
+    // ---- stage input halo (zero padding outside the image)
+    const int nh = tl.HH * tl.HWd;
+    for (int hp = vp; hp < nh; hp += 64) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int hy = hp / tl.HWd, hx = hp - (hp / tl.HWd) * tl.HWd;
+      const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
+      if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+        v = *reinterpret_cast<const uint4*>(x_base + ((long)n * g.IH * g.IW + (long)iy * g.IW + ix) * g.Cgi);
+      *reinterpret_cast<uint2*>(&sX[hp * DW_LD + 8 * vv]) = make_uint2(v.x, v.y);
+      *reinterpret_cast<uint2*>(&sX[hp * DW_LD + 8 * vv + 4]) = make_uint2(v.z, v.w);
+    }
+    __syncthreads();
+    for (int sl = 0; sl < nslice; ++sl) {
+      const int plo = 32 * sl + 8 * lg + q, phi = plo + 4;
+      const int ylo = plo < npx ? plo : nslice * 32, yhi = phi < npx ? phi : nslice * 32;
+      uint4 fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint2 lo = tr_read(&sY[ylo * DW_LD + 16 * i + 4 * p4]);
+        const uint2 hi = tr_read(&sY[yhi * DW_LD + 16 * i + 4 * p4]);
+        fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+      const int plc = plo < npx ? plo : 0, phc = phi < npx ? phi : 0;
+      const int lty = plc / tl.TW, ltx = plc - lty * tl.TW;
+      const int hty = phc / tl.TW, htx = phc - hty * tl.TW;
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) {
+        const int pr = wave + 4 * j;
+        if (pr < npairs) {
+          const int t = pr >> 1, cf = pr & 1;
+          const int2 d = s_tap[t];
+          const int xlo = (lty + d.x) * tl.HWd + ltx + d.y;
+          const int xhi = (hty + d.x) * tl.HWd + htx + d.y;
+          const uint2 lo = tr_read(&sX[xlo * DW_LD + 16 * cf + 4 * p4]);
+          const uint2 hi = tr_read(&sX[xhi * DW_LD + 16 * cf + 4 * p4]);
+          const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          acc[0][j] = mfma16x16x32(fa[0], fb, acc[0][j]);
+          acc[1][j] = mfma16x16x32(fa[1], fb, acc[1][j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int pr = wave + 4 * j;
+    if (pr >= npairs) continue;
+    const int t = pr >> 1, cf = pr & 1;
+    const int ci = ci0 + 16 * cf + lr;
+    if (ci >= Cip) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + 16 * i + 4 * lg + r;
+        if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dw[(long)co * KT + t * Cip + ci], acc[i][j][r]);
+      }
+  }
+}
+
 __global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, int nrow, int nch,
                                    int T, int Cpk, int Kp, int t_base, int c_base, long s_row, long s_ch) {
   const long total = (long)nrow * nch * T;
@@ -461,10 +586,50 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   else dispatch_igemm<false>(a, mi, wpx, s);
 }
 
+static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
+  if (g.stride != 1 || g.T > 9) return false;
+  int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
+  for (int t = 0; t < g.T; ++t) {
+    ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
+    ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
+  }
+  if (g.OH != g.IH || g.OW != g.IW) return false;
+  const int nx = cdiv(g.OW, 32);
+  tl.TW = cdiv(g.OW, nx);
+  tl.TH = std::max(1, std::min(g.OH, 256 / tl.TW));
+  tl.ey0 = ey0; tl.ex0 = ex0;
+  tl.HH = tl.TH + ey1 - ey0;
+  tl.HWd = tl.TW + ex1 - ex0;
+  tl.tiles_y = cdiv(g.OH, tl.TH);
+  tl.tiles_x = cdiv(g.OW, tl.TW);
+  const int nslice = cdiv(tl.TH * tl.TW, 32);
+  const size_t lds = ((size_t)(nslice * 32 + 1) + (size_t)tl.HH * tl.HWd) * DW_LD * 2;
+  return lds <= 64 * 1024;
+}
+
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
                 hipStream_t s) {
   const int KT = g.T * g.Gi * g.Cgi;
   const int rows = g.Go * g.Cgo;
+  WgradPtrs P{};
+  for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
+  for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT, s);
+  DwTile tl{};
+  if (!trans && wgrad_halo_ok(g, tl)) {
+    const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;
+    const int gy = cdiv(rows, DW_CH), gz = cdiv(g.Gi * g.Cgi, DW_CH);
+    long nsplit = 1536 / ((long)gy * gz);
+    if (nsplit < 1) nsplit = 1;
+    if (nsplit > ntiles) nsplit = ntiles;
+    const int nslice = cdiv(tl.TH * tl.TW, 32);
+    const size_t lds = ((size_t)(nslice * 32 + 1) + (size_t)tl.HH * tl.HWd) * DW_LD * 2;
+    dim3 grid((unsigned)nsplit, gy, gz);
+    const int npw = cdiv(2 * g.T, 4);
+#define HW_(N_) if (npw == N_) { hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_>), grid, dim3(256), lds, s, P, dw, g, tl, KT, ntiles); return; }
+    HW_(1) HW_(2) HW_(3) HW_(4) HW_(5)
+#undef HW_
+  }
   const long M = (long)g.N * g.OH * g.OW;
   const long nchunks = (M + WG_M - 1) / WG_M;
   const int co_t = rows <= 32 ? 32 : 64;
@@ -473,11 +638,7 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
   long target = 2048 / ((long)gx * gy);
   if (target < 1) target = 1;
   if (target > nchunks) target = nchunks;
-  WgradPtrs P{};
-  for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
-  for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
   dim3 grid(gx, gy, (unsigned)target);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT, s);
 #define WG(CO_, K_)                                                                                  \
   if (co_t == CO_ && k_t == K_) {                                                                    \
     if (trans) hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, true>), grid, dim3(256), 0, s, P, dw, g, KT); \

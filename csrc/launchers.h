@@ -58,19 +58,20 @@ constexpr int kMaxSumInputs = 8;
 long bn_partial_blocks(long P, int Cp);
 void sum_stats(const uint16_t* const* inputs, int k, uint16_t* out, float* part, long P, int Cp,
                hipStream_t s);
-// sums[2][Cp] = sum_b part[b][s][col_off + c]; part rows are [2][width]; tmp = fp64 workspace of
-// bn_reduce_splits(nblk) * 2*Cp elements
+// Channel reductions of [nblk][2][width] partials (columns col_off .. col_off+Cp) into an fp64
+// workspace tmp[S][2*Cp], S = bn_reduce_splits(nblk); the finalize kernels sum the S rows themselves.
+// bn_collapse sums them into out[2*Cp] (fp64) -- the SyncBN path all-reduces that buffer (S = 1).
 int bn_reduce_splits(long nblk);
-void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, float* sums, double* tmp,
-                        hipStream_t s);
-void bn_finalize(const float* sums, int C, int Cp, float count, const float* gamma, const float* beta,
+void bn_reduce_partials(const float* part, long nblk, int width, int col_off, int Cp, double* tmp, hipStream_t s);
+void bn_collapse(const double* tmp, int S, int Cp, double* out, hipStream_t s);
+void bn_finalize(const double* tmp, int S, int C, int Cp, float count, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, int training,
                  float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
 void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
                   int relu, hipStream_t s);
 void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
                         const float* mean, float* part, long P, int Cp, int relu, hipStream_t s);
-void bn_bwd_finalize(const float* sums, int C, int Cp, float count, const float* scale,
+void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale,
                      const float* invstd, const float* mean, float* dgamma, float* dbeta,
                      float* coef, hipStream_t s);
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

@@ -133,6 +133,7 @@ class BaseConfig:
         self.graph_warmup = 3          # eager iterations before the hipGraph capture
         self.graph_ddp = False         # also capture multi-GPU steps (RCCL inside the graph)
         self.progress_bar = True
+        self.dist_group = None         # process sub-group (concurrent HPO trials); None = WORLD
 
     # ------------------------------------------------------------------
     def init_dependent_config(self):

@@ -39,9 +39,11 @@ class BaseTrainer:
         self.local_rank = int(os.getenv('LOCAL_RANK', -1))
         self.world_size = int(os.getenv('WORLD_SIZE', 1))
         config.DDP = self.local_rank != -1
-        self.main_rank = self.local_rank in [-1, 0]
-        self.logger = get_logger(config, self.main_rank)
         self.device = set_device(config, self.local_rank)
+        # main rank = rank 0 of this run's process group (a trial sub-group in concurrent HPO)
+        from ..utils.parallel import group_rank
+        self.main_rank = (group_rank(config) == 0) if config.DDP else True
+        self.logger = get_logger(config, self.main_rank)
         amp_fp16 = config.amp_training and config.amp_dtype == 'fp16' and self.device.type == 'cuda'
         self.scaler = torch.amp.GradScaler('cuda', enabled=amp_fp16)
         if self.main_rank:
@@ -100,7 +102,8 @@ class BaseTrainer:
             self.writer.flush()
             self.writer.close()
         if config.DDP:
-            torch.distributed.barrier()
+            from ..utils.parallel import get_group
+            torch.distributed.barrier(group=get_group(config))
         best_score = self.best_score
         if config.save_ckpt:
             best_score = self.val_best(config, self.val_loader)

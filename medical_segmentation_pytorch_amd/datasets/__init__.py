@@ -22,11 +22,11 @@ def _ensure_data(config):
     if want:
         root = config.data_root if config.data_root and config.data_root != '/path/to/your/dataset' \
             else os.path.join(config.save_dir, 'synthetic_polyp')
-        rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
-        if rank0:
+        from ..utils.parallel import get_group, group_rank
+        if group_rank(config) == 0:
             make_synthetic_polyp(root, config.synthetic_num, config.synthetic_size, config.random_seed)
-        if dist.is_available() and dist.is_initialized():
-            dist.barrier()
+        if get_group(config) is not None:
+            dist.barrier(group=get_group(config))
         config.data_root = root
 
 
@@ -51,7 +51,8 @@ def get_loader(config, rank, mode, pin_memory=True, drop_last=True):
     common = dict(num_workers=workers, worker_init_fn=seed_worker, persistent_workers=workers > 0)
     if config.DDP:
         from torch.utils.data.distributed import DistributedSampler
-        grank = dist.get_rank() if dist.is_initialized() else max(rank, 0)
+        from ..utils.parallel import group_rank
+        grank = group_rank(config) if dist.is_initialized() else max(rank, 0)
         sampler = DistributedSampler(dataset, num_replicas=config.gpu_num, rank=grank, shuffle=shuffle,
                                      seed=config.random_seed)
         return DataLoader(dataset, batch_size=bs, shuffle=False, pin_memory=pin_memory, sampler=sampler,

@@ -56,6 +56,20 @@ def _world(group):
     return dist.get_world_size(group)
 
 
+def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev):
+    """fp64 [S, 2*Cp] split sums (finalize kernels sum the S rows); SyncBN: collapsed to one row and
+    all-reduced across the group (one RCCL call of 2*Cp doubles)."""
+    S = C.bn_reduce_splits(nblk)
+    tmp = torch.empty(S, 2 * Cp, dtype=torch.float64, device=dev)
+    C.bn_reduce_partials(part, nblk, width, col_off, Cp, tmp)
+    if _world(group) > 1:
+        out = torch.empty(1, 2 * Cp, dtype=torch.float64, device=dev)
+        C.bn_collapse(tmp, Cp, out)
+        dist.all_reduce(out, group=group)
+        return out
+    return tmp
+
+
 class _BNAct(torch.autograd.Function):
     # inputs: st, relu, training, part_info, gamma, beta, *xs  (gamma/beta are inputs so that their
     # grads reach autograd when the engine gives no grad sink)
@@ -72,19 +86,15 @@ class _BNAct(torch.autograd.Function):
         b_ = beta.detach() if beta is not None else None
         y = torch.empty_like(y0) if len(xs) > 1 else y0
         if training:
-            sums = torch.empty(2, Cp, dtype=torch.float32, device=dev)
             if part_info is not None and len(xs) == 1:
                 part, width, col_off = part_info
-                C.bn_reduce_partials(part, part.shape[0], width, col_off, Cp, sums)
+                sums = _channel_sums(C, part, part.shape[0], width, col_off, Cp, st.group, dev)
             else:
                 nblk = C.bn_partial_blocks(P, Cp)
                 part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
                 C.sum_stats(xs, y if len(xs) > 1 else None, part, P, Cp)
-                C.bn_reduce_partials(part, nblk, Cp, 0, Cp, sums)
-            world = _world(st.group)
-            if world > 1:
-                dist.all_reduce(sums, group=st.group)
-            count = float(P * world)
+                sums = _channel_sums(C, part, nblk, Cp, 0, Cp, st.group, dev)
+            count = float(P * _world(st.group))
             C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
                           st.eps, True, stats)
             if st.count_nbt and st.num_batches_tracked is not None:
@@ -92,7 +102,7 @@ class _BNAct(torch.autograd.Function):
         else:
             if len(xs) > 1:
                 C.add_n(xs, y)
-            sums = torch.zeros(2, Cp, dtype=torch.float32, device=dev)
+            sums = torch.zeros(1, 2 * Cp, dtype=torch.float64, device=dev)
             C.bn_finalize(sums, st.C, Cp, 1.0, g_, b_, st.running_mean, st.running_var, st.momentum,
                           st.eps, False, stats)
             count = float(P)
@@ -114,10 +124,7 @@ class _BNAct(torch.autograd.Function):
         nblk = C.bn_partial_blocks(P, Cp)
         part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
         C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
-        sums = torch.empty(2, Cp, dtype=torch.float32, device=dev)
-        C.bn_reduce_partials(part, nblk, Cp, 0, Cp, sums)
-        if ctx.training and _world(st.group) > 1:
-            dist.all_reduce(sums, group=st.group)
+        sums = _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
         need_g = ctx.needs_input_grad[4] and st.weight_sink is None
         need_b = ctx.needs_input_grad[5] and st.bias_sink is None
         dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
@@ -131,10 +138,11 @@ class _BNAct(torch.autograd.Function):
             # eval-mode BN is a per-channel affine map: dx = dzr * scale
             coef[0] = stats[0]
             coef[1:] = 0
+            tot = sums.sum(0).float().view(2, Cp)
             if g_t is not None:
-                g_t[:st.C] += (sums[1] * stats[3])[:st.C]
+                g_t[:st.C] += (tot[1] * stats[3])[:st.C]
             if b_t is not None:
-                b_t[:st.C] += sums[0][:st.C]
+                b_t[:st.C] += tot[0][:st.C]
         dy = torch.empty_like(y)
         C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
         if st.ready_hook is not None:

@@ -32,8 +32,9 @@ def confmat_torch(preds, target, num_classes, ignore_index=None):
 
 
 class _ConfmatMetric(nn.Module):
-    def __init__(self, num_classes, ignore_index=None, sync=True):
+    def __init__(self, num_classes, ignore_index=None, sync=True, group=None):
         super().__init__()
+        self.group = group
         self.num_classes = num_classes
         self.ignore_index = ignore_index
         self.sync = sync
@@ -53,8 +54,8 @@ class _ConfmatMetric(nn.Module):
 
     def _synced(self):
         cm = self.confmat.clone()
-        if self.sync and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(cm)
+        if self.sync and dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(cm, group=self.group)
         return cm
 
     def reset(self):
@@ -108,9 +109,14 @@ def foreground_dice(preds, target, fg=1):
 
 
 def get_seg_metrics(config, metric_name):
+    nc = max(config.num_class, 2)          # num_class == 1 (sigmoid) is scored as background/foreground
+    group = getattr(config, 'dist_group', None)
     if metric_name == 'iou':
-        return JaccardIndex(task='multiclass', num_classes=config.num_class, ignore_index=config.ignore_index,
-                            average='none')
-    if metric_name == 'dice':
-        return Dice(num_classes=config.num_class, average='macro')
-    raise ValueError(f'Unsupported metric: {metric_name}.\n')
+        m = JaccardIndex(task='multiclass', num_classes=nc, ignore_index=config.ignore_index, average='none')
+    elif metric_name == 'dice':
+        m = Dice(num_classes=nc, average='macro')
+    else:
+        raise ValueError(f'Unsupported metric: {metric_name}.\n')
+    m.group = group
+    return m
+

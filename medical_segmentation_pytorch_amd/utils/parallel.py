@@ -34,6 +34,24 @@ class FusedModel(nn.Module):
         return self.executor(x, training=self.training)
 
 
+def get_group(config=None):
+    """Process group of this run: ``config.dist_group`` (a trial sub-group for concurrent HPO) or WORLD."""
+    g = getattr(config, 'dist_group', None) if config is not None else None
+    if g is not None:
+        return g
+    return dist.group.WORLD if dist.is_available() and dist.is_initialized() else None
+
+
+def group_size(config=None):
+    g = get_group(config)
+    return dist.get_world_size(g) if g is not None else 1
+
+
+def group_rank(config=None):
+    g = get_group(config)
+    return dist.get_rank(g) if g is not None else 0
+
+
 def is_parallel(model):
     return isinstance(model, (nn.parallel.DataParallel, nn.parallel.DistributedDataParallel, FusedModel))
 
@@ -52,7 +70,7 @@ def set_device(config, rank):
             kw = {'device_id': torch.device('cuda', rank)} if (use_gpu and backend == 'nccl') else {}
             dist.init_process_group(backend=backend, init_method='env://', **kw)
         device = torch.device('cuda', rank) if use_gpu else torch.device('cpu')
-        config.gpu_num = dist.get_world_size()
+        config.gpu_num = group_size(config)
     else:
         device = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
         config.gpu_num = max(torch.cuda.device_count(), 1)
@@ -76,10 +94,10 @@ def use_fused(config, model, device) -> bool:
 
 def parallel_model(config, model, rank, device, optimizer=None):
     if getattr(config, '_fused', False):
-        group = dist.group.WORLD if (config.DDP and dist.is_initialized()) else None
+        group = get_group(config) if config.DDP else None
         arena = getattr(optimizer, 'arena', None)
         bucketer = None
-        if group is not None and dist.get_world_size() > 1 and arena is not None:
+        if group is not None and dist.get_world_size(group) > 1 and arena is not None:
             from ..runtime.engine import GradBucketer
             bucketer = GradBucketer(arena, group, config.bucket_cap_mb)
             optimizer.attach_bucketer(bucketer)
@@ -89,11 +107,12 @@ def parallel_model(config, model, rank, device, optimizer=None):
     if config.DDP:
         if config.synBN and device.type == 'cuda':
             model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        pg = get_group(config)
         if device.type == 'cuda':
             model = DDP(model.to(device), device_ids=[rank], output_device=rank,
-                        bucket_cap_mb=config.bucket_cap_mb)
+                        bucket_cap_mb=config.bucket_cap_mb, process_group=pg)
         else:
-            model = DDP(model)
+            model = DDP(model, process_group=pg)
     elif device.type == 'cuda' and torch.cuda.device_count() > 1:
         model = nn.DataParallel(model)
         model.to(device)
@@ -101,7 +120,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
 
 
 def destroy_ddp_process(config):
-    if config.DDP and config.destroy_ddp_process and dist.is_initialized():
+    if config.DDP and config.destroy_ddp_process and dist.is_initialized() and \
+            getattr(config, 'dist_group', None) is None:
         dist.destroy_process_group()
 
 
