@@ -2,7 +2,7 @@
 
 Streamlit / plotly / OpenCV are not installable here, so the same application logic is exposed as
 (1) a CLI (images, image folders, or frame folders / GIFs as "video") and (2) an HTTP service on
-FastAPI + uvicorn (``python app.py --serve``; POST an image to ``/predict`` -> blended PNG, GET
+FastAPI + uvicorn (``python app.py --serve``; POST raw image bytes to ``/predict`` -> blended PNG, GET
 ``/metrics`` -> the PerformanceTracker table).  If streamlit IS importable, ``streamlit run app.py``
 shows the same controls as the reference.
 
@@ -198,13 +198,14 @@ class PolyPredictorApp:
 
 
 def make_server(app: PolyPredictorApp):
-    from fastapi import FastAPI, File, UploadFile
+    from fastapi import FastAPI, Request
     from fastapi.responses import JSONResponse, Response
     api = FastAPI(title='MI355X polyp segmentation')
 
     @api.post('/predict')
-    async def predict(file: UploadFile = File(...)):
-        image = Image.open(io.BytesIO(await file.read()))
+    async def predict(request: Request):
+        # raw image bytes in the body (multipart parsing needs python-multipart, not installed)
+        image = Image.open(io.BytesIO(await request.body()))
         _, blended = app.process_image(image)
         buf = io.BytesIO()
         Image.fromarray(blended).save(buf, format='PNG')

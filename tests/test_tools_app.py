@@ -36,6 +36,6 @@ def test_app_cli_and_server(tmp_path):
     import io
     buf = io.BytesIO()
     img.save(buf, format='PNG')
-    r = client.post('/predict', files={'file': ('a.png', buf.getvalue(), 'image/png')})
+    r = client.post('/predict', content=buf.getvalue(), headers={'content-type': 'image/png'})
     assert r.status_code == 200 and r.headers['content-type'] == 'image/png'
     assert client.get('/metrics').status_code == 200
