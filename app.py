@@ -13,7 +13,6 @@ sigmoid > 0.5 when ``num_class == 1`` else argmax; colour overlay blended 0.7/0.
 (mean/min/max/std ms) for preprocessing, inference and visualisation.  Checkpoints are read with
 ``torch.load(weights_only=True)``.  On MI355X the native models run on the fused HIP executor.
 """
-from __future__ import annotations
 
 import argparse
 import io
