@@ -81,6 +81,10 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cur_stream());
 }
 
+bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  return conv_uses_halo(make_geom(dims, dy, dx), trans);
+}
+
 int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
   return conv_stat_blocks(make_geom(dims, dy, dx));
 }
@@ -298,6 +302,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);
   m.def("conv_stat_blocks", &conv_stat_blocks_t);
+  m.def("conv_uses_halo", &conv_uses_halo_t);
+  m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);
   m.def("unpack_wgrad", &unpack_wgrad_t);
   m.def("pack_batch", &pack_batch_t);

@@ -98,25 +98,43 @@ __global__ void reduce_partials_stage2(const double* __restrict__ tmp, int split
 }
 
 // sum of the S split rows of column i (fixed order -> deterministic)
-DEVI double split_sum(const double* __restrict__ tmp, int S, int ncol, int i) {
-  double s = 0.0;
-  for (int k = 0; k < S; ++k) s += tmp[(long)k * ncol + i];
-  return s;
+// Finalize kernels: a block owns kFinCols channels; its kFinParts waves each sum a strided subset of
+// the S split rows (independent loads in flight), then the parts are combined in a fixed order
+// (deterministic).  Returns (sum, second-column sum) for channel c in lanes of part 0.
+constexpr int kFinCols = 64, kFinParts = 4;
+
+DEVI void split_sum2(const double* __restrict__ tmp, int S, int Cp, int c, bool valid, double& a, double& b) {
+  __shared__ double red[2][kFinParts][kFinCols];
+  const int cl = threadIdx.x % kFinCols, pt = threadIdx.x / kFinCols;
+  double sa = 0.0, sb = 0.0;
+  if (valid) {
+#pragma unroll 4
+    for (int k = pt; k < S; k += kFinParts) {
+      sa += tmp[(long)k * 2 * Cp + c];
+      sb += tmp[(long)k * 2 * Cp + Cp + c];
+    }
+  }
+  red[0][pt][cl] = sa; red[1][pt][cl] = sb;
+  __syncthreads();
+  a = 0.0; b = 0.0;
+#pragma unroll
+  for (int i = 0; i < kFinParts; ++i) { a += red[0][i][cl]; b += red[1][i][cl]; }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ tmp, int S, int C, int Cp, float count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
-                                   float eps, int training, float* __restrict__ scale,
-                                   float* __restrict__ shift, float* __restrict__ mean_out,
-                                   float* __restrict__ invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cp) return;
+__global__ __launch_bounds__(kFinCols * kFinParts) void bn_finalize_kernel(
+    const double* __restrict__ tmp, int S, int C, int Cp, float count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
+    int training, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * kFinCols + (int)(threadIdx.x % kFinCols);
+  double sm = 0.0, sq = 0.0;
+  if (training) split_sum2(tmp, S, Cp, c, c < C, sm, sq);
+  if (threadIdx.x >= kFinCols || c >= Cp) return;
   if (c >= C) { scale[c] = 0.f; shift[c] = 0.f; mean_out[c] = 0.f; invstd_out[c] = 0.f; return; }
   float mean, var;
   if (training) {
-    const double m = split_sum(tmp, S, 2 * Cp, c) / count;
-    double v = split_sum(tmp, S, 2 * Cp, Cp + c) / count - m * m;
+    const double m = sm / count;
+    double v = sq / count - m * m;
     if (v < 0) v = 0;
     mean = (float)m; var = (float)v;
     if (rmean != nullptr) {
@@ -206,14 +224,16 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
 
 // coef[3][Cp]: dy = k1*dzr + k2*y + k3  (k1 = gamma*invstd, k2 = -k1*invstd*sum(dzr*xmu)/M,
 // k3 = -k1*sum(dzr)/M - k2*mean).  dgamma/dbeta are ACCUMULATED into the fp32 parameter grads.
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ tmp, int S, int C, int Cp, float count,
-                                       const float* __restrict__ scale, const float* __restrict__ invstd,
-                                       const float* __restrict__ mean, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cp) return;
+__global__ __launch_bounds__(kFinCols * kFinParts) void bn_bwd_finalize_kernel(
+    const double* __restrict__ tmp, int S, int C, int Cp, float count, const float* __restrict__ scale,
+    const float* __restrict__ invstd, const float* __restrict__ mean, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * kFinCols + (int)(threadIdx.x % kFinCols);
+  double a, b;
+  split_sum2(tmp, S, Cp, c, c < C, a, b);
+  if (threadIdx.x >= kFinCols || c >= Cp) return;
   if (c >= C) { coef[c] = 0.f; coef[Cp + c] = 0.f; coef[2 * Cp + c] = 0.f; return; }
-  const float sd = (float)split_sum(tmp, S, 2 * Cp, c), sdx = (float)split_sum(tmp, S, 2 * Cp, Cp + c);
+  const float sd = (float)a, sdx = (float)b;
   if (dgamma != nullptr) dgamma[c] += sdx * invstd[c];
   if (dbeta != nullptr) dbeta[c] += sd;
   const float k1 = scale[c];
@@ -287,7 +307,7 @@ void bn_collapse(const double* tmp, int S, int Cp, double* out, hipStream_t s) {
 void bn_finalize(const double* tmp, int S, int C, int Cp, float count, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, int training,
                  float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, tmp, S, C, Cp, count, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp, count, gamma, beta,
                      running_mean, running_var, momentum, eps, training, scale, shift, mean, invstd);
 }
 
@@ -306,7 +326,7 @@ void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scal
 
 void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale, const float* invstd,
                      const float* mean, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, 256)), dim3(256), 0, s, tmp, S, C, Cp, count, scale,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp, count, scale,
                      invstd, mean, dgamma, dbeta, coef);
 }
 

@@ -79,11 +79,20 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
 
   const long OHW = (long)g.OH * g.OW;
   const long M = (long)g.N * OHW;
-  const long m0 = ((long)blockIdx.x * WPX + wave) * (16 * NJ);
-  const int co0 = blockIdx.y * (16 * MI);
+  const int rows = g.Go * g.Cgo;
+  // 1-D grid, XCD-aware: blocks sharing a pixel tile (all co tiles of it) get consecutive logical
+  // ids placed on ONE XCD (bijective remap of the round-robin dispatch, guide T1), so the input
+  // tile is fetched into that XCD's L2 once and re-read from there by the other co tiles.
+  const int n_co = (rows + 16 * MI - 1) / (16 * MI);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int co_t = wgid % n_co;
+  const long px_t = wgid / n_co;
+  const long m0 = (px_t * WPX + wave) * (16 * NJ);
+  const int co0 = co_t * (16 * MI);
   const int lr = lane & 15, lg = lane >> 4;
   const int IHW = g.IH * g.IW;
-  const int rows = g.Go * g.Cgo;
 
   int pn[NJ], ph[NJ], pw[NJ];
 #pragma unroll
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
         if (lr == 0) { s_stat[wave][0][16 * i + 4 * lg + r] = s; s_stat[wave][1][16 * i + 4 * lg + r] = q; }
       }
     __syncthreads();
-    const long blk = (long)blockIdx.x;
+    const long blk = px_t;
     for (int c = tid; c < 16 * MI; c += 64 * WPX) {
       const int co = co0 + c;
       if (co < rows) {
@@ -359,6 +368,8 @@ constexpr int DW_LD = DW_CH + 4;        // LDS pixel pitch (bf16 elems): 72 B, 8
 
 struct DwTile { int TH, TW, ey0, ex0, HH, HWd, tiles_y, tiles_x; };
 
+constexpr int kDwLd = 8;
+
 template <int NPW>
 __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
                                                               DwTile tl, int KT, long ntiles) {
@@ -401,26 +412,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
     const int rem = (int)(tix - (long)n * per_img);
     const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
     __syncthreads();   // previous tile's LDS reads are done
-    // ---- stage dY tile (pixels beyond the image -> 0)
-    for (int px = vp; px < nslice * 32; px += 64) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      const int ty = px / tl.TW, tx = px - (px / tl.TW) * tl.TW;
-      const int oy = y0 + ty, ox = x0 + tx;
-      if (px < npx && y_ok && oy < g.OH && ox < g.OW)
-        v = *reinterpret_cast<const uint4*>(y_base + ((long)n * g.OH * g.OW + (long)oy * g.OW + ox) * g.Cgo);
-      *reinterpret_cast<uint2*>(&sY[px * DW_LD + 8 * vv]) = make_uint2(v.x, v.y);
-      *reinterpret_cast<uint2*>(&sY[px * DW_LD + 8 * vv + 4]) = make_uint2(v.z, v.w);
-    }
-    // ---- stage input halo (zero padding outside the image)
-    const int nh = tl.HH * tl.HWd;
-    for (int hp = vp; hp < nh; hp += 64) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      const int hy = hp / tl.HWd, hx = hp - (hp / tl.HWd) * tl.HWd;
-      const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
-      if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
-        v = *reinterpret_cast<const uint4*>(x_base + ((long)n * g.IH * g.IW + (long)iy * g.IW + ix) * g.Cgi);
-      *reinterpret_cast<uint2*>(&sX[hp * DW_LD + 8 * vv]) = make_uint2(v.x, v.y);
-      *reinterpret_cast<uint2*>(&sX[hp * DW_LD + 8 * vv + 4]) = make_uint2(v.z, v.w);
+    // ---- stage dY tile (pixels beyond the image -> 0) and the input halo (zero padding outside the
+    // image); kDwLd loads in flight per thread before the LDS writes of each batch.
+    const int nyp = nslice * 32, nh = tl.HH * tl.HWd;
+    for (int base = vp; base < nyp + nh; base += 64 * kDwLd) {
+      uint4 v[kDwLd];
+      int dst[kDwLd];
+#pragma unroll
+      for (int u = 0; u < kDwLd; ++u) {
+        const int e = base + 64 * u;
+        v[u] = make_uint4(0, 0, 0, 0);
+        dst[u] = -1;
+        if (e < nyp) {
+          const int px = e;
+          const int ty = px / tl.TW, tx = px - (px / tl.TW) * tl.TW;
+          const int oy = y0 + ty, ox = x0 + tx;
+          dst[u] = px * DW_LD + 8 * vv;
+          if (px < npx && y_ok && oy < g.OH && ox < g.OW)
+            v[u] = *reinterpret_cast<const uint4*>(y_base + ((long)n * g.OH * g.OW + (long)oy * g.OW + ox) * g.Cgo);
+        } else if (e < nyp + nh) {
+          const int hp = e - nyp;
+          const int hy = hp / tl.HWd, hx = hp - (hp / tl.HWd) * tl.HWd;
+          const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
+          dst[u] = (int)(sX - sY) + hp * DW_LD + 8 * vv;
+          if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+            v[u] = *reinterpret_cast<const uint4*>(x_base + ((long)n * g.IH * g.IW + (long)iy * g.IW + ix) * g.Cgi);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kDwLd; ++u) {
+        if (dst[u] < 0) continue;
+        *reinterpret_cast<uint2*>(&sY[dst[u]]) = make_uint2(v[u].x, v[u].y);
+        *reinterpret_cast<uint2*>(&sY[dst[u] + 4]) = make_uint2(v[u].z, v[u].w);
+      }
     }
     __syncthreads();
     for (int sl = 0; sl < nslice; ++sl) {
@@ -524,20 +548,194 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Halo-tiled direct convolution (stride 1, non-TRANS): forward of every stride-1 conv and the
+// data-gradient of every stride-1 conv whose (summed) input width fits the LDS tile.
+// A block owns a TH x TW output-pixel tile of one image and ALL output rows.  The input tile plus its
+// tap halo (all Cip channels, zero outside the image) is staged once in LDS with a pixel pitch of an
+// odd number of 16-B slots, so the 16 consecutive pixels of a ds_read_b128 hit distinct banks.  Every
+// 32-wide k-chunk then reads its B fragment at  pixel_base(lane) + koff[chunk][lane>>4]  -- one
+// table lookup replaces the per-lane tap/bounds arithmetic of the gather kernel, and the input is read
+// from HBM once per tile (halo overhead (TH+ey)(TW+ex)/(TH*TW)) instead of once per tap from L2.
+// Waves split the tile's pixels (NJ 16-pixel columns each) and loop over the 16*MI-row groups.
+struct HaloGeom { int TH, TW, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, KC; };
+
+constexpr int kHaloMaxKC = 64;
+constexpr int kHaloWaves = 4;
+constexpr int kHaloMaxRows = 512;
+constexpr int kHaloLd = 8;
+
+template <int MI, int NJ>
+__global__ __launch_bounds__(64 * kHaloWaves, 3) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+  extern __shared__ uint4 halo_smem[];
+  uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
+  __shared__ int s_koff[kHaloMaxKC * 4];
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Cip = g.Gi * g.Cgi, C8 = Cip >> 3;
+  const int rows = g.Go * g.Cgo;
+  // per-wave (sum, sum^2) rows after the tile (+ zero slot): [kHaloWaves][2][rows] fp32
+  float* s_stat = reinterpret_cast<float*>(tile + hg.HH * hg.HWD * hg.pitch + 8);
+
+  // XCD-aware bijective remap: neighbouring tiles (shared halo rows) land on one XCD's L2.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int per_img = hg.tiles_y * hg.tiles_x;
+  const int n = wgid / per_img;
+  const int trem = wgid - n * per_img;
+  const int ty0 = (trem / hg.tiles_x) * hg.TH, tx0 = (trem % hg.tiles_x) * hg.TW;
+
+  // ---- stage the halo tile: 16 B per element, kHaloLd loads in flight per thread before any LDS
+  // write (a load->store loop would serialise one HBM latency per iteration).
+  const int hpx = hg.HH * hg.HWD;
+  const long img = (long)n * g.IH * g.IW;
+  const int total = hpx * C8;
+  for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
+    uint4 v[kHaloLd];
+    int dst[kHaloLd];
+#pragma unroll
+    for (int u = 0; u < kHaloLd; ++u) {
+      const int idx = base + u * 64 * kHaloWaves;
+      v[u] = make_uint4(0, 0, 0, 0);
+      dst[u] = -1;
+      if (idx < total) {
+        const int hp = idx / C8, c8 = idx - hp * C8;
+        const int hy = hp / hg.HWD, hx = hp - hy * hg.HWD;
+        const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
+        dst[u] = hp * hg.pitch + c8 * 8;
+        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
+          const int ci = c8 * 8, gi = ci / g.Cgi, cl = ci - gi * g.Cgi;
+          v[u] = *reinterpret_cast<const uint4*>(a.x[gi] + (img + (long)iy * g.IW + ix) * g.Cgi + cl);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kHaloLd; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<uint4*>(tile + dst[u]) = v[u];
+  }
+  const int zero_off = hpx * hg.pitch;  // one zeroed 16-B slot for k beyond T*Cip
+  if (tid == 0) *reinterpret_cast<uint4*>(tile + zero_off) = make_uint4(0, 0, 0, 0);
+  for (int e = tid; e < hg.KC * 4; e += 64 * kHaloWaves) {
+    const int kk = 32 * (e >> 2) + 8 * (e & 3);
+    int off = -1;
+    if (kk < g.T * Cip) {
+      const int t = kk / Cip, ci = kk - t * Cip;
+      off = ((g.dy[t] - hg.ey0) * hg.HWD + (g.dx[t] - hg.ex0)) * hg.pitch + ci;
+    }
+    s_koff[e] = off;
+  }
+  __syncthreads();
+
+  int pb[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int p = (wave * NJ + j) * 16 + lr;
+    const int ty = p / hg.TW, tx = p - (p / hg.TW) * hg.TW;
+    pb[j] = (ty * hg.HWD + tx) * hg.pitch;
+  }
+
+  const int n_rg = (rows + 16 * MI - 1) / (16 * MI);
+  for (int rg = 0; rg < n_rg; ++rg) {
+    const int co0 = rg * 16 * MI;
+    const uint16_t* wrow[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + 8 * lg;
+    f32x4_t acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint4 A[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i]);
+    for (int kc = 0; kc < hg.KC; ++kc) {
+      uint4 An[MI];
+      const bool more = kc + 1 < hg.KC;
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) An[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * (kc + 1));
+      }
+      const int ko = s_koff[kc * 4 + lg];
+      uint4 B[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + (ko >= 0 ? pb[j] + ko : zero_off));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) A[i] = An[i];
+      }
+    }
+    // epilogue: bias, bf16 round, 8-B NHWC stores, per-row (sum, sum^2) of the stored values
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+      const int cb = co0 + 16 * i + 4 * lg;
+      if (cb < rows) {
+        const int og = cb / g.Cgo, cl = cb - (cb / g.Cgo) * g.Cgo;
+        uint16_t* yb = a.y[og] + cl;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = (a.bias != nullptr && cl + r < g.Cgo_l) ? a.bias[cl + r] : 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int p = (wave * NJ + j) * 16 + lr;
+          const int ty = ty0 + p / hg.TW, tx = tx0 + p % hg.TW;
+          if (ty >= g.OH || tx >= g.OW) continue;
+          const long pm = img + (long)ty * g.OW + tx;   // OH == IH, OW == IW
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
+            v[r] = bf2f(f2bf(o));
+            cs[r] += v[r];
+            cq[r] += v[r] * v[r];
+          }
+          *reinterpret_cast<uint2*>(yb + pm * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+      if (a.stat_part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s = cs[r], q = cq[r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+          if (lr == 0 && cb + r < rows) { s_stat[(wave * 2 + 0) * rows + cb + r] = s; s_stat[(wave * 2 + 1) * rows + cb + r] = q; }
+        }
+      }
+    }
+  }
+  if (a.stat_part != nullptr) {
+    __syncthreads();
+    for (int c = tid; c < rows; c += 64 * kHaloWaves) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < kHaloWaves; ++wv) { s += s_stat[(wv * 2 + 0) * rows + c]; q += s_stat[(wv * 2 + 1) * rows + c]; }
+      a.stat_part[((long)wgid * 2 + 0) * rows + c] = s;
+      a.stat_part[((long)wgid * 2 + 1) * rows + c] = q;
+    }
+  }
+}
+
 template <int MI, int NJ, int WPX, bool TRANS>
 void launch_igemm(const ConvArgs& a, hipStream_t s) {
   const long M = (long)a.g.N * a.g.OH * a.g.OW;
-  dim3 grid(cdiv(M, 16 * NJ * WPX), cdiv(a.g.Go * a.g.Cgo, 16 * MI));
-  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS>), grid, dim3(64 * WPX), 0, s, a);
+  const long blocks = (long)cdiv(M, 16 * NJ * WPX) * cdiv(a.g.Go * a.g.Cgo, 16 * MI);
+  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS>), dim3((unsigned)blocks), dim3(64 * WPX), 0, s, a);
 }
 
 template <bool TRANS>
-void dispatch_igemm(const ConvArgs& a, int mi, int wpx, hipStream_t s) {
-#define CASE(MI_, WPX_)                                         \
-  if (mi == MI_ && wpx == WPX_) { launch_igemm<MI_, 4, WPX_, TRANS>(a, s); return; }
-  CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
-  CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
-  CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1)
+void dispatch_igemm(const ConvArgs& a, int mi, int nj, int wpx, hipStream_t s) {
+#define CASE(MI_, NJ_, WPX_)                                                  \
+  if (mi == MI_ && nj == NJ_ && wpx == WPX_) { launch_igemm<MI_, NJ_, WPX_, TRANS>(a, s); return; }
+  CASE(1, 4, 4) CASE(2, 4, 4) CASE(3, 4, 4) CASE(4, 4, 4)
+  CASE(1, 4, 2) CASE(2, 4, 2) CASE(3, 4, 2) CASE(4, 4, 2)
+  CASE(1, 4, 1) CASE(2, 4, 1) CASE(3, 4, 1) CASE(4, 4, 1)
+  CASE(1, 8, 4) CASE(2, 8, 4) CASE(1, 8, 2) CASE(2, 8, 2) CASE(1, 8, 1) CASE(2, 8, 1)
 #undef CASE
 }
 
@@ -564,26 +762,112 @@ int conv_pick_mi(int rows) {
 
 int conv_rows_alloc(int rows) { const int mi = conv_pick_mi(rows); return cdiv(rows, 16 * mi) * 16 * mi; }
 
-static int conv_pick_wpx(const ConvGeom& g, int mi) {
+// Pixels per wave: 128 (NJ = 8) for narrow outputs (<= 32 rows) with plenty of pixels -- amortises the
+// weight-fragment loads and doubles the MFMAs per pixel-operand load; else 64.
+static int conv_pick_nj(const ConvGeom& g, int mi) {
+  const long M = (long)g.N * g.OH * g.OW;
+  return (mi <= 2 && M >= 256L * 1024) ? 8 : 4;
+}
+
+static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
   const long M = (long)g.N * g.OH * g.OW;
   const long co_tiles = cdiv(g.Go * g.Cgo, 16 * mi);
   for (int wpx = 4; wpx > 1; wpx >>= 1)
-    if ((long)cdiv(M, 64 * wpx) * co_tiles >= 1024) return wpx;
+    if ((long)cdiv(M, 16 * nj * wpx) * co_tiles >= 1024) return wpx;
   return 1;
 }
 
+// Halo-kernel eligibility + tile geometry.  Pixel tile = 4 waves x NJ x 16 pixels (NJ = 8 for
+// MI <= 2, else 4); TW in {16, 32, 64} chosen to minimise (padded tile area) x (halo overhead).
+static int halo_nj(int mi) { return mi <= 2 ? 8 : 4; }
+
+static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
+  if (trans || g.stride != 1 || g.OH != g.IH || g.OW != g.IW) return false;
+  const int rows = g.Go * g.Cgo;
+  if (rows > kHaloMaxRows || g.T > kMaxTaps) return false;
+  const int Cip = g.Gi * g.Cgi;
+  if (Cip % 8 != 0 || g.Cgi % 8 != 0) return false;
+  const int KC = g.Kp / 32;
+  if (KC > kHaloMaxKC || g.Kp % 32 != 0) return false;
+  int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
+  for (int t = 0; t < g.T; ++t) {
+    ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
+    ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
+  }
+  const int mi = conv_pick_mi(rows);
+  const int tp = kHaloWaves * halo_nj(mi) * 16;
+  int c8 = Cip / 8;
+  if ((c8 & 1) == 0) ++c8;
+  const int pitch = 8 * c8;
+  double best = 1e30;
+  bool found = false;
+  for (int tw = 16; tw <= 64; tw *= 2) {
+    const int th = tp / tw;
+    const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
+    const size_t lds = ((size_t)HH * HWD * pitch + 8) * 2 + (size_t)kHaloWaves * 2 * rows * 4;
+    if (lds > 64 * 1024) continue;
+    const double tiles = (double)cdiv(g.OH, th) * cdiv(g.OW, tw);
+    const double cost = tiles * ((double)tp + 0.5 * (double)HH * HWD);   // stores + halo loads
+    if (cost < best) {
+      best = cost; found = true;
+      hg.TH = th; hg.TW = tw; hg.HH = HH; hg.HWD = HWD;
+    }
+  }
+  if (!found) return false;
+  hg.ey0 = ey0; hg.ex0 = ex0;
+  hg.tiles_y = cdiv(g.OH, hg.TH);
+  hg.tiles_x = cdiv(g.OW, hg.TW);
+  hg.pitch = pitch;
+  hg.KC = KC;
+  return true;
+}
+
+static size_t halo_lds(const HaloGeom& hg, int rows) {
+  return ((size_t)hg.HH * hg.HWD * hg.pitch + 8) * 2 + (size_t)kHaloWaves * 2 * rows * 4;
+}
+
+static int g_halo_mode = -1;   // -1: from MSP_CONV_HALO (default on), 0: off, 1: on
+
+static bool halo_enabled() {
+  if (g_halo_mode < 0) { const char* e = getenv("MSP_CONV_HALO"); g_halo_mode = (e == nullptr || e[0] != '0') ? 1 : 0; }
+  return g_halo_mode == 1;
+}
+
+void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
+bool conv_uses_halo(const ConvGeom& g, bool trans) {
+  HaloGeom hg;
+  return halo_enabled() && conv_halo_ok(g, trans, hg);
+}
+
 long conv_stat_blocks(const ConvGeom& g) {
+  HaloGeom hg;
+  if (halo_enabled() && conv_halo_ok(g, false, hg)) return (long)g.N * hg.tiles_y * hg.tiles_x;
   const int mi = conv_pick_mi(g.Go * g.Cgo);
-  const int wpx = conv_pick_wpx(g, mi);
+  const int nj = conv_pick_nj(g, mi);
+  const int wpx = conv_pick_wpx(g, mi, nj);
   const long M = (long)g.N * g.OH * g.OW;
-  return cdiv(M, 64 * wpx);
+  return cdiv(M, 16 * nj * wpx);
 }
 
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   const int mi = conv_pick_mi(a.g.Go * a.g.Cgo);
-  const int wpx = conv_pick_wpx(a.g, mi);
-  if (trans) dispatch_igemm<true>(a, mi, wpx, s);
-  else dispatch_igemm<false>(a, mi, wpx, s);
+  HaloGeom hg;
+  if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
+    const unsigned blocks = (unsigned)((long)a.g.N * hg.tiles_y * hg.tiles_x);
+    const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo);
+#define HC_(MI_)                                                                                          \
+    if (mi == MI_) {                                                                                      \
+      hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4)>), dim3(blocks), dim3(64 * kHaloWaves), \
+                         lds, s, a, hg);                                                                  \
+      return;                                                                                             \
+    }
+    HC_(1) HC_(2) HC_(3) HC_(4)
+#undef HC_
+  }
+  const int nj = conv_pick_nj(a.g, mi);
+  const int wpx = conv_pick_wpx(a.g, mi, nj);
+  if (trans) dispatch_igemm<true>(a, mi, nj, wpx, s);
+  else dispatch_igemm<false>(a, mi, nj, wpx, s);
 }
 
 static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {

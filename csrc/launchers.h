@@ -37,6 +37,8 @@ struct ConvArgs {
 // conv.hip
 int conv_pick_mi(int rows);
 int conv_rows_alloc(int rows);
+void conv_set_halo(int on);
+bool conv_uses_halo(const ConvGeom& g, bool trans);
 long conv_stat_blocks(const ConvGeom& g);
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)

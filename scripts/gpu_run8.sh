@@ -1,0 +1,13 @@
+#!/bin/bash
+# batched halo staging: numerics + per-layer bench + model bench
+set -o pipefail
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_gpu_kernels.py -x -q > gpurun_out/t8_kernels.log 2>&1; rc=$?; echo "kernel tests exit $rc" >> gpurun_out/status8.txt
+tail -2 gpurun_out/t8_kernels.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/conv_bench.py --halo 1 > gpurun_out/cb8_halo.log 2>&1 || exit $?
+grep -v "^{" gpurun_out/cb8_halo.log | cut -c1-120
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b8_bs16.json 2>gpurun_out/b8_bs16.err || exit $?
+cat gpurun_out/b8_bs16.json

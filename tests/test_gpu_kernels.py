@@ -285,3 +285,54 @@ def test_confmat(gpu):
     valid = tgt != 255
     ref = torch.bincount(tgt[valid] * 3 + pred[valid], minlength=9).view(3, 3)
     assert torch.equal(cm, ref)
+
+
+HALO_CASES = [
+    # N, H, W, Cin, Cout, (kh, kw), pad, dil, Go   (stride 1; partial tiles in both dims)
+    (2, 70, 90, 17, 17, (3, 3), (1, 1), (1, 1), 1),
+    (1, 45, 37, 34, 34, (3, 3), (3, 3), (3, 3), 1),
+    (2, 33, 50, 17, 17, (1, 7), (0, 3), (1, 1), 1),
+    (1, 40, 29, 68, 68, (7, 1), (3, 0), (1, 1), 1),
+    (2, 44, 44, 17, 17, (3, 3), (1, 1), (1, 1), 8),
+    (1, 22, 22, 34, 34, (3, 3), (1, 1), (1, 1), 3),
+    (2, 19, 23, 8, 40, (3, 3), (1, 1), (1, 1), 1),
+]
+
+
+@pytest.mark.parametrize('case', HALO_CASES)
+def test_conv_halo_matches_gather(gpu, case):
+    """The halo-tiled stride-1 kernel vs the gather igemm kernel (same packed operands) and vs fp32."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    C = _ext.require()
+    n, h, w, ci, co, (kh, kw), pad, dil, go = case
+    torch.manual_seed(4)
+    convs = [nn.Conv2d(ci, co, (kh, kw), 1, pad, dil, bias=False).to(gpu) for _ in range(go)]
+    plan = ConvPlan(kh, kw, ci, co, [Branch(c.weight, g, 0, kh * kw) for g, c in enumerate(convs)], padding=pad,
+                    dilation=dil, Go=go)
+    x = _bf(torch.randn(n, ci, h, w, device=gpu))
+    dims = plan.fwd_dims(n, h, w, h, w)
+    dy, dx = [t[0] for t in plan.taps_fwd], [t[1] for t in plan.taps_fwd]
+    assert C.conv_uses_halo(dims, dy, dx, False), 'case must exercise the halo kernel'
+    outs = {}
+    for mode in (True, False):
+        C.conv_set_halo(mode)
+        try:
+            xf = to_fm_reference(x).requires_grad_(True)
+            ys, part = conv(plan, [xf], want_stats=True)
+            gs = [to_fm_reference(_bf(torch.randn(n, co, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(9 + i))))
+                  for i in range(go)]
+            torch.autograd.backward(ys, gs)
+            outs[mode] = ([y.float() for y in ys], part.sum(0), xf.grad.float(), [c.weight.grad.clone() for c in convs])
+            for c in convs:
+                c.weight.grad = None
+        finally:
+            C.conv_set_halo(True)
+    (yh, ph, dxh, wh), (yg, pg, dxg, wg) = outs[True], outs[False]
+    for a, b, cv in zip(yh, yg, convs):
+        assert _rel(a, b) < 5e-3
+        ref = F.conv2d(x, _bf(cv.weight.detach()), None, 1, pad, dil)
+        assert _rel(from_fm_reference(a.to(torch.bfloat16), co), ref) < 1e-2
+    assert _rel(ph, pg) < 1e-3
+    assert _rel(dxh, dxg) < 5e-3
+    for a, b in zip(wh, wg):
+        assert _rel(a, b) < 5e-3

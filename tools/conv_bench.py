@@ -51,13 +51,18 @@ def main():
     ap.add_argument('--size', type=int, default=352)
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--miopen', action='store_true')
+    ap.add_argument('--halo', type=int, default=1, help='1: halo-tiled stride-1 kernel where eligible, 0: gather only')
+    ap.add_argument('--only', default='', help='substring filter on layer names')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     from medical_segmentation_pytorch_amd.ops import _ext
     C = _ext.require()
+    C.conv_set_halo(bool(a.halo))
     res = []
     tot = {'fwd': 0.0, 'dgrad': 0.0, 'wgrad': 0.0}
     for name, lvl, ci, co, k, s, p, d, groups in layers():
+        if a.only and a.only not in name:
+            continue
         hw = a.size >> lvl
         n = a.batch
         convs = [nn.Conv2d(ci, co, k, s, p, d, bias=False).to(dev) for _ in range(groups)]
@@ -89,12 +94,14 @@ def main():
             xm = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
             wm = torch.randn(co * groups, ci, *k, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
             row['miopen_fwd_ms'] = round(timeit(lambda: F.conv2d(xm, wm, None, s, p, d), a.iters), 4)
+        row['halo_fwd'] = bool(C.conv_uses_halo(dims, dy, dx, False))
+        row['halo_dgrad'] = bool(C.conv_uses_halo(dims_d, bdy, bdx, s > 1))
         res.append(row)
         tot['fwd'] += t_f; tot['dgrad'] += t_d; tot['wgrad'] += t_w
         print(f"{name:28s} fwd {t_f:7.3f} ms ({row['fwd_tflops']:6.1f} TF)  dgrad {t_d:7.3f} ({row['dgrad_tflops']:6.1f})"
               f"  wgrad {t_w:7.3f} ({row['wgrad_tflops']:6.1f})" +
               (f"  miopen-fwd {row['miopen_fwd_ms']:7.3f}" if a.miopen else ''), flush=True)
-    print(json.dumps({'batch': a.batch, 'size': a.size, 'layers': res, 'totals_ms': tot}))
+    print(json.dumps({'batch': a.batch, 'size': a.size, 'halo': a.halo, 'layers': res, 'totals_ms': tot}))
 
 
 if __name__ == '__main__':
