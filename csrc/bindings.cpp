@@ -177,12 +177,12 @@ void bn_act_bwd_partial_t(const at::Tensor& dz, const at::Tensor& y, const at::T
 
 void bn_bwd_finalize_t(const at::Tensor& tmp, int64_t C, int64_t Cp, double count, const at::Tensor& stats,
                        const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
-                       const at::Tensor& coef) {
+                       const at::Tensor& coef, double pscale) {
   CHECK_F64(tmp); CHECK_F32(stats); CHECK_F32(coef);
   TORCH_CHECK(coef.numel() == 3 * Cp && stats.numel() == 4 * Cp && tmp.numel() % (2 * Cp) == 0);
   const float* st = f32(stats);
   bn_bwd_finalize(tmp.data_ptr<double>(), (int)(tmp.numel() / (2 * Cp)), C, Cp, (float)count, st, st + 3 * Cp,
-                  st + 2 * Cp, f32_opt_mut(dgamma), f32_opt_mut(dbeta), f32(coef), cur_stream());
+                  st + 2 * Cp, f32_opt_mut(dgamma), f32_opt_mut(dbeta), f32(coef), (float)pscale, cur_stream());
 }
 
 void bn_act_bwd_apply_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& coef,
@@ -316,7 +316,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_finalize", &bn_finalize_t);
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
-  m.def("bn_bwd_finalize", &bn_bwd_finalize_t);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),
+        py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("pscale") = 1.0);
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
   m.def("nchw_to_nhwc", &nchw_to_nhwc_t);
   m.def("nhwc_to_nchw", &nhwc_to_nchw_t);

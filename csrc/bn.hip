@@ -227,15 +227,17 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
 __global__ __launch_bounds__(kFinCols * kFinParts) void bn_bwd_finalize_kernel(
     const double* __restrict__ tmp, int S, int C, int Cp, float count, const float* __restrict__ scale,
     const float* __restrict__ invstd, const float* __restrict__ mean, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ coef) {
+    float* __restrict__ dbeta, float* __restrict__ coef, float pscale) {
   const int c = blockIdx.x * kFinCols + (int)(threadIdx.x % kFinCols);
   double a, b;
   split_sum2(tmp, S, Cp, c, c < C, a, b);
   if (threadIdx.x >= kFinCols || c >= Cp) return;
   if (c >= C) { coef[c] = 0.f; coef[Cp + c] = 0.f; coef[2 * Cp + c] = 0.f; return; }
   const float sd = (float)a, sdx = (float)b;
-  if (dgamma != nullptr) dgamma[c] += sdx * invstd[c];
-  if (dbeta != nullptr) dbeta[c] += sd;
+  // SyncBN: the sums are global; dgamma/dbeta take pscale = 1/world of them so that the DDP-style
+  // average over ranks (sum all-reduce * 1/world) yields the mean of the per-rank local gradients.
+  if (dgamma != nullptr) dgamma[c] += pscale * sdx * invstd[c];
+  if (dbeta != nullptr) dbeta[c] += pscale * sd;
   const float k1 = scale[c];
   const float k2 = -k1 * invstd[c] * invstd[c] * sdx / count;
   const float k3 = -k1 * sd / count - k2 * mean[c];
@@ -325,9 +327,9 @@ void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scal
 }
 
 void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale, const float* invstd,
-                     const float* mean, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+                     const float* mean, float* dgamma, float* dbeta, float* coef, float pscale, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp, count, scale,
-                     invstd, mean, dgamma, dbeta, coef);
+                     invstd, mean, dgamma, dbeta, coef, pscale);
 }
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

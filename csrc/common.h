@@ -17,14 +17,14 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 DEVI float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-DEVI uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+// fp32 -> bf16, round-to-nearest-even, NaN preserved: the compiler emits v_cvt_pk_bf16_f32.
+DEVI uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
-DEVI uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+DEVI uint32_t pack2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
 
 DEVI void unpack8(const uint4& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
@@ -49,6 +49,25 @@ DEVI float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15): four v_add_f32_dpp row_ror, every lane
+// of the row ends with the total.  The MFMA 16x16 D layout keeps one output column per lane & 15.
+DEVI float row16_sum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x124, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x122, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x121, 0xf, 0xf, false));
+  return x;
+}
+
+// n / d for 0 <= n < 2^22 via a host-precomputed fp32 reciprocal (one multiply + one fix-up) instead
+// of the ~30-instruction integer division sequence; exact in that range.
+DEVI int fdiv(int n, int d, float inv) {
+  int q = (int)((float)n * inv);
+  const int r = n - __mul24(q, d);
+  q += (r >= d) - (r < 0);
+  return q;
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -363,21 +363,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
 // supplies its own pixel row address, so the shift is free).  Block output = dW[32 co][T taps][32 ci];
 // the 4 waves own disjoint (tap, ci16) pairs, so no cross-wave reduction.  Blocks loop over pixel
 // tiles (accumulating in registers) and finish with one fp32 atomic per output element.
+// LDS layout: one 64-B row per pixel (32 channels, no padding); the two 32-B halves are XOR-swizzled
+// by bit 3 of the pixel index.  A transposed read of 32 lanes touches pixels {b..b+3, b+8..b+11}
+// (+ a tap shift): pixels p and p+8 share a bank quadrant and always sit in opposite halves, so both
+// the dY and the halo reads are bank-conflict-free for every tap (a padded 72-B pitch is 2-way).
+// Tile width TW in {16, 32} and TH = 256 / TW (eight 32-pixel slices); the halo row pitch HWd is
+// padded to a multiple of 16 pixels, so a lane's read offsets are per-lane constants plus a
+// per-slice uniform: the slice loop is only transposed reads and MFMAs.
 constexpr int DW_CH = 32;               // co rows and ci channels per block
-constexpr int DW_LD = DW_CH + 4;        // LDS pixel pitch (bf16 elems): 72 B, 8-B aligned
 
-struct DwTile { int TH, TW, ey0, ex0, HH, HWd, tiles_y, tiles_x; };
+struct DwTile { int TH, TW, tw_shift, ey0, ex0, HH, HWd, HWv, tiles_y, tiles_x; float inv_hwv; };
 
 constexpr int kDwLd = 8;
+constexpr long kDwSplitTarget = 768;
+
+DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 16-ch half, 4-ch sub)
+  return pix * DW_CH + 16 * (half ^ ((pix >> 3) & 1)) + 4 * sub4;
+}
 
 template <int NPW>
 __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
                                                               DwTile tl, int KT, long ntiles) {
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
-  const int npx = tl.TH * tl.TW;
-  const int nslice = (npx + 31) / 32;
-  uint16_t* sY = dsm;                                    // [nslice*32 + 1][DW_LD] (last row = zeros)
-  uint16_t* sX = dsm + (nslice * 32 + 1) * DW_LD;        // [HH*HWd][DW_LD]
+  constexpr int NPX = 256, NSL = 8;
+  uint16_t* sY = dsm;                       // [256][32]  swizzled
+  uint16_t* sX = dsm + NPX * DW_CH;         // [HH * HWd][32]  swizzled
   __shared__ int2 s_tap[kMaxTaps];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -385,10 +395,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
   const int co0 = blockIdx.y * DW_CH, ci0 = blockIdx.z * DW_CH;
   const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
-  // zero row for out-of-tile pixels
-  if (tid < DW_LD) sY[nslice * 32 * DW_LD + tid] = 0;
 
-  // per-thread loader roles: vector v = tid & 3 (8 channels), pixel = tid >> 2 (+ 64*i)
+  // per-thread loader roles: vector vv = tid & 3 (8 channels), pixel lane vp = tid >> 2
   const int vv = tid & 3, vp = tid >> 2;
   const int yco = co0 + 8 * vv;
   const bool y_ok = yco < rows;
@@ -398,24 +406,47 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
   const bool x_ok = xci < Cip;
   const int x_g = x_ok ? xci / g.Cgi : 0;
   const uint16_t* x_base = P.x[x_g] + (xci - x_g * g.Cgi);
+  __syncthreads();
+
+  // lane pixel within a 32-pixel slice: lo = 8*lg + q, hi = lo + 4 (tile coords: row ry, column cx)
+  const int plo = 8 * lg + q, phi = plo + 4;
+  const int ry_lo = plo >> tl.tw_shift, cx_lo = plo & (tl.TW - 1);
+  const int ry_hi = phi >> tl.tw_shift, cx_hi = phi & (tl.TW - 1);
+  const int rows_per_slice = 32 >> tl.tw_shift;
+  // A (dY) read offsets: slice sl adds 32*32*sl (bit 3 of the pixel is lg & 1 for every slice)
+  int offA[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { offA[i][0] = dw_elem(plo, i, p4); offA[i][1] = dw_elem(phi, i, p4); }
+  // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32
+  const int npairs = 2 * g.T;
+  int offB[NPW][2];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int pr = wave + 4 * j;
+    const int t = pr < npairs ? pr >> 1 : 0, cf = pr & 1;
+    const int2 d = s_tap[t];
+    offB[j][0] = dw_elem((ry_lo + d.x) * tl.HWd + cx_lo + d.y, cf, p4);
+    offB[j][1] = dw_elem((ry_hi + d.x) * tl.HWd + cx_hi + d.y, cf, p4);
+  }
 
   f32x4_t acc[2][NPW];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NPW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int npairs = 2 * g.T;
 
+  const int nh = tl.HH * tl.HWv;
   for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
     const int per_img = tl.tiles_y * tl.tiles_x;
     const int n = (int)(tix / per_img);
     const int rem = (int)(tix - (long)n * per_img);
     const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
+    const uint16_t* yim = y_base + (long)n * g.OH * g.OW * g.Cgo;
+    const uint16_t* xim = x_base + (long)n * g.IH * g.IW * g.Cgi;
     __syncthreads();   // previous tile's LDS reads are done
     // ---- stage dY tile (pixels beyond the image -> 0) and the input halo (zero padding outside the
     // image); kDwLd loads in flight per thread before the LDS writes of each batch.
-    const int nyp = nslice * 32, nh = tl.HH * tl.HWd;
-    for (int base = vp; base < nyp + nh; base += 64 * kDwLd) {
+    for (int base = vp; base < NPX + nh; base += 64 * kDwLd) {
       uint4 v[kDwLd];
       int dst[kDwLd];
 #pragma unroll
@@ -423,53 +454,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
         const int e = base + 64 * u;
         v[u] = make_uint4(0, 0, 0, 0);
         dst[u] = -1;
-        if (e < nyp) {
-          const int px = e;
-          const int ty = px / tl.TW, tx = px - (px / tl.TW) * tl.TW;
-          const int oy = y0 + ty, ox = x0 + tx;
-          dst[u] = px * DW_LD + 8 * vv;
-          if (px < npx && y_ok && oy < g.OH && ox < g.OW)
-            v[u] = *reinterpret_cast<const uint4*>(y_base + ((long)n * g.OH * g.OW + (long)oy * g.OW + ox) * g.Cgo);
-        } else if (e < nyp + nh) {
-          const int hp = e - nyp;
-          const int hy = hp / tl.HWd, hx = hp - (hp / tl.HWd) * tl.HWd;
+        if (e < NPX) {
+          const int oy = y0 + (e >> tl.tw_shift), ox = x0 + (e & (tl.TW - 1));
+          dst[u] = dw_elem(e, vv >> 1, 2 * (vv & 1));
+          if (y_ok && oy < g.OH && ox < g.OW)
+            v[u] = *reinterpret_cast<const uint4*>(yim + (oy * g.OW + ox) * g.Cgo);
+        } else if (e < NPX + nh) {
+          const int hp = e - NPX;
+          const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
           const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
-          dst[u] = (int)(sX - sY) + hp * DW_LD + 8 * vv;
+          dst[u] = NPX * DW_CH + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
           if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
-            v[u] = *reinterpret_cast<const uint4*>(x_base + ((long)n * g.IH * g.IW + (long)iy * g.IW + ix) * g.Cgi);
+            v[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
         }
       }
 #pragma unroll
-      for (int u = 0; u < kDwLd; ++u) {
-        if (dst[u] < 0) continue;
-        *reinterpret_cast<uint2*>(&sY[dst[u]]) = make_uint2(v[u].x, v[u].y);
-        *reinterpret_cast<uint2*>(&sY[dst[u] + 4]) = make_uint2(v[u].z, v[u].w);
-      }
+      for (int u = 0; u < kDwLd; ++u)
+        if (dst[u] >= 0) *reinterpret_cast<uint4*>(&sY[dst[u]]) = v[u];
     }
     __syncthreads();
-    for (int sl = 0; sl < nslice; ++sl) {
-      const int plo = 32 * sl + 8 * lg + q, phi = plo + 4;
-      const int ylo = plo < npx ? plo : nslice * 32, yhi = phi < npx ? phi : nslice * 32;
+    for (int sl = 0; sl < NSL; ++sl) {
+      const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
       uint4 fa[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const uint2 lo = tr_read(&sY[ylo * DW_LD + 16 * i + 4 * p4]);
-        const uint2 hi = tr_read(&sY[yhi * DW_LD + 16 * i + 4 * p4]);
+        const uint2 lo = tr_read(&sY[sa + offA[i][0]]);
+        const uint2 hi = tr_read(&sY[sa + offA[i][1]]);
         fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
-      const int plc = plo < npx ? plo : 0, phc = phi < npx ? phi : 0;
-      const int lty = plc / tl.TW, ltx = plc - lty * tl.TW;
-      const int hty = phc / tl.TW, htx = phc - hty * tl.TW;
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
-        const int pr = wave + 4 * j;
-        if (pr < npairs) {
-          const int t = pr >> 1, cf = pr & 1;
-          const int2 d = s_tap[t];
-          const int xlo = (lty + d.x) * tl.HWd + ltx + d.y;
-          const int xhi = (hty + d.x) * tl.HWd + htx + d.y;
-          const uint2 lo = tr_read(&sX[xlo * DW_LD + 16 * cf + 4 * p4]);
-          const uint2 hi = tr_read(&sX[xhi * DW_LD + 16 * cf + 4 * p4]);
+        if (wave + 4 * j < npairs) {
+          const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
+          const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
           acc[0][j] = mfma16x16x32(fa[0], fb, acc[0][j]);
           acc[1][j] = mfma16x16x32(fa[1], fb, acc[1][j]);
@@ -558,25 +575,39 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restri
 // table lookup replaces the per-lane tap/bounds arithmetic of the gather kernel, and the input is read
 // from HBM once per tile (halo overhead (TH+ey)(TW+ex)/(TH*TW)) instead of once per tap from L2.
 // Waves split the tile's pixels (NJ 16-pixel columns each) and loop over the 16*MI-row groups.
-struct HaloGeom { int TH, TW, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, KC; };
+struct HaloGeom {
+  int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
+  float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
+};
 
-constexpr int kHaloMaxKC = 64;
+constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel) units each)
 constexpr int kHaloWaves = 4;
 constexpr int kHaloMaxRows = 512;
-constexpr int kHaloLd = 8;
+constexpr int kHaloLd = 8;       // 16-B loads in flight per thread while staging
 
-template <int MI, int NJ>
-__global__ __launch_bounds__(64 * kHaloWaves, 3) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+// K is walked in UNITS of (tap t, 8 channels c8) -- the lane group lg of k-step ks takes unit
+// 4*ks + lg.  Per unit: A offset t*Cip + 8*c8 (+ chunk base) into the packed weight row, B offset
+// tapoff(t) + 8*c8 into the LDS tile.  With one chunk (CC == Cip) this is exactly the packed
+// k = t*Cip + ci order, so A is read contiguously and the padding units past T*Cip hit the packed
+// rows' zero padding (their B offset is a harmless in-tile address).  With CHUNKED the input channels
+// are staged CC at a time (inputs too wide for one LDS tile: the data-gradient of horizontally fused
+// convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
+// registers while the current one runs on the MFMAs, and the accumulators persist across chunks
+// (single row group).
+template <int MI, int NJ, bool CHUNKED>
+__global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
-  __shared__ int s_koff[kHaloMaxKC * 4];
+  __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
+  __shared__ int s_ub[kHaloMaxKS * 4];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int Cip = g.Gi * g.Cgi, C8 = Cip >> 3;
+  const int Cip = g.Gi * g.Cgi, C8c = hg.CC >> 3;
   const int rows = g.Go * g.Cgo;
-  // per-wave (sum, sum^2) rows after the tile (+ zero slot): [kHaloWaves][2][rows] fp32
-  float* s_stat = reinterpret_cast<float*>(tile + hg.HH * hg.HWD * hg.pitch + 8);
+  const int hpx = hg.HH * hg.HWD;
+  // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
+  float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
 
   // XCD-aware bijective remap: neighbouring tiles (shared halo rows) land on one XCD's L2.
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -586,125 +617,171 @@ __global__ __launch_bounds__(64 * kHaloWaves, 3) void conv_halo_kernel(ConvArgs 
   const int n = wgid / per_img;
   const int trem = wgid - n * per_img;
   const int ty0 = (trem / hg.tiles_x) * hg.TH, tx0 = (trem % hg.tiles_x) * hg.TW;
-
-  // ---- stage the halo tile: 16 B per element, kHaloLd loads in flight per thread before any LDS
-  // write (a load->store loop would serialise one HBM latency per iteration).
-  const int hpx = hg.HH * hg.HWD;
   const long img = (long)n * g.IH * g.IW;
-  const int total = hpx * C8;
-  for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
-    uint4 v[kHaloLd];
-    int dst[kHaloLd];
+  const int total = hpx * C8c;
+
+  // staging: element idx -> (halo pixel, 8-channel slot of the chunk); zero outside the image.
+  // 32-bit per-image offsets (one image's activations < 2^31 elements) from per-image base pointers.
+  const uint16_t* xim0 = a.x[0] + img * g.Cgi;
+  auto load_batch = [&](int c0, int base, uint4* v, int* dst) {
 #pragma unroll
     for (int u = 0; u < kHaloLd; ++u) {
       const int idx = base + u * 64 * kHaloWaves;
       v[u] = make_uint4(0, 0, 0, 0);
       dst[u] = -1;
       if (idx < total) {
-        const int hp = idx / C8, c8 = idx - hp * C8;
-        const int hy = hp / hg.HWD, hx = hp - hy * hg.HWD;
+        const int hp = fdiv(idx, C8c, hg.inv_c8), c8 = idx - __mul24(hp, C8c);
+        const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
         const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
-        dst[u] = hp * hg.pitch + c8 * 8;
+        dst[u] = __mul24(hp, hg.pitch) + c8 * 8;
         if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
-          const int ci = c8 * 8, gi = ci / g.Cgi, cl = ci - gi * g.Cgi;
-          v[u] = *reinterpret_cast<const uint4*>(a.x[gi] + (img + (long)iy * g.IW + ix) * g.Cgi + cl);
+          const int ci = c0 + c8 * 8;
+          const int pix = iy * g.IW + ix;
+          if (g.Gi == 1) {
+            v[u] = *reinterpret_cast<const uint4*>(xim0 + pix * g.Cgi + ci);
+          } else {
+            const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
+            v[u] = *reinterpret_cast<const uint4*>(a.x[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+          }
         }
       }
     }
+  };
+  auto store_batch = [&](const uint4* v, const int* dst) {
 #pragma unroll
     for (int u = 0; u < kHaloLd; ++u)
       if (dst[u] >= 0) *reinterpret_cast<uint4*>(tile + dst[u]) = v[u];
-  }
-  const int zero_off = hpx * hg.pitch;  // one zeroed 16-B slot for k beyond T*Cip
-  if (tid == 0) *reinterpret_cast<uint4*>(tile + zero_off) = make_uint4(0, 0, 0, 0);
-  for (int e = tid; e < hg.KC * 4; e += 64 * kHaloWaves) {
-    const int kk = 32 * (e >> 2) + 8 * (e & 3);
-    int off = -1;
-    if (kk < g.T * Cip) {
-      const int t = kk / Cip, ci = kk - t * Cip;
-      off = ((g.dy[t] - hg.ey0) * hg.HWD + (g.dx[t] - hg.ex0)) * hg.pitch + ci;
+  };
+
+  for (int e = tid; e < hg.KS * 4; e += 64 * kHaloWaves) {
+    int ua = -1, ub = 0;
+    if (e < g.T * C8c) {
+      const int t = e / C8c, c8 = e - t * C8c;
+      ua = t * Cip + 8 * c8;
+      ub = ((g.dy[t] - hg.ey0) * hg.HWD + (g.dx[t] - hg.ex0)) * hg.pitch + 8 * c8;
     }
-    s_koff[e] = off;
+    if (CHUNKED) s_ua[e] = ua;
+    s_ub[e] = ub;
   }
-  __syncthreads();
+
+  uint4 pv[CHUNKED ? kHaloLd : 1];
+  int pd[CHUNKED ? kHaloLd : 1];
+  if (CHUNKED) load_batch(0, tid, pv, pd);   // host guarantees total <= 64*kHaloWaves*kHaloLd
 
   int pb[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int p = (wave * NJ + j) * 16 + lr;
-    const int ty = p / hg.TW, tx = p - (p / hg.TW) * hg.TW;
-    pb[j] = (ty * hg.HWD + tx) * hg.pitch;
+    pb[j] = ((p >> hg.tw_shift) * hg.HWD + (p & (hg.TW - 1))) * hg.pitch;
   }
 
-  const int n_rg = (rows + 16 * MI - 1) / (16 * MI);
+  const int n_rg = CHUNKED ? 1 : (rows + 16 * MI - 1) / (16 * MI);
   for (int rg = 0; rg < n_rg; ++rg) {
     const int co0 = rg * 16 * MI;
     const uint16_t* wrow[MI];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + 8 * lg;
+    for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + (CHUNKED ? 0 : 8 * lg);
     f32x4_t acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    uint4 A[MI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i]);
-    for (int kc = 0; kc < hg.KC; ++kc) {
-      uint4 An[MI];
-      const bool more = kc + 1 < hg.KC;
-      if (more) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) An[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * (kc + 1));
+
+    for (int ch = 0; ch < hg.nch; ++ch) {
+      const int c0 = ch * hg.CC;
+      if (CHUNKED) {
+        if (ch > 0) __syncthreads();           // every wave is done reading the previous chunk
+        store_batch(pv, pd);
+        __syncthreads();
+        if (ch + 1 < hg.nch) load_batch(c0 + hg.CC, tid, pv, pd);   // in flight during the MFMAs
+      } else if (rg == 0) {
+        for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
+          uint4 v[kHaloLd];
+          int dst[kHaloLd];
+          load_batch(0, base, v, dst);
+          store_batch(v, dst);
+        }
+        __syncthreads();
       }
-      const int ko = s_koff[kc * 4 + lg];
-      uint4 B[NJ];
+      auto load_a = [&](uint4* A, int ks) {
+        if (CHUNKED) {
+          const int ua = s_ua[4 * ks + lg];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + (ko >= 0 ? pb[j] + ko : zero_off));
+          for (int i = 0; i < MI; ++i)
+            A[i] = ua >= 0 ? *reinterpret_cast<const uint4*>(wrow[i] + ua + c0) : make_uint4(0, 0, 0, 0);
+        } else {
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * ks);
+        }
+      };
+      uint4 A[MI];
+      load_a(A, 0);
+      for (int ks = 0; ks < hg.KS; ++ks) {
+        uint4 An[MI];
+        const bool more = ks + 1 < hg.KS;
+        if (more) load_a(An, ks + 1);
+        const int ub = s_ub[4 * ks + lg];
+        uint4 B[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
-      if (more) {
+        for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
 #pragma unroll
-        for (int i = 0; i < MI; ++i) A[i] = An[i];
-      }
-    }
-    // epilogue: bias, bf16 round, 8-B NHWC stores, per-row (sum, sum^2) of the stored values
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
-      const int cb = co0 + 16 * i + 4 * lg;
-      if (cb < rows) {
-        const int og = cb / g.Cgo, cl = cb - (cb / g.Cgo) * g.Cgo;
-        uint16_t* yb = a.y[og] + cl;
-        float bv[4];
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
+        if (more) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = (a.bias != nullptr && cl + r < g.Cgo_l) ? a.bias[cl + r] : 0.f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int p = (wave * NJ + j) * 16 + lr;
-          const int ty = ty0 + p / hg.TW, tx = tx0 + p % hg.TW;
-          if (ty >= g.OH || tx >= g.OW) continue;
-          const long pm = img + (long)ty * g.OW + tx;   // OH == IH, OW == IW
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
-            v[r] = bf2f(f2bf(o));
-            cs[r] += v[r];
-            cq[r] += v[r] * v[r];
-          }
-          *reinterpret_cast<uint2*>(yb + pm * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          for (int i = 0; i < MI; ++i) A[i] = An[i];
         }
       }
-      if (a.stat_part != nullptr) {
+    }
+    // epilogue: bias, bf16 round (v_cvt_pk), 8-B NHWC stores, per-row (sum, sum^2) of the stored
+    // values reduced over the 16 pixel lanes with DPP row adds.
+    uint16_t* yb[MI];
+    float bv[MI][4], cs[MI][4], cq[MI][4];
+    bool rv[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int cb = co0 + 16 * i + 4 * lg;
+      const int og = cb < rows ? cb / g.Cgo : 0, cl = cb - og * g.Cgo;
+      yb[i] = cb < rows ? a.y[og] + img * g.Cgo + cl : nullptr;   // per-image base
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rv[i][r] = cb < rows && cl + r < g.Cgo_l;
+        bv[i][r] = (a.bias != nullptr && rv[i][r]) ? a.bias[cl + r] : 0.f;
+        cs[i][r] = 0.f; cq[i][r] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int p = (wave * NJ + j) * 16 + lr;
+      const int ty = ty0 + (p >> hg.tw_shift), tx = tx0 + (p & (hg.TW - 1));
+      if (ty >= g.OH || tx >= g.OW) continue;
+      const int pm = (ty * g.OW + tx) * g.Cgo;   // OH == IH, OW == IW; within the image
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (yb[i] == nullptr) continue;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = rv[i][r] ? acc[i][j][r] + bv[i][r] : 0.f;
+        const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
+        const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
+        const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
+        cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
+        cq[i][0] += v0 * v0; cq[i][1] += v1 * v1; cq[i][2] += v2 * v2; cq[i][3] += v3 * v3;
+      }
+    }
+    if (a.stat_part != nullptr) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int cb = co0 + 16 * i + 4 * lg;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float s = cs[r], q = cq[r];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-          if (lr == 0 && cb + r < rows) { s_stat[(wave * 2 + 0) * rows + cb + r] = s; s_stat[(wave * 2 + 1) * rows + cb + r] = q; }
+          const float s = row16_sum(cs[i][r]), q = row16_sum(cq[i][r]);
+          if (lr == 0 && cb + r < rows) {
+            s_stat[(wave * 2 + 0) * rows + cb + r] = s;
+            s_stat[(wave * 2 + 1) * rows + cb + r] = q;
+          }
         }
       }
     }
@@ -778,8 +855,14 @@ static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
 }
 
 // Halo-kernel eligibility + tile geometry.  Pixel tile = 4 waves x NJ x 16 pixels (NJ = 8 for
-// MI <= 2, else 4); TW in {16, 32, 64} chosen to minimise (padded tile area) x (halo overhead).
+// MI <= 2, else 4); TW in {16, 32, 64} minimising (tiles) x (stores + halo loads).  The input is staged
+// whole (one chunk, LDS <= 64 KB) or -- single row group only -- in chunks of CC channels (CC | Cip, a
+// chunk's staging fits the kHaloLd registers per thread), widest CC first.
 static int halo_nj(int mi) { return mi <= 2 ? 8 : 4; }
+
+static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
+  return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
+}
 
 static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   if (trans || g.stride != 1 || g.OH != g.IH || g.OW != g.IW) return false;
@@ -787,44 +870,57 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   if (rows > kHaloMaxRows || g.T > kMaxTaps) return false;
   const int Cip = g.Gi * g.Cgi;
   if (Cip % 8 != 0 || g.Cgi % 8 != 0) return false;
-  const int KC = g.Kp / 32;
-  if (KC > kHaloMaxKC || g.Kp % 32 != 0) return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
   for (int t = 0; t < g.T; ++t) {
     ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
   const int mi = conv_pick_mi(rows);
+  const int n_rg = cdiv(rows, 16 * mi);
   const int tp = kHaloWaves * halo_nj(mi) * 16;
-  int c8 = Cip / 8;
-  if ((c8 & 1) == 0) ++c8;
-  const int pitch = 8 * c8;
-  double best = 1e30;
-  bool found = false;
-  for (int tw = 16; tw <= 64; tw *= 2) {
-    const int th = tp / tw;
-    const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
-    const size_t lds = ((size_t)HH * HWD * pitch + 8) * 2 + (size_t)kHaloWaves * 2 * rows * 4;
-    if (lds > 64 * 1024) continue;
-    const double tiles = (double)cdiv(g.OH, th) * cdiv(g.OW, tw);
-    const double cost = tiles * ((double)tp + 0.5 * (double)HH * HWD);   // stores + halo loads
-    if (cost < best) {
-      best = cost; found = true;
-      hg.TH = th; hg.TW = tw; hg.HH = HH; hg.HWD = HWD;
+  const int C8 = Cip / 8;
+  for (int pass = 0; pass < 2; ++pass) {          // pass 0: whole input; pass 1: channel chunks
+    if (pass == 1 && n_rg != 1) break;
+    for (int d = C8; d >= 1; --d) {
+      if (C8 % d != 0) continue;
+      if (pass == 0 && d != C8) break;
+      if (pass == 1 && d == C8) continue;
+      const int pitch = 8 * ((d & 1) ? d : d + 1);   // odd number of 16-B slots per pixel
+      const int ks = cdiv(g.T * d, 4);
+      if (ks > kHaloMaxKS) continue;
+      double best = 1e30;
+      bool found = false;
+      for (int tw = 16; tw <= 64; tw *= 2) {
+        const int th = tp / tw;
+        const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
+        if (halo_lds_bytes(HH, HWD, pitch, rows) > 64 * 1024) continue;
+        if (pass == 1 && HH * HWD * d > 64 * kHaloWaves * kHaloLd) continue;
+        const double tiles = (double)cdiv(g.OH, th) * cdiv(g.OW, tw);
+        const double cost = tiles * ((double)tp * rows / 8.0 + 0.5 * (double)HH * HWD * C8);
+        if (cost < best) {
+          best = cost; found = true;
+          hg.TH = th; hg.TW = tw; hg.HH = HH; hg.HWD = HWD;
+        }
+      }
+      if (!found) continue;
+      hg.ey0 = ey0; hg.ex0 = ex0;
+      hg.tiles_y = cdiv(g.OH, hg.TH);
+      hg.tiles_x = cdiv(g.OW, hg.TW);
+      hg.pitch = pitch;
+      hg.CC = 8 * d;
+      hg.nch = C8 / d;
+      hg.KS = ks;
+      hg.tw_shift = hg.TW == 16 ? 4 : (hg.TW == 32 ? 5 : 6);
+      hg.inv_c8 = 1.0f / (float)d;
+      hg.inv_hwd = 1.0f / (float)hg.HWD;
+      hg.inv_cgi = 1.0f / (float)g.Cgi;
+      return true;
     }
   }
-  if (!found) return false;
-  hg.ey0 = ey0; hg.ex0 = ex0;
-  hg.tiles_y = cdiv(g.OH, hg.TH);
-  hg.tiles_x = cdiv(g.OW, hg.TW);
-  hg.pitch = pitch;
-  hg.KC = KC;
-  return true;
+  return false;
 }
 
-static size_t halo_lds(const HaloGeom& hg, int rows) {
-  return ((size_t)hg.HH * hg.HWD * hg.pitch + 8) * 2 + (size_t)kHaloWaves * 2 * rows * 4;
-}
+static size_t halo_lds(const HaloGeom& hg, int rows) { return halo_lds_bytes(hg.HH, hg.HWD, hg.pitch, rows); }
 
 static int g_halo_mode = -1;   // -1: from MSP_CONV_HALO (default on), 0: off, 1: on
 
@@ -855,11 +951,15 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
     const unsigned blocks = (unsigned)((long)a.g.N * hg.tiles_y * hg.tiles_x);
     const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo);
-#define HC_(MI_)                                                                                          \
-    if (mi == MI_) {                                                                                      \
-      hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4)>), dim3(blocks), dim3(64 * kHaloWaves), \
-                         lds, s, a, hg);                                                                  \
-      return;                                                                                             \
+#define HC_(MI_)                                                                                             \
+    if (mi == MI_) {                                                                                         \
+      if (hg.nch > 1)                                                                                        \
+        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true>), dim3(blocks), dim3(64 * kHaloWaves), \
+                           lds, s, a, hg);                                                                   \
+      else                                                                                                   \
+        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false>), dim3(blocks), dim3(64 * kHaloWaves), \
+                           lds, s, a, hg);                                                                   \
+      return;                                                                                                \
     }
     HC_(1) HC_(2) HC_(3) HC_(4)
 #undef HC_
@@ -870,6 +970,8 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   else dispatch_igemm<false>(a, mi, nj, wpx, s);
 }
 
+static size_t wgrad_halo_lds(const DwTile& tl) { return ((size_t)256 + (size_t)tl.HH * tl.HWd) * DW_CH * 2; }
+
 static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
   if (g.stride != 1 || g.T > 9) return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
@@ -878,17 +980,18 @@ static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
   if (g.OH != g.IH || g.OW != g.IW) return false;
-  const int nx = cdiv(g.OW, 32);
-  tl.TW = cdiv(g.OW, nx);
-  tl.TH = std::max(1, std::min(g.OH, 256 / tl.TW));
+  // TW = 32 unless the image is narrow enough that 16 wastes less
+  tl.TW = (cdiv(g.OW, 16) * 16 < cdiv(g.OW, 32) * 32) ? 16 : 32;
+  tl.tw_shift = tl.TW == 16 ? 4 : 5;
+  tl.TH = 256 / tl.TW;
   tl.ey0 = ey0; tl.ex0 = ex0;
   tl.HH = tl.TH + ey1 - ey0;
-  tl.HWd = tl.TW + ex1 - ex0;
+  tl.HWv = tl.TW + ex1 - ex0;
+  tl.HWd = cdiv(tl.HWv, 16) * 16;
+  tl.inv_hwv = 1.0f / (float)tl.HWv;
   tl.tiles_y = cdiv(g.OH, tl.TH);
   tl.tiles_x = cdiv(g.OW, tl.TW);
-  const int nslice = cdiv(tl.TH * tl.TW, 32);
-  const size_t lds = ((size_t)(nslice * 32 + 1) + (size_t)tl.HH * tl.HWd) * DW_LD * 2;
-  return lds <= 64 * 1024;
+  return wgrad_halo_lds(tl) <= 64 * 1024;
 }
 
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
@@ -903,11 +1006,13 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
   if (!trans && wgrad_halo_ok(g, tl)) {
     const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;
     const int gy = cdiv(rows, DW_CH), gz = cdiv(g.Gi * g.Cgi, DW_CH);
-    long nsplit = 1536 / ((long)gy * gz);
+    // Blocks split the tiles and add their dW slab with fp32 atomics: atomic bytes = nsplit * rows * KT * 4
+    // at ~1.3 TB/s chip-wide, so keep nsplit near 3 blocks per CU (LDS-limited residency) -- enough
+    // to overlap one block's staging with another's MFMA phase -- rather than one tile per block.
+    long nsplit = kDwSplitTarget / ((long)gy * gz);
     if (nsplit < 1) nsplit = 1;
     if (nsplit > ntiles) nsplit = ntiles;
-    const int nslice = cdiv(tl.TH * tl.TW, 32);
-    const size_t lds = ((size_t)(nslice * 32 + 1) + (size_t)tl.HH * tl.HWd) * DW_LD * 2;
+    const size_t lds = wgrad_halo_lds(tl);
     dim3 grid((unsigned)nsplit, gy, gz);
     const int npw = cdiv(2 * g.T, 4);
 #define HW_(N_) if (npw == N_) { hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_>), grid, dim3(256), lds, s, P, dw, g, tl, KT, ntiles); return; }

@@ -75,7 +75,7 @@ void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scal
                         const float* mean, float* part, long P, int Cp, int relu, hipStream_t s);
 void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale,
                      const float* invstd, const float* mean, float* dgamma, float* dbeta,
-                     float* coef, hipStream_t s);
+                     float* coef, float pscale, hipStream_t s);
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
                       const float* coef, uint16_t* dy, long P, int Cp, int relu, hipStream_t s);
 

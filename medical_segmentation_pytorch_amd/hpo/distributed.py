@@ -55,11 +55,14 @@ def make_trial_groups(ranks_per_trial):
     world, rank = dist.get_world_size(), dist.get_rank()
     assert world % ranks_per_trial == 0, 'world size must be a multiple of ranks_per_trial'
     n = world // ranks_per_trial
+    from ..runtime.engine import register_stat_group
     mine = None
     for g in range(n):
         ranks = list(range(g * ranks_per_trial, (g + 1) * ranks_per_trial))
         pg = dist.new_group(ranks)
+        spg = dist.new_group(ranks)      # the trial's SyncBN-statistics communicator
         if rank in ranks:
+            register_stat_group(pg, spg)
             mine = (pg, g, n, ranks[0])
     return mine
 

@@ -133,7 +133,9 @@ class _BNAct(torch.autograd.Function):
         b_t = st.bias_sink if st.bias_sink is not None else dbeta
         coef = torch.empty(3, Cp, dtype=torch.float32, device=dev)
         if ctx.training:
-            C.bn_bwd_finalize(sums, st.C, Cp, ctx.count, stats, g_t, b_t, coef)
+            # global (SyncBN) sums -> dgamma/dbeta scaled by 1/world: the bucketed all-reduce-average
+            # then yields the mean of the per-rank local parameter gradients (torch SyncBatchNorm).
+            C.bn_bwd_finalize(sums, st.C, Cp, ctx.count, stats, g_t, b_t, coef, 1.0 / _world(st.group))
         else:
             # eval-mode BN is a per-channel affine map: dx = dzr * scale
             coef[0] = stats[0]

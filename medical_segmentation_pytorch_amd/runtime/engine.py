@@ -72,6 +72,34 @@ class Arena:
         return {id(p): i for i, p in enumerate(self.params)}
 
 
+_STAT_GROUPS = {}
+
+
+def register_stat_group(group, stat_group):
+    """Pair ``group`` with a dedicated communicator for SyncBN statistics (created collectively by the
+    caller, e.g. :func:`hpo.distributed.make_trial_groups`)."""
+    _STAT_GROUPS[group] = stat_group
+
+
+def stat_group(group):
+    """Communicator for the SyncBN statistic exchanges of a run on ``group``.
+
+    Each RCCL communicator runs its collectives in order on its own stream, so tiny BN all-reduces
+    that share the gradient buckets' communicator queue behind multi-MB bucket all-reduces during
+    backward.  For WORLD a duplicate communicator is created here (every rank of the job reaches this
+    point together); a sub-group uses the partner registered by ``register_stat_group`` or, failing
+    that, itself.
+    """
+    if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return group
+    if group in _STAT_GROUPS:
+        return _STAT_GROUPS[group]
+    if group is dist.group.WORLD or dist.get_world_size(group) == dist.get_world_size():
+        _STAT_GROUPS[group] = dist.new_group(list(range(dist.get_world_size())))
+        return _STAT_GROUPS[group]
+    return group
+
+
 class GradBucketer:
     """DDP-equivalent gradient averaging over RCCL: buckets are contiguous slices of the grad arena
     in REVERSE parameter order (backward produces the last layers first); a bucket is all-reduced

@@ -15,7 +15,7 @@ import torch.distributed as dist
 
 from ..ops._ext import require
 from ..ops.losses import cross_entropy
-from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle
+from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, stat_group
 from .fused_model import FusedExecutor
 
 
@@ -33,7 +33,8 @@ class FusedStep:
         self.ema_model = copy.deepcopy(model).eval()
         self.arena = Arena(model, dev)
         self.bucketer = GradBucketer(self.arena, group, bucket_cap_mb) if distributed else None
-        self.ex = FusedExecutor(model, group=group if syncbn else None, sinks=self.arena.sinks(), count_nbt=False,
+        self.ex = FusedExecutor(model, group=stat_group(group) if syncbn else None, sinks=self.arena.sinks(),
+                                count_nbt=False,
                                 ready_hook=self.bucketer.ready if self.bucketer else None)
         kind = optimizer
         self.opt = FlatOptimizer(self.arena, kind, lr=lr, weight_decay=weight_decay, momentum=momentum)

@@ -101,7 +101,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
             from ..runtime.engine import GradBucketer
             bucketer = GradBucketer(arena, group, config.bucket_cap_mb)
             optimizer.attach_bucketer(bucketer)
-        return FusedModel(model, group=group if config.synBN else None,
+        from ..runtime.engine import stat_group
+        return FusedModel(model, group=stat_group(group) if config.synBN else None,
                           sinks=arena.sinks() if arena is not None else None,
                           ready_hook=bucketer.ready if bucketer is not None else None)
     if config.DDP:

@@ -24,12 +24,17 @@ torch.manual_seed(0)
 model = DuckNet(2, 3, 8).to(dev).train()
 g = torch.Generator().manual_seed(1)
 x = torch.randn(4, 3, 128, 128, generator=g).to(dev)   # the global batch, same for every world size
-y = (torch.rand(4, 128, 128, generator=g) > 0.5).long().to(dev)
-if world == 1:
+# labels correlated with the input (random per-pixel labels give a gradient that is a heavily
+# cancelling sum of noise, which amplifies bf16 rounding differences beyond any useful tolerance)
+y = (torch.nn.functional.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long().to(dev)
+if os.environ.get('PERTURB') == '1':   # noise-floor run: bf16-rounding-sized input perturbation
+    x = x * (1 + 4e-3 * torch.randn(x.shape, generator=torch.Generator().manual_seed(7)).to(dev))
+if world == 1 or os.environ.get('DUP') == '1':   # DUP: every rank holds the full batch
     xs, ys = x, y
 else:
     xs, ys = x[2 * rank:2 * rank + 2].contiguous(), y[2 * rank:2 * rank + 2].contiguous()
-w0 = torch.cat([p.detach().float().flatten() for p in model.parameters()]).cpu()
+w0 = [p.detach().float().cpu().clone() for p in model.parameters()]
+names = [n for n, _ in model.named_parameters()]
 step = FusedStep(model, xs, ys, optimizer='sgd', lr=0.05, momentum=0.0, use_graph=False,
                  distributed=world > 1, syncbn=True, bucket_cap_mb=0.5)
 step.sched.max_lr = 0.05
@@ -39,18 +44,21 @@ loss = torch.tensor([float(loss)])
 dist.all_reduce(loss)                     # mean of the per-rank half-batch losses == full-batch loss
 loss = loss / world
 if rank == 0:
-    w = torch.cat([p.detach().float().flatten() for p in model.parameters()]).cpu() - w0   # the SGD update
+    upd = [p.detach().float().cpu() - a for p, a in zip(model.parameters(), w0)]   # the SGD update
+    w = torch.cat([u.flatten() for u in upd])
     rms = [b.detach().float().cpu() for n, b in model.named_buffers() if 'running_mean' in n]
-    torch.save({'w': w, 'rm': torch.cat(rms), 'rms': rms, 'loss': float(loss)}, os.environ['OUT'])
+    torch.save({'w': w, 'upd': upd, 'names': names, 'rm': torch.cat(rms), 'rms': rms, 'loss': float(loss)},
+               os.environ['OUT'])
 dist.destroy_process_group()
 '''
 
 
-def _run(world, out, tmp):
+def _run(world, out, tmp, dup=False, perturb=False):
     s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
     script = tmp / 'w.py'
     script.write_text(WORKER)
-    env = dict(os.environ, ROOT=ROOT, OUT=str(out), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    env = dict(os.environ, ROOT=ROOT, OUT=str(out), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+               DUP='1' if dup else '0', PERTURB='1' if perturb else '0')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={world}',
            '--master-addr', '127.0.0.1', '--master-port', str(port), str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
@@ -58,20 +66,38 @@ def _run(world, out, tmp):
     return torch.load(out, weights_only=True)
 
 
+def test_replicated_batch_is_exact(gpu, tmp_path):
+    """Both ranks hold the SAME full batch: SyncBN statistics and averaged gradients are then
+    mathematically identical to the single-process step, so only rounding may differ -- this isolates
+    exchange bugs from the bf16 drift of the split-batch comparison below."""
+    one = _run(1, tmp_path / 'one.pt', tmp_path)
+    dup = _run(2, tmp_path / 'dup.pt', tmp_path, dup=True)
+    per = sorted(((((a - b).norm() / a.norm().clamp_min(1e-20)).item(), (b.norm() / a.norm().clamp_min(1e-20)).item(), n)
+                  for a, b, n in zip(one['upd'], dup['upd'], one['names'])), reverse=True)
+    print('replicated: worst params (rel diff, norm ratio, name):', per[:8])
+    rel = [((a - b).norm() / a.norm().clamp_min(1e-12)).item() for a, b in zip(one['rms'], dup['rms'])]
+    print('replicated: max running_mean rel diff', max(rel))
+    assert max(rel) < 1e-4, rel
+    assert per[0][0] < 1e-2, per[:8]
+
+
+def _upd_rel(a, b):
+    return ((a['w'] - b['w']).norm() / a['w'].norm()).item()
+
+
 def test_syncbn_ddp_matches_single_process(gpu, tmp_path):
+    """Split batch (2 images per rank) vs one process on all 4.  The BN statistics are identical up to
+    fp64 summation order, but a 1-ulp change of a BN scale flips bf16 roundings that the ~100-layer
+    forward/backward at random init amplifies; the update is therefore compared against a measured
+    noise floor: the same single-process step on a 0.4 %-perturbed input."""
     one = _run(1, tmp_path / 'one.pt', tmp_path)
     two = _run(2, tmp_path / 'two.pt', tmp_path)
-    # SyncBN => identical batch statistics; averaged grads of two half batches == full-batch grad.
-    # The first BN layer sees bit-identical inputs (exact up to fp64 summation order); deeper layers
-    # drift by bf16 rounding amplified through ~100 layers at tiny BN batches, while a missing SyncBN /
-    # gradient exchange shows up as tens of percent from the FIRST layer on.
+    pert = _run(1, tmp_path / 'pert.pt', tmp_path, perturb=True)
     rel = [((a - b).norm() / a.norm().clamp_min(1e-12)).item() for a, b in zip(one['rms'], two['rms'])]
     print('per-layer running_mean rel diff:', ' '.join(f'{r:.1e}' for r in rel))
-    # observed: ~1e-7 for the first ~25 layers, growing smoothly to ~1e-1 at the 2x2 bottleneck of a
-    # 64x64 input; a missing exchange is ~30 % already at layer 0.
+    # the first BN layers see bit-identical inputs; a missing exchange is ~30 % already at layer 0
     assert max(rel[:16]) < 1e-5, rel[:16]
-    assert max(rel) < 0.25, rel
-    wrel = ((one['w'] - two['w']).norm() / one['w'].norm()).item()   # update = -lr * (averaged) grad
-    print('update rel diff', wrel, 'loss', one['loss'], two['loss'])
-    assert wrel < 0.1, wrel
+    split, floor = _upd_rel(one, two), _upd_rel(one, pert)
+    print('update rel diff: split', split, 'noise floor', floor, 'loss', one['loss'], two['loss'], pert['loss'])
+    assert split < 2.0 * floor + 0.05, (split, floor)
     assert abs(one['loss'] - two['loss']) < 1e-2 * abs(one['loss']), (one['loss'], two['loss'])

@@ -313,6 +313,11 @@ def test_conv_halo_matches_gather(gpu, case):
     dims = plan.fwd_dims(n, h, w, h, w)
     dy, dx = [t[0] for t in plan.taps_fwd], [t[1] for t in plan.taps_fwd]
     assert C.conv_uses_halo(dims, dy, dx, False), 'case must exercise the halo kernel'
+    if go > 1:   # data-gradient reads go dY groups: the channel-chunked halo path
+        _, kp_d = plan.pack_dgrad(gpu)
+        dims_d = [n, h, w, plan.Go, plan.Cgo, h, w, 1, plan.Cgi, ci, plan.T, kp_d, 1]
+        bdy, bdx = [t[0] for t in plan.taps_bwd], [t[1] for t in plan.taps_bwd]
+        assert C.conv_uses_halo(dims_d, bdy, bdx, False), 'dgrad must exercise the chunked halo kernel'
     outs = {}
     for mode in (True, False):
         C.conv_set_halo(mode)
