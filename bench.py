@@ -103,7 +103,9 @@ def main(argv=None):
             'config': {'model': f'DUCKNet-{args.base_channel}', 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
-                       'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph},
+                       'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph,
+                       'peak_mem_gib': round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
+                       if torch.cuda.is_available() else None},
         }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -77,8 +77,13 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   for (auto& t : xs) { CHECK_BF16(t); TORCH_CHECK(t.numel() == (int64_t)g.N * g.IH * g.IW * g.Cgi); px.push_back(bf(t)); }
   for (auto& t : dys) { CHECK_BF16(t); TORCH_CHECK(t.numel() == (int64_t)g.N * g.OH * g.OW * g.Cgo); pd.push_back(bf(t)); }
   CHECK_F32(dw);
-  TORCH_CHECK(dw.numel() == (int64_t)g.Go * g.Cgo * g.T * g.Gi * g.Cgi, "dw numel mismatch");
+  const int64_t one = (int64_t)g.Go * g.Cgo * g.T * g.Gi * g.Cgi;
+  TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans), "dw numel mismatch (replicas)");
   conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cur_stream());
+}
+
+int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  return conv_wgrad_replicas(make_geom(dims, dy, dx), trans);
 }
 
 bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
@@ -98,13 +103,16 @@ void pack_weight_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, i
 }
 
 void unpack_wgrad_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
-                    int64_t Ktot, int64_t t_base, int64_t c_base, int64_t s_row, int64_t s_ch, bool accumulate) {
+                    int64_t Ktot, int64_t t_base, int64_t c_base, int64_t s_row, int64_t s_ch, bool accumulate,
+                    int64_t nrep, int64_t rep_stride) {
   CHECK_F32(src);
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat, "dst must be fp32 GPU");
-  TORCH_CHECK(src.numel() >= nrow * Ktot && (t_base + T - 1) * Cpk + c_base + nch <= Ktot, "src too small");
+  TORCH_CHECK(nrep >= 1 && (nrep == 1 || rep_stride >= nrow * Ktot), "bad replica layout");
+  TORCH_CHECK(src.numel() >= (nrep - 1) * rep_stride + nrow * Ktot && (t_base + T - 1) * Cpk + c_base + nch <= Ktot,
+              "src too small");
   TORCH_CHECK(dst.numel() >= (nrow - 1) * s_row + (nch - 1) * s_ch + T, "dst too small");
   unpack_wgrad(f32(src), dst.data_ptr<float>(), nrow, nch, T, Cpk, Ktot, t_base, c_base, s_row, s_ch, accumulate,
-               cur_stream());
+               (int)nrep, rep_stride, cur_stream());
 }
 
 void pack_batch_t(const at::Tensor& jobs, const at::Tensor& prefix, int64_t total_blocks) {
@@ -305,7 +313,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_uses_halo", &conv_uses_halo_t);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);
-  m.def("unpack_wgrad", &unpack_wgrad_t);
+  m.def("unpack_wgrad", &unpack_wgrad_t, py::arg("src"), py::arg("dst"), py::arg("nrow"), py::arg("nch"),
+        py::arg("T"), py::arg("Cpk"), py::arg("Ktot"), py::arg("t_base"), py::arg("c_base"), py::arg("s_row"),
+        py::arg("s_ch"), py::arg("accumulate"), py::arg("nrep") = 1, py::arg("rep_stride") = 0);
+  m.def("conv_wgrad_replicas", &conv_wgrad_replicas_t);
   m.def("pack_batch", &pack_batch_t);
   m.def("pack_per_block", &pack_per_block);
   m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });

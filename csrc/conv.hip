@@ -374,16 +374,17 @@ constexpr int DW_CH = 32;               // co rows and ci channels per block
 
 struct DwTile { int TH, TW, tw_shift, ey0, ex0, HH, HWd, HWv, tiles_y, tiles_x; float inv_hwv; };
 
-constexpr int kDwLd = 8;
-constexpr long kDwSplitTarget = 768;
+constexpr int kDwWaves = 8;      // waves per block: each owns <= 3 (tap, ci16) pairs of a 3x3
+constexpr int kDwStage = 7;      // staging elements per thread: (256 + halo) / (16 * kDwWaves) for every T <= 9 tap set
+constexpr long kDwSplitTarget = 256;
 
 DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 16-ch half, 4-ch sub)
   return pix * DW_CH + 16 * (half ^ ((pix >> 3) & 1)) + 4 * sub4;
 }
 
 template <int NPW>
-__global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
-                                                              DwTile tl, int KT, long ntiles) {
+__global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
+                                                              DwTile tl, int KT, long ntiles, int nrep) {
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
   constexpr int NPX = 256, NSL = 8;
   uint16_t* sY = dsm;                       // [256][32]  swizzled
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
   const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
 
-  // per-thread loader roles: vector vv = tid & 3 (8 channels), pixel lane vp = tid >> 2
+  // per-thread loader roles: vector vv = tid & 3 (8 channels), pixel lane vp = tid >> 2 (16 per wave)
   const int vv = tid & 3, vp = tid >> 2;
   const int yco = co0 + 8 * vv;
   const bool y_ok = yco < rows;
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
   int offB[NPW][2];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
-    const int pr = wave + 4 * j;
+    const int pr = wave + kDwWaves * j;
     const int t = pr < npairs ? pr >> 1 : 0, cf = pr & 1;
     const int2 d = s_tap[t];
     offB[j][0] = dw_elem((ry_lo + d.x) * tl.HWd + cx_lo + d.y, cf, p4);
@@ -436,43 +437,46 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
     for (int j = 0; j < NPW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nh = tl.HH * tl.HWv;
-  for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
+  // Software pipeline over the block's tiles: a tile's staging loads (<= kDwStage x 16 B per thread,
+  // host-checked) are issued into registers before the previous tile's MFMA phase and written to LDS
+  // after it, so HBM latency hides under the MFMAs.
+  uint4 sv[kDwStage];
+  int sd[kDwStage];
+  auto stage_load = [&](long tix) {
     const int per_img = tl.tiles_y * tl.tiles_x;
     const int n = (int)(tix / per_img);
     const int rem = (int)(tix - (long)n * per_img);
     const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
     const uint16_t* yim = y_base + (long)n * g.OH * g.OW * g.Cgo;
     const uint16_t* xim = x_base + (long)n * g.IH * g.IW * g.Cgi;
-    __syncthreads();   // previous tile's LDS reads are done
-    // ---- stage dY tile (pixels beyond the image -> 0) and the input halo (zero padding outside the
-    // image); kDwLd loads in flight per thread before the LDS writes of each batch.
-    for (int base = vp; base < NPX + nh; base += 64 * kDwLd) {
-      uint4 v[kDwLd];
-      int dst[kDwLd];
 #pragma unroll
-      for (int u = 0; u < kDwLd; ++u) {
-        const int e = base + 64 * u;
-        v[u] = make_uint4(0, 0, 0, 0);
-        dst[u] = -1;
-        if (e < NPX) {
-          const int oy = y0 + (e >> tl.tw_shift), ox = x0 + (e & (tl.TW - 1));
-          dst[u] = dw_elem(e, vv >> 1, 2 * (vv & 1));
-          if (y_ok && oy < g.OH && ox < g.OW)
-            v[u] = *reinterpret_cast<const uint4*>(yim + (oy * g.OW + ox) * g.Cgo);
-        } else if (e < NPX + nh) {
-          const int hp = e - NPX;
-          const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
-          const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
-          dst[u] = NPX * DW_CH + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
-          if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
-            v[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
-        }
+    for (int u = 0; u < kDwStage; ++u) {
+      const int e = vp + 16 * kDwWaves * u;
+      sv[u] = make_uint4(0, 0, 0, 0);
+      sd[u] = -1;
+      if (e < NPX) {
+        const int oy = y0 + (e >> tl.tw_shift), ox = x0 + (e & (tl.TW - 1));
+        sd[u] = dw_elem(e, vv >> 1, 2 * (vv & 1));
+        if (y_ok && oy < g.OH && ox < g.OW)
+          sv[u] = *reinterpret_cast<const uint4*>(yim + (oy * g.OW + ox) * g.Cgo);
+      } else if (e < NPX + nh) {
+        const int hp = e - NPX;
+        const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
+        const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
+        sd[u] = NPX * DW_CH + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
+        if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+          sv[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
       }
-#pragma unroll
-      for (int u = 0; u < kDwLd; ++u)
-        if (dst[u] >= 0) *reinterpret_cast<uint4*>(&sY[dst[u]]) = v[u];
     }
+  };
+  if ((long)blockIdx.x < ntiles) stage_load(blockIdx.x);
+  for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
+    __syncthreads();   // previous tile's LDS reads are done
+#pragma unroll
+    for (int u = 0; u < kDwStage; ++u)
+      if (sd[u] >= 0) *reinterpret_cast<uint4*>(&sY[sd[u]]) = sv[u];
     __syncthreads();
+    if (tix + gridDim.x < ntiles) stage_load(tix + gridDim.x);   // in flight during the MFMAs
     for (int sl = 0; sl < NSL; ++sl) {
       const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
       uint4 fa[2];
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
       }
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
-        if (wave + 4 * j < npairs) {
+        if (wave + kDwWaves * j < npairs) {
           const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
           const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -494,9 +498,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
       }
     }
   }
+  // every block adds into one of nrep dW replicas (summed by unpack_wgrad): spreads the adds of
+  // ~nsplit blocks over nrep x more addresses instead of hot-spotting a few L2 lines
+  float* dwr = dw + (long)(blockIdx.x % nrep) * rows * KT;
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
-    const int pr = wave + 4 * j;
+    const int pr = wave + kDwWaves * j;
     if (pr >= npairs) continue;
     const int t = pr >> 1, cf = pr & 1;
     const int ci = ci0 + 16 * cf + lr;
@@ -506,7 +513,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(WgradPtrs P, float
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + 16 * i + 4 * lg + r;
-        if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dw[(long)co * KT + t * Cip + ci], acc[i][j][r]);
+        if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dwr[(long)co * KT + t * Cip + ci], acc[i][j][r]);
       }
   }
 }
@@ -524,14 +531,17 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __re
 }
 
 __global__ void unpack_wgrad_kernel(const float* __restrict__ src, float* __restrict__ dst, int nrow, int nch, int T,
-                                    int Cpk, int Ktot, int t_base, int c_base, long s_row, long s_ch, int accumulate) {
+                                    int Cpk, int Ktot, int t_base, int c_base, long s_row, long s_ch, int accumulate,
+                                    int nrep, long rep_stride) {
   const long total = (long)nrow * nch * T;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int t = (int)(i % T);
     const long rc = i / T;
     const int c = (int)(rc % nch);
     const int row = (int)(rc / nch);
-    const float v = src[(long)row * Ktot + (t_base + t) * Cpk + c_base + c];
+    const long si = (long)row * Ktot + (t_base + t) * Cpk + c_base + c;
+    float v = 0.f;
+    for (int r = 0; r < nrep; ++r) v += src[r * rep_stride + si];   // sum of the atomic replicas
     float* d = dst + row * s_row + c * s_ch + t;
     *d = accumulate ? *d + v : v;
   }
@@ -991,7 +1001,17 @@ static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
   tl.inv_hwv = 1.0f / (float)tl.HWv;
   tl.tiles_y = cdiv(g.OH, tl.TH);
   tl.tiles_x = cdiv(g.OW, tl.TW);
+  if (256 + tl.HH * tl.HWv > 16 * kDwWaves * kDwStage) return false;   // the pipelined staging registers
   return wgrad_halo_lds(tl) <= 64 * 1024;
+}
+
+// dW replicas for the halo path: as many as fit in ~4 MB (at most 16)
+int conv_wgrad_replicas(const ConvGeom& g, bool trans) {
+  DwTile tl{};
+  if (trans || !wgrad_halo_ok(g, tl)) return 1;
+  const long bytes = 4L * g.Go * g.Cgo * g.T * g.Gi * g.Cgi;
+  long r = (4L << 20) / std::max(bytes, 1L);
+  return (int)std::max(1L, std::min(16L, r));
 }
 
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
@@ -1001,22 +1021,23 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
   WgradPtrs P{};
   for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
   for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT, s);
+  const int nrep = conv_wgrad_replicas(g, trans);
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT * nrep, s);
   DwTile tl{};
   if (!trans && wgrad_halo_ok(g, tl)) {
     const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;
     const int gy = cdiv(rows, DW_CH), gz = cdiv(g.Gi * g.Cgi, DW_CH);
-    // Blocks split the tiles and add their dW slab with fp32 atomics: atomic bytes = nsplit * rows * KT * 4
-    // at ~1.3 TB/s chip-wide, so keep nsplit near 3 blocks per CU (LDS-limited residency) -- enough
-    // to overlap one block's staging with another's MFMA phase -- rather than one tile per block.
+    // Blocks split the tiles and add their dW slab with fp32 atomics (into nrep replicas): atomic bytes
+    // = nsplit * rows * KT * 4, so one 8-wave block per CU that software-pipelines its ~8 tiles beats
+    // more, shorter-lived blocks.
     long nsplit = kDwSplitTarget / ((long)gy * gz);
     if (nsplit < 1) nsplit = 1;
     if (nsplit > ntiles) nsplit = ntiles;
     const size_t lds = wgrad_halo_lds(tl);
     dim3 grid((unsigned)nsplit, gy, gz);
-    const int npw = cdiv(2 * g.T, 4);
-#define HW_(N_) if (npw == N_) { hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_>), grid, dim3(256), lds, s, P, dw, g, tl, KT, ntiles); return; }
-    HW_(1) HW_(2) HW_(3) HW_(4) HW_(5)
+    const int npw = cdiv(2 * g.T, kDwWaves);
+#define HW_(N_) if (npw == N_) { hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, tl, KT, ntiles, nrep); return; }
+    HW_(1) HW_(2) HW_(3)
 #undef HW_
   }
   const long M = (long)g.N * g.OH * g.OW;
@@ -1053,8 +1074,8 @@ void pack_batch(const int64_t* jobs, const int* prefix, int njobs, int total_blo
 int pack_per_block() { return kPackPerBlock; }
 
 void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base, int c_base,
-                  long s_row, long s_ch, bool accumulate, hipStream_t s) {
+                  long s_row, long s_ch, bool accumulate, int nrep, long rep_stride, hipStream_t s) {
   const long total = (long)nrow * nch * T;
   hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid1d(total)), dim3(256), 0, s, src, dst, nrow, nch, T, Cpk, Ktot,
-                     t_base, c_base, s_row, s_ch, accumulate ? 1 : 0);
+                     t_base, c_base, s_row, s_ch, accumulate ? 1 : 0, nrep, rep_stride);
 }

@@ -42,6 +42,7 @@ bool conv_uses_halo(const ConvGeom& g, bool trans);
 long conv_stat_blocks(const ConvGeom& g);
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
+int conv_wgrad_replicas(const ConvGeom& g, bool trans);
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
                 hipStream_t s);
 // dst[row][(t_base + t)*Cpk + c_base + c] = src[row*s_row + c*s_ch + t], row < nrow, c < nch, t < T
@@ -53,7 +54,7 @@ void pack_batch(const int64_t* jobs, const int* prefix, int njobs, int total_blo
 int pack_per_block();
 // dst[row*s_row + c*s_ch + t] (+)= src[row*Ktot + (t_base + t)*Cpk + c_base + c]
 void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base, int c_base,
-                  long s_row, long s_ch, bool accumulate, hipStream_t s);
+                  long s_row, long s_ch, bool accumulate, int nrep, long rep_stride, hipStream_t s);
 
 // bn.hip  (P = number of pixels, Cp = padded channels; partial buffers are [nblk][2][Cp] fp32)
 constexpr int kMaxSumInputs = 8;

@@ -286,7 +286,8 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
     dims = plan.fwd_dims(n, ih, iw, oh, ow)
     dy, dx = _taps(plan.taps_fwd)
     KT = plan.T * plan.Cip
-    dwp = torch.empty(plan.rows * KT, dtype=torch.float32, device=dev)
+    nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # atomic-spreading dW replicas, summed on unpack
+    dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
     C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False)
     cin_tot = plan.Gi * plan.ci_l
     for b, nd in zip(plan.branches, need):
@@ -298,7 +299,7 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
         flat = dst.view(-1)
         for gi in range(plan.Gi):
             C.unpack_wgrad(src, flat[gi * plan.ci_l * b.T:], plan.co_l, plan.ci_l, b.T, plan.Cip, KT, b.t_base,
-                           gi * plan.Cgi, cin_tot * b.T, b.T, True)
+                           gi * plan.Cgi, cin_tot * b.T, b.T, True, nrep, plan.rows * KT)
         res.append(None if b.sink is not None else dst)
     return res
 
