@@ -167,6 +167,38 @@ void bn_finalize_t(const at::Tensor& tmp, int64_t C, int64_t Cp, double count, c
               st, st + Cp, st + 2 * Cp, st + 3 * Cp, cur_stream());
 }
 
+void bn_reduce_finalize_t(const at::Tensor& part, int64_t nblk, int64_t width, int64_t col_off, int64_t C, int64_t Cp,
+                          const at::Tensor& tmp, const at::Tensor& cnt, double count,
+                          const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                          const c10::optional<at::Tensor>& rmean, const c10::optional<at::Tensor>& rvar,
+                          double momentum, double eps, const at::Tensor& stats) {
+  CHECK_F32(part); CHECK_F64(tmp); CHECK_F32(stats); CHECK_DEV(cnt);
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.numel() >= bn_rf_chunks(Cp), "cnt: int32 >= Cp/32 counters");
+  TORCH_CHECK(part.numel() >= nblk * 2 * width && col_off + Cp <= width, "partials too small");
+  TORCH_CHECK(tmp.numel() >= (int64_t)bn_reduce_splits(nblk) * 2 * Cp, "tmp too small");
+  TORCH_CHECK(stats.numel() == 4 * Cp, "stats = [scale, shift, mean, invstd] x Cp");
+  float* st = f32(stats);
+  bn_reduce_finalize(f32(part), nblk, width, col_off, C, Cp, tmp.data_ptr<double>(),
+                     reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), (float)count, f32_opt(gamma), f32_opt(beta),
+                     f32_opt_mut(rmean), f32_opt_mut(rvar), (float)momentum, (float)eps, st, st + Cp, st + 2 * Cp,
+                     st + 3 * Cp, cur_stream());
+}
+
+void bn_reduce_bwd_finalize_t(const at::Tensor& part, int64_t nblk, int64_t C, int64_t Cp, const at::Tensor& tmp,
+                              const at::Tensor& cnt, double count, const at::Tensor& stats,
+                              const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+                              const at::Tensor& coef, double pscale) {
+  CHECK_F32(part); CHECK_F64(tmp); CHECK_F32(stats); CHECK_F32(coef); CHECK_DEV(cnt);
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.numel() >= bn_rf_chunks(Cp), "cnt: int32 >= Cp/32 counters");
+  TORCH_CHECK(part.numel() >= nblk * 2 * Cp, "partials too small");
+  TORCH_CHECK(tmp.numel() >= (int64_t)bn_reduce_splits(nblk) * 2 * Cp, "tmp too small");
+  TORCH_CHECK(coef.numel() == 3 * Cp && stats.numel() == 4 * Cp);
+  const float* st = f32(stats);
+  bn_reduce_bwd_finalize(f32(part), nblk, C, Cp, tmp.data_ptr<double>(), reinterpret_cast<unsigned*>(cnt.data_ptr<int>()),
+                         (float)count, st, st + 3 * Cp, st + 2 * Cp, f32_opt_mut(dgamma), f32_opt_mut(dbeta), f32(coef),
+                         (float)pscale, cur_stream());
+}
+
 void bn_act_apply_t(const at::Tensor& y, const at::Tensor& stats, const at::Tensor& z, int64_t P, int64_t Cp, bool relu) {
   CHECK_BF16(y); CHECK_BF16(z); CHECK_F32(stats);
   TORCH_CHECK(y.numel() == P * Cp && z.numel() == P * Cp && stats.numel() == 4 * Cp);
@@ -325,6 +357,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_reduce_splits", [](int64_t nblk) { return bn_reduce_splits(nblk); });
   m.def("bn_collapse", &bn_collapse_t);
   m.def("bn_finalize", &bn_finalize_t);
+  m.def("bn_reduce_finalize", &bn_reduce_finalize_t);
+  m.def("bn_reduce_bwd_finalize", &bn_reduce_bwd_finalize_t);
+  m.def("bn_rf_chunks", [](int64_t Cp) { return bn_rf_chunks((int)Cp); });
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),

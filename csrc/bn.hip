@@ -78,6 +78,7 @@ __global__ __launch_bounds__(256) void reduce_partials_stage1(const float* __res
   if (col < ncol) {
     const int sidx = col / Cp, c = col - sidx * Cp;
     const float* src = part + (long)sidx * width + col_off + c;
+#pragma unroll 8
     for (long b = r0 + rl; b < r1; b += kRedRows) acc += (double)src[b * 2 * width];
   }
   red[rl][cl] = acc;
@@ -93,6 +94,7 @@ __global__ void reduce_partials_stage2(const double* __restrict__ tmp, int split
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= ncol) return;
   double s = 0.0;
+#pragma unroll 8
   for (int i = 0; i < splits; ++i) s += tmp[(long)i * ncol + col];
   sums[col] = s;
 }
@@ -121,37 +123,68 @@ DEVI void split_sum2(const double* __restrict__ tmp, int S, int Cp, int c, bool 
   for (int i = 0; i < kFinParts; ++i) { a += red[0][i][cl]; b += red[1][i][cl]; }
 }
 
-__global__ __launch_bounds__(kFinCols * kFinParts) void bn_finalize_kernel(
-    const double* __restrict__ tmp, int S, int C, int Cp, float count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
-    int training, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out) {
+struct FinFwd {   // forward finalize operands
+  float count, momentum, eps;
+  const float* gamma; const float* beta;
+  float* rmean; float* rvar;
+  float* scale; float* shift; float* mean; float* invstd;
+};
+struct FinBwd {   // backward finalize operands
+  float count, pscale;
+  const float* scale; const float* invstd; const float* mean;
+  float* dgamma; float* dbeta; float* coef;
+};
+
+// nn.BatchNorm2d training semantics: biased variance normalises, the running variance takes the
+// unbiased one, padded channels (C <= c < Cp) get zero scale/shift.
+DEVI void fin_fwd_channel(int c, int C, int Cp, bool training, double sm, double sq, const FinFwd& f) {
+  if (c >= Cp) return;
+  if (c >= C) { f.scale[c] = 0.f; f.shift[c] = 0.f; f.mean[c] = 0.f; f.invstd[c] = 0.f; return; }
+  float mean, var;
+  if (training) {
+    const double m = sm / f.count;
+    double v = sq / f.count - m * m;
+    if (v < 0) v = 0;
+    mean = (float)m; var = (float)v;
+    if (f.rmean != nullptr) {
+      const float unbiased = f.count > 1.f ? (float)(v * f.count / (f.count - 1.f)) : (float)v;
+      f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
+      f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
+    }
+  } else {
+    mean = f.rmean[c]; var = f.rvar[c];
+  }
+  const float inv = rsqrtf(var + f.eps);
+  const float gm = f.gamma != nullptr ? f.gamma[c] : 1.f;
+  const float bt = f.beta != nullptr ? f.beta[c] : 0.f;
+  f.scale[c] = gm * inv;
+  f.shift[c] = bt - mean * gm * inv;
+  f.mean[c] = mean;
+  f.invstd[c] = inv;
+}
+
+// dx = k1*dzr + k2*y + k3.  SyncBN: the sums are global; dgamma/dbeta take pscale = 1/world of them so
+// that the DDP-style average over ranks (sum all-reduce * 1/world) yields the mean of the per-rank
+// local gradients.
+DEVI void fin_bwd_channel(int c, int C, int Cp, double sdd, double sdxd, const FinBwd& f) {
+  if (c >= Cp) return;
+  if (c >= C) { f.coef[c] = 0.f; f.coef[Cp + c] = 0.f; f.coef[2 * Cp + c] = 0.f; return; }
+  const float sd = (float)sdd, sdx = (float)sdxd;
+  if (f.dgamma != nullptr) f.dgamma[c] += f.pscale * sdx * f.invstd[c];
+  if (f.dbeta != nullptr) f.dbeta[c] += f.pscale * sd;
+  const float k1 = f.scale[c];
+  const float k2 = -k1 * f.invstd[c] * f.invstd[c] * sdx / f.count;
+  const float k3 = -k1 * sd / f.count - k2 * f.mean[c];
+  f.coef[c] = k1; f.coef[Cp + c] = k2; f.coef[2 * Cp + c] = k3;
+}
+
+__global__ __launch_bounds__(kFinCols * kFinParts) void bn_finalize_kernel(const double* __restrict__ tmp, int S,
+                                                                            int C, int Cp, int training, FinFwd f) {
   const int c = blockIdx.x * kFinCols + (int)(threadIdx.x % kFinCols);
   double sm = 0.0, sq = 0.0;
   if (training) split_sum2(tmp, S, Cp, c, c < C, sm, sq);
-  if (threadIdx.x >= kFinCols || c >= Cp) return;
-  if (c >= C) { scale[c] = 0.f; shift[c] = 0.f; mean_out[c] = 0.f; invstd_out[c] = 0.f; return; }
-  float mean, var;
-  if (training) {
-    const double m = sm / count;
-    double v = sq / count - m * m;
-    if (v < 0) v = 0;
-    mean = (float)m; var = (float)v;
-    if (rmean != nullptr) {
-      const float unbiased = count > 1.f ? (float)(v * count / (count - 1.f)) : (float)v;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
-    }
-  } else {
-    mean = rmean[c]; var = rvar[c];
-  }
-  const float inv = rsqrtf(var + eps);
-  const float gm = gamma != nullptr ? gamma[c] : 1.f;
-  const float bt = beta != nullptr ? beta[c] : 0.f;
-  scale[c] = gm * inv;
-  shift[c] = bt - mean * gm * inv;
-  mean_out[c] = mean;
-  invstd_out[c] = inv;
+  if (threadIdx.x >= kFinCols) return;
+  fin_fwd_channel(c, C, Cp, training != 0, sm, sq, f);
 }
 
 __global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __restrict__ y,
@@ -224,24 +257,73 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
 
 // coef[3][Cp]: dy = k1*dzr + k2*y + k3  (k1 = gamma*invstd, k2 = -k1*invstd*sum(dzr*xmu)/M,
 // k3 = -k1*sum(dzr)/M - k2*mean).  dgamma/dbeta are ACCUMULATED into the fp32 parameter grads.
-__global__ __launch_bounds__(kFinCols * kFinParts) void bn_bwd_finalize_kernel(
-    const double* __restrict__ tmp, int S, int C, int Cp, float count, const float* __restrict__ scale,
-    const float* __restrict__ invstd, const float* __restrict__ mean, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ coef, float pscale) {
+__global__ __launch_bounds__(kFinCols * kFinParts) void bn_bwd_finalize_kernel(const double* __restrict__ tmp, int S,
+                                                                                int C, int Cp, FinBwd f) {
   const int c = blockIdx.x * kFinCols + (int)(threadIdx.x % kFinCols);
   double a, b;
   split_sum2(tmp, S, Cp, c, c < C, a, b);
-  if (threadIdx.x >= kFinCols || c >= Cp) return;
-  if (c >= C) { coef[c] = 0.f; coef[Cp + c] = 0.f; coef[2 * Cp + c] = 0.f; return; }
-  const float sd = (float)a, sdx = (float)b;
-  // SyncBN: the sums are global; dgamma/dbeta take pscale = 1/world of them so that the DDP-style
-  // average over ranks (sum all-reduce * 1/world) yields the mean of the per-rank local gradients.
-  if (dgamma != nullptr) dgamma[c] += pscale * sdx * invstd[c];
-  if (dbeta != nullptr) dbeta[c] += pscale * sd;
-  const float k1 = scale[c];
-  const float k2 = -k1 * invstd[c] * invstd[c] * sdx / count;
-  const float k3 = -k1 * sd / count - k2 * mean[c];
-  coef[c] = k1; coef[Cp + c] = k2; coef[2 * Cp + c] = k3;
+  if (threadIdx.x >= kFinCols) return;
+  fin_bwd_channel(c, C, Cp, a, b, f);
+}
+
+// Fused column reduction + finalize (single-rank BN): grid (Cp/32 channel chunks, S row splits),
+// 256 threads = 64 columns (32 channels x {sum, sum^2}) x 4 row lanes.  Every block publishes its
+// fp64 column sums with agent-scope stores, drains, and bumps its chunk's arrival counter; the LAST
+// arriving block of a chunk acquires, sums the S split rows in fixed order (deterministic) and
+// finalizes those channels, then re-arms the counter for the next BN (kernels on a stream run in
+// order, so one counter array serves every call).  Replaces stage-1 + finalize launches.
+constexpr int kRfCh = 32;
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const float* __restrict__ part, long nblk, int width,
+                                                                 int col_off, int C, int Cp, double* __restrict__ tmp,
+                                                                 unsigned* __restrict__ cnt, FinFwd ff, FinBwd fb) {
+  __shared__ double red[4][64];
+  __shared__ int s_last;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int which = cl >> 5, ch = blockIdx.x * kRfCh + (cl & 31);
+  const long per = (nblk + gridDim.y - 1) / gridDim.y;
+  const long r0 = (long)blockIdx.y * per;
+  const long r1 = r0 + per < nblk ? r0 + per : nblk;
+  double acc = 0.0;
+  if (ch < Cp) {
+    const float* src = part + (long)which * width + col_off + ch;
+#pragma unroll 8
+    for (long b = r0 + rl; b < r1; b += 4) acc += (double)src[b * 2 * width];
+  }
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && ch < Cp) {
+    const double s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    __hip_atomic_store(&tmp[(long)blockIdx.y * 2 * Cp + which * Cp + ch], s, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains before the arrival
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.y - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // last block of this chunk: 64 columns x 4 lanes sum the S rows (lane-strided, fixed order)
+  const int S = gridDim.y;
+  double t = 0.0;
+  if (ch < Cp)
+#pragma unroll 8
+    for (int k = rl; k < S; k += 4) t += tmp[(long)k * 2 * Cp + which * Cp + ch];
+  __syncthreads();
+  red[rl][cl] = t;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int c = blockIdx.x * kRfCh + threadIdx.x;
+    const double a = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    const double b = red[0][32 + threadIdx.x] + red[1][32 + threadIdx.x] + red[2][32 + threadIdx.x] +
+                     red[3][32 + threadIdx.x];
+    if (BWD) fin_bwd_channel(c, C, Cp, a, b, fb);
+    else fin_fwd_channel(c, C, Cp, true, a, b, ff);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
@@ -309,8 +391,30 @@ void bn_collapse(const double* tmp, int S, int Cp, double* out, hipStream_t s) {
 void bn_finalize(const double* tmp, int S, int C, int Cp, float count, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, int training,
                  float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp, count, gamma, beta,
-                     running_mean, running_var, momentum, eps, training, scale, shift, mean, invstd);
+  const FinFwd f{count, momentum, eps, gamma, beta, running_mean, running_var, scale, shift, mean, invstd};
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp,
+                     training, f);
+}
+
+int bn_rf_chunks(int Cp) { return cdiv(Cp, kRfCh); }
+
+void bn_reduce_finalize(const float* part, long nblk, int width, int col_off, int C, int Cp, double* tmp,
+                        unsigned* cnt, float count, const float* gamma, const float* beta, float* running_mean,
+                        float* running_var, float momentum, float eps, float* scale, float* shift, float* mean,
+                        float* invstd, hipStream_t s) {
+  const FinFwd f{count, momentum, eps, gamma, beta, running_mean, running_var, scale, shift, mean, invstd};
+  const FinBwd b{};
+  hipLaunchKernelGGL((bn_reduce_finalize_kernel<false>), dim3(cdiv(Cp, kRfCh), bn_reduce_splits(nblk)), dim3(256), 0, s,
+                     part, nblk, width, col_off, C, Cp, tmp, cnt, f, b);
+}
+
+void bn_reduce_bwd_finalize(const float* part, long nblk, int C, int Cp, double* tmp, unsigned* cnt, float count,
+                            const float* scale, const float* invstd, const float* mean, float* dgamma, float* dbeta,
+                            float* coef, float pscale, hipStream_t s) {
+  const FinFwd f{};
+  const FinBwd b{count, pscale, scale, invstd, mean, dgamma, dbeta, coef};
+  hipLaunchKernelGGL((bn_reduce_finalize_kernel<true>), dim3(cdiv(Cp, kRfCh), bn_reduce_splits(nblk)), dim3(256), 0, s,
+                     part, nblk, Cp, 0, C, Cp, tmp, cnt, f, b);
 }
 
 void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
@@ -328,8 +432,9 @@ void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scal
 
 void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale, const float* invstd,
                      const float* mean, float* dgamma, float* dbeta, float* coef, float pscale, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp, count, scale,
-                     invstd, mean, dgamma, dbeta, coef, pscale);
+  const FinBwd f{count, pscale, scale, invstd, mean, dgamma, dbeta, coef};
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp,
+                     f);
 }
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

@@ -70,6 +70,14 @@ void bn_collapse(const double* tmp, int S, int Cp, double* out, hipStream_t s);
 void bn_finalize(const double* tmp, int S, int C, int Cp, float count, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, int training,
                  float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+int bn_rf_chunks(int Cp);
+void bn_reduce_finalize(const float* part, long nblk, int width, int col_off, int C, int Cp, double* tmp,
+                        unsigned* cnt, float count, const float* gamma, const float* beta, float* running_mean,
+                        float* running_var, float momentum, float eps, float* scale, float* shift, float* mean,
+                        float* invstd, hipStream_t s);
+void bn_reduce_bwd_finalize(const float* part, long nblk, int C, int Cp, double* tmp, unsigned* cnt, float count,
+                            const float* scale, const float* invstd, const float* mean, float* dgamma, float* dbeta,
+                            float* coef, float pscale, hipStream_t s);
 void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
                   int relu, hipStream_t s);
 void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

@@ -56,6 +56,18 @@ def _world(group):
     return dist.get_world_size(group)
 
 
+_COUNTERS = {}
+
+
+def _counters(dev):
+    """Per-device arrival counters of the fused reduce+finalize kernels (zeroed once; every call
+    re-arms the counters it used, and kernels on a stream run in order)."""
+    t = _COUNTERS.get(dev)
+    if t is None:
+        t = _COUNTERS[dev] = torch.zeros(256, dtype=torch.int32, device=dev)
+    return t
+
+
 def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev):
     """fp64 [S, 2*Cp] split sums (finalize kernels sum the S rows); SyncBN: collapsed to one row and
     all-reduced across the group (one RCCL call of 2*Cp doubles)."""
@@ -88,15 +100,22 @@ class _BNAct(torch.autograd.Function):
         if training:
             if part_info is not None and len(xs) == 1:
                 part, width, col_off = part_info
-                sums = _channel_sums(C, part, part.shape[0], width, col_off, Cp, st.group, dev)
+                nblk = part.shape[0]
             else:
                 nblk = C.bn_partial_blocks(P, Cp)
                 part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
                 C.sum_stats(xs, y if len(xs) > 1 else None, part, P, Cp)
-                sums = _channel_sums(C, part, nblk, Cp, 0, Cp, st.group, dev)
-            count = float(P * _world(st.group))
-            C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
-                          st.eps, True, stats)
+                width, col_off = Cp, 0
+            world = _world(st.group)
+            count = float(P * world)
+            if world == 1:   # one launch: column reduction + finalize (last-arriving block)
+                tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
+                C.bn_reduce_finalize(part, nblk, width, col_off, st.C, Cp, tmp, _counters(dev), count, g_, b_,
+                                     st.running_mean, st.running_var, st.momentum, st.eps, stats)
+            else:            # SyncBN: collapse, RCCL all-reduce, finalize
+                sums = _channel_sums(C, part, nblk, width, col_off, Cp, st.group, dev)
+                C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
+                              st.eps, True, stats)
             if st.count_nbt and st.num_batches_tracked is not None:
                 st.num_batches_tracked.add_(1)
         else:
@@ -124,7 +143,9 @@ class _BNAct(torch.autograd.Function):
         nblk = C.bn_partial_blocks(P, Cp)
         part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
         C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
-        sums = _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
+        world = _world(st.group) if ctx.training else 1
+        fused = ctx.training and world == 1
+        sums = None if fused else _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
         need_g = ctx.needs_input_grad[4] and st.weight_sink is None
         need_b = ctx.needs_input_grad[5] and st.bias_sink is None
         dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
@@ -132,10 +153,13 @@ class _BNAct(torch.autograd.Function):
         g_t = st.weight_sink if st.weight_sink is not None else dgamma
         b_t = st.bias_sink if st.bias_sink is not None else dbeta
         coef = torch.empty(3, Cp, dtype=torch.float32, device=dev)
-        if ctx.training:
+        if fused:            # one launch: column reduction + backward finalize (last-arriving block)
+            tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
+            C.bn_reduce_bwd_finalize(part, nblk, st.C, Cp, tmp, _counters(dev), ctx.count, stats, g_t, b_t, coef, 1.0)
+        elif ctx.training:
             # global (SyncBN) sums -> dgamma/dbeta scaled by 1/world: the bucketed all-reduce-average
             # then yields the mean of the per-rank local parameter gradients (torch SyncBatchNorm).
-            C.bn_bwd_finalize(sums, st.C, Cp, ctx.count, stats, g_t, b_t, coef, 1.0 / _world(st.group))
+            C.bn_bwd_finalize(sums, st.C, Cp, ctx.count, stats, g_t, b_t, coef, 1.0 / world)
         else:
             # eval-mode BN is a per-channel affine map: dx = dzr * scale
             coef[0] = stats[0]
