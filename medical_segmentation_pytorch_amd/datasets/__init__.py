@@ -18,16 +18,20 @@ dataset_hub = {'polyp': PolypDataset, 'synthetic': PolypDataset}
 
 
 def _ensure_data(config):
-    want = config.dataset == 'synthetic' or (config.synthetic_data and not os.path.isdir(str(config.data_root)))
-    if want:
-        root = config.data_root if config.data_root and config.data_root != '/path/to/your/dataset' \
-            else os.path.join(config.save_dir, 'synthetic_polyp')
-        from ..utils.parallel import get_group, group_rank
-        if group_rank(config) == 0:
-            make_synthetic_polyp(root, config.synthetic_num, config.synthetic_size, config.random_seed)
-        if get_group(config) is not None:
-            dist.barrier(group=get_group(config))
-        config.data_root = root
+    # Only rank 0 looks at the file system; every rank takes the barrier.  (A slower rank that
+    # decided by itself would see the directory rank 0 is still writing, skip the barrier and read a
+    # half-written split.)
+    if getattr(config, '_synthetic_ready', False) or not (config.dataset == 'synthetic' or config.synthetic_data):
+        return
+    root = config.data_root if config.data_root and config.data_root != '/path/to/your/dataset' \
+        else os.path.join(config.save_dir, 'synthetic_polyp')
+    from ..utils.parallel import get_group, group_rank
+    if group_rank(config) == 0 and (config.dataset == 'synthetic' or not os.path.isdir(str(config.data_root))):
+        make_synthetic_polyp(root, config.synthetic_num, config.synthetic_size, config.random_seed)
+    if get_group(config) is not None:
+        dist.barrier(group=get_group(config))
+    config.data_root = root
+    config._synthetic_ready = True
 
 
 def get_dataset(config, mode):
