@@ -187,31 +187,51 @@ __global__ __launch_bounds__(kFinCols * kFinParts) void bn_finalize_kernel(const
   fin_fwd_channel(c, C, Cp, training != 0, sm, sq, f);
 }
 
-__global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __restrict__ y,
-                                                              const float* __restrict__ scale,
-                                                              const float* __restrict__ shift,
-                                                              uint16_t* __restrict__ z, long nvec, int CG,
-                                                              int relu) {
-  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
-    const int c0 = (int)(i % CG) * 8;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), v);
-    const float4 a0 = *reinterpret_cast<const float4*>(scale + c0), a1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(shift + c0), b1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
-    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float o = fmaf(v[e], a[e], b[e]);
-      v[e] = relu ? fmaxf(o, 0.f) : o;
-    }
-    *reinterpret_cast<uint4*>(z + i * 8) = pack8(v);
-  }
-}
-
 DEVI void load8f(const float* p, float* d) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// Elementwise BN passes: each thread owns ONE 8-channel group (cg = tid % CG) for all its pixels, so
+// its per-channel coefficients are loaded once into registers (a per-vector reload costs 4-10x the
+// 16 B of activation it serves); rows r = tid / CG of a block walk consecutive pixels (the wave's
+// accesses stay contiguous), and an unroll of kUnroll pixels keeps that many loads in flight.
+constexpr int kUnroll = 4;
+
+__global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __restrict__ y,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              uint16_t* __restrict__ z, long P, int CG,
+                                                              int relu) {
+  const int R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG;
+  if (r >= R) return;
+  float a[8], b[8];
+  load8f(scale + 8 * cg, a);
+  load8f(shift + 8 * cg, b);
+  const long stride = (long)gridDim.x * R;
+  const long Cp = 8L * CG;
+  long p = (long)blockIdx.x * R + r;
+  for (; p < P; p += kUnroll * stride) {
+    uint4 in[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      in[u] = q < P ? *reinterpret_cast<const uint4*>(y + q * Cp + 8 * cg) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      if (q >= P) break;
+      float v[8];
+      unpack8(in[u], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = fmaf(v[e], a[e], b[e]);
+        v[e] = relu ? fmaxf(o, 0.f) : o;
+      }
+      *reinterpret_cast<uint4*>(z + q * Cp + 8 * cg) = pack8(v);
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
@@ -328,27 +348,46 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const float* __
 
 __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
     const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ coef, uint16_t* __restrict__ dy, long nvec,
+    const float* __restrict__ shift, const float* __restrict__ coef, uint16_t* __restrict__ dy, long P,
     int CG, int relu) {
-  const int Cp = CG * 8;
-  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
-    const int c0 = (int)(i % CG) * 8;
-    float g[8], v[8], a[8], b[8], k1[8], k2[8], k3[8];
-    unpack8(*reinterpret_cast<const uint4*>(dz + i * 8), g);
-    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), v);
-    load8f(scale + c0, a); load8f(shift + c0, b);
-    load8f(coef + c0, k1); load8f(coef + Cp + c0, k2); load8f(coef + 2 * Cp + c0, k3);
+  const int R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG;
+  if (r >= R) return;
+  const int Cp = CG * 8, c0 = 8 * cg;
+  float a[8], b[8], k1[8], k2[8], k3[8];
+  load8f(scale + c0, a); load8f(shift + c0, b);
+  load8f(coef + c0, k1); load8f(coef + Cp + c0, k2); load8f(coef + 2 * Cp + c0, k3);
+  const long stride = (long)gridDim.x * R;
+  long p = (long)blockIdx.x * R + r;
+  for (; p < P; p += kUnroll * stride) {
+    uint4 gin[kUnroll], yin[kUnroll];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
-      g[e] = k1[e] * gr + k2[e] * v[e] + k3[e];
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      const bool ok = q < P;
+      gin[u] = ok ? *reinterpret_cast<const uint4*>(dz + q * Cp + c0) : make_uint4(0, 0, 0, 0);
+      yin[u] = ok ? *reinterpret_cast<const uint4*>(y + q * Cp + c0) : make_uint4(0, 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(g);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      if (q >= P) break;
+      float g[8], v[8];
+      unpack8(gin[u], g);
+      unpack8(yin[u], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
+        g[e] = k1[e] * gr + k2[e] * v[e] + k3[e];
+      }
+      *reinterpret_cast<uint4*>(dy + q * Cp + c0) = pack8(g);
+    }
   }
 }
 
-int grid_for(long nvec) {
-  long b = (nvec + kBlock - 1) / kBlock;
+// Grid of the channel-owning elementwise passes: ~kUnroll pixels per thread per loop trip, <= 8192 blocks.
+int grid_rows(long P, int CG) {
+  const long R = kBlock / CG;
+  long b = (P + R * kUnroll - 1) / (R * kUnroll);
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
   return (int)b;
@@ -419,8 +458,7 @@ void bn_reduce_bwd_finalize(const float* part, long nblk, int C, int Cp, double*
 
 void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
                   int relu, hipStream_t s) {
-  const long nvec = P * (Cp / 8);
-  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, y, scale, shift, z, nvec,
+  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), 0, s, y, scale, shift, z, P,
                      Cp / 8, relu);
 }
 
@@ -439,7 +477,6 @@ void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
                       const float* coef, uint16_t* dy, long P, int Cp, int relu, hipStream_t s) {
-  const long nvec = P * (Cp / 8);
-  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, dz, y, scale, shift, coef,
-                     dy, nvec, Cp / 8, relu);
+  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), 0, s, dz, y, scale, shift,
+                     coef, dy, P, Cp / 8, relu);
 }

@@ -65,20 +65,32 @@ DEVI int in_pixel(int pn, int ph, int pw, int2 d, const ConvGeom& g) {
   }
 }
 
-template <int MI, int NJ, int WPX, bool TRANS>
-__global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
+// Output-phase decomposition of a strided TRANS conv (data-gradient of a stride-s conv, forward of
+// ConvTranspose2d): output pixels with (oh % s, ow % s) == (py, px) only see the taps t with
+// (py + dy[t]) % s == 0 and (px + dx[t]) % s == 0, and for those the input pixel is
+// (oh / s + qy[t], ow / s + qx[t]) with qy = (py + dy) / s exact -- a plain stride-1 gather over a
+// (OH/s x OW/s) sub-grid.  The host launches one grid per phase with the reduced tap table (qy, qx)
+// in g.dy/g.dx and tA[] = the taps' positions in the packed weight rows, so the K loop covers only
+// the Tv valid taps (a 3x3 s2 data-gradient does 2.25 of 9 taps' work on average, not 9).
+struct PhaseArgs { int s, py, px, OHp, OWp, Kloop; int tA[kMaxTaps]; };
+
+template <int MI, int NJ, int WPX, bool TRANS, bool PH = false>
+__global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseArgs pa) {
   const ConvGeom& g = a.g;
   __shared__ int2 s_tap[kMaxTaps];
+  __shared__ int s_ta[PH ? kMaxTaps : 1];
   __shared__ const uint16_t* s_x[kMaxGroups];
   __shared__ uint16_t* s_y[kMaxGroups];
   __shared__ float s_stat[WPX][2][16 * MI];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid], g.dx[tid]);
+  if (PH && tid < kMaxTaps) s_ta[tid] = pa.tA[tid];
   if (tid < kMaxGroups) { s_x[tid] = a.x[tid]; s_y[tid] = a.y[tid]; }
   __syncthreads();
 
-  const long OHW = (long)g.OH * g.OW;
+  const long OHW = PH ? (long)pa.OHp * pa.OWp : (long)g.OH * g.OW;
   const long M = (long)g.N * OHW;
+  const int Kloop = PH ? pa.Kloop : g.Kp;
   const int rows = g.Go * g.Cgo;
   // 1-D grid, XCD-aware: blocks sharing a pixel tile (all co tiles of it) get consecutive logical
   // ids placed on ONE XCD (bijective remap of the round-robin dispatch, guide T1), so the input
@@ -101,17 +113,18 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
     if (m < M) {
       const int n = (int)(m / OHW);
       const int r = (int)(m - (long)n * OHW);
-      const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
+      const int RW = PH ? pa.OWp : g.OW;   // PH: (oh, ow) index the phase sub-grid
+      const int oh = r / RW, ow = r - (r / RW) * RW;
       pn[j] = n * IHW;
-      ph[j] = TRANS ? oh : oh * g.stride;
-      pw[j] = TRANS ? ow : ow * g.stride;
+      ph[j] = (TRANS || PH) ? oh : oh * g.stride;
+      pw[j] = (TRANS || PH) ? ow : ow * g.stride;
     } else {
       pn[j] = -1; ph[j] = 0; pw[j] = 0;
     }
   }
   const uint16_t* wrow[MI];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + 8 * lg;
+  for (int i = 0; i < MI; ++i) wrow[i] = a.w + (long)(co0 + 16 * i + lr) * g.Kp + (PH ? 0 : 8 * lg);
 
   KPos kp = kpos_init(8 * lg, g);
 
@@ -129,9 +142,16 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
       B[j] = v;
     }
   };
-  auto load_a = [&](uint4* A, int k0) {
+  auto load_a = [&](uint4* A, int k0, const KPos& p) {
+    if (PH) {   // the lane's 8 k sit at tap s_ta[t] of the full packed row (zero past the valid taps)
+      const int off = p.t < g.T ? s_ta[p.t] * (g.Gi * g.Cgi) + p.gi * g.Cgi + p.cl : -1;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + k0);
+      for (int i = 0; i < MI; ++i)
+        A[i] = off >= 0 ? *reinterpret_cast<const uint4*>(wrow[i] + off) : make_uint4(0, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + k0);
+    }
   };
 
   f32x4_t acc[MI][NJ];
@@ -141,14 +161,14 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   uint4 A[MI], B[NJ];
-  load_a(A, 0);
+  load_a(A, 0, kp);
   load_b(B, kp);
-  for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+  for (int k0 = 0; k0 < Kloop; k0 += 32) {
     uint4 An[MI], Bn[NJ];
-    const bool more = k0 + 32 < g.Kp;
+    const bool more = k0 + 32 < Kloop;
     if (more) {
       kpos_advance(kp, 32, g);
-      load_a(An, k0 + 32);
+      load_a(An, k0 + 32, kp);
       load_b(Bn, kp);
     }
 #pragma unroll
@@ -181,6 +201,13 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
     for (int j = 0; j < NJ; ++j) {
       const long m = m0 + 16 * j + lr;
       if (m < M) {
+        long mo = m;   // output pixel index
+        if (PH) {
+          const long n = m / OHW;
+          const int r = (int)(m - n * OHW);
+          const int qa = r / pa.OWp, qb = r - qa * pa.OWp;
+          mo = (n * g.OH + (long)qa * pa.s + pa.py) * g.OW + (long)qb * pa.s + pa.px;
+        }
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -189,7 +216,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a) {
           csum[i][r] += v[r];
           csq[i][r] += v[r] * v[r];
         }
-        *reinterpret_cast<uint2*>(yb + m * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        *reinterpret_cast<uint2*>(yb + mo * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
   }
@@ -808,22 +835,32 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
   }
 }
 
-template <int MI, int NJ, int WPX, bool TRANS>
-void launch_igemm(const ConvArgs& a, hipStream_t s) {
-  const long M = (long)a.g.N * a.g.OH * a.g.OW;
+template <int MI, int NJ, int WPX, bool TRANS, bool PH>
+void launch_igemm(const ConvArgs& a, const PhaseArgs& pa, hipStream_t s) {
+  const long M = PH ? (long)a.g.N * pa.OHp * pa.OWp : (long)a.g.N * a.g.OH * a.g.OW;
   const long blocks = (long)cdiv(M, 16 * NJ * WPX) * cdiv(a.g.Go * a.g.Cgo, 16 * MI);
-  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS>), dim3((unsigned)blocks), dim3(64 * WPX), 0, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS, PH>), dim3((unsigned)blocks), dim3(64 * WPX), 0, s, a,
+                     pa);
 }
 
 template <bool TRANS>
 void dispatch_igemm(const ConvArgs& a, int mi, int nj, int wpx, hipStream_t s) {
+  const PhaseArgs pa{};
 #define CASE(MI_, NJ_, WPX_)                                                  \
-  if (mi == MI_ && nj == NJ_ && wpx == WPX_) { launch_igemm<MI_, NJ_, WPX_, TRANS>(a, s); return; }
+  if (mi == MI_ && nj == NJ_ && wpx == WPX_) { launch_igemm<MI_, NJ_, WPX_, TRANS, false>(a, pa, s); return; }
   CASE(1, 4, 4) CASE(2, 4, 4) CASE(3, 4, 4) CASE(4, 4, 4)
   CASE(1, 4, 2) CASE(2, 4, 2) CASE(3, 4, 2) CASE(4, 4, 2)
   CASE(1, 4, 1) CASE(2, 4, 1) CASE(3, 4, 1) CASE(4, 4, 1)
   CASE(1, 8, 4) CASE(2, 8, 4) CASE(1, 8, 2) CASE(2, 8, 2) CASE(1, 8, 1) CASE(2, 8, 1)
 #undef CASE
+}
+
+void dispatch_phase(const ConvArgs& a, const PhaseArgs& pa, int mi, int wpx, hipStream_t s) {
+#define CASEP(MI_, WPX_) if (mi == MI_ && wpx == WPX_) { launch_igemm<MI_, 4, WPX_, false, true>(a, pa, s); return; }
+  CASEP(1, 4) CASEP(2, 4) CASEP(3, 4) CASEP(4, 4)
+  CASEP(1, 2) CASEP(2, 2) CASEP(3, 2) CASEP(4, 2)
+  CASEP(1, 1) CASEP(2, 1) CASEP(3, 1) CASEP(4, 1)
+#undef CASEP
 }
 
 int grid1d(long total) {
@@ -955,8 +992,51 @@ long conv_stat_blocks(const ConvGeom& g) {
   return cdiv(M, 16 * nj * wpx);
 }
 
+static int g_phase_mode = -1;   // -1: from MSP_CONV_PHASE (default on), 0: off, 1: on
+
+static bool phase_enabled() {
+  if (g_phase_mode < 0) { const char* e = getenv("MSP_CONV_PHASE"); g_phase_mode = (e == nullptr || e[0] != '0') ? 1 : 0; }
+  return g_phase_mode == 1;
+}
+
+void conv_set_phase(int on) { g_phase_mode = on ? 1 : 0; }
+
+// Strided TRANS conv as stride x stride phase launches (see PhaseArgs): each phase gathers only its
+// valid taps over its output sub-grid; a phase without taps writes zeros.
+static void conv_igemm_phased(const ConvArgs& a, int mi, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  const int st = g.stride, Cip = g.Gi * g.Cgi;
+  for (int py = 0; py < st; ++py)
+    for (int px = 0; px < st; ++px) {
+      PhaseArgs pa{};
+      pa.s = st; pa.py = py; pa.px = px;
+      pa.OHp = (g.OH - py + st - 1) / st;
+      pa.OWp = (g.OW - px + st - 1) / st;
+      if (pa.OHp <= 0 || pa.OWp <= 0) continue;
+      ConvArgs b = a;
+      int tv = 0;
+      for (int t = 0; t < g.T; ++t) {
+        const int ay = py + g.dy[t], ax = px + g.dx[t];
+        if (((ay % st) + st) % st != 0 || ((ax % st) + st) % st != 0) continue;
+        b.g.dy[tv] = ay / st;   // exact division
+        b.g.dx[tv] = ax / st;
+        pa.tA[tv] = t;
+        ++tv;
+      }
+      b.g.T = tv;
+      pa.Kloop = (tv * Cip + 31) / 32 * 32;
+      ConvGeom gp = b.g;
+      gp.OH = pa.OHp; gp.OW = pa.OWp;
+      dispatch_phase(b, pa, mi, conv_pick_wpx(gp, mi, 4), s);
+    }
+}
+
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   const int mi = conv_pick_mi(a.g.Go * a.g.Cgo);
+  if (trans && a.g.stride > 1 && a.stat_part == nullptr && phase_enabled()) {
+    conv_igemm_phased(a, mi, s);
+    return;
+  }
   HaloGeom hg;
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
     const unsigned blocks = (unsigned)((long)a.g.N * hg.tiles_y * hg.tiles_x);

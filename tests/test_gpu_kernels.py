@@ -34,6 +34,8 @@ CONV_CASES = [
     (2, 8, 8, 136, 68, (1, 1), 1, (0, 0), (1, 1)),
     (1, 11, 11, 272, 544, (3, 3), 1, (1, 1), (1, 1)),
     (3, 9, 7, 40, 72, (3, 3), 1, (1, 1), (1, 1)),
+    (2, 17, 15, 17, 34, (3, 3), 2, (1, 1), (1, 1)),    # odd sizes: uneven output phases in the dgrad
+    (2, 16, 16, 64, 128, (1, 1), 2, (0, 0), (1, 1)),   # ResNet downsample: 3 of 4 dgrad phases are empty
 ]
 
 
@@ -137,6 +139,26 @@ def test_conv_transpose(gpu):
     assert _rel(from_fm_reference(xf.grad, ci), xr.grad) < 2e-2
     assert _rel(m.weight.grad, wr.grad) < 2e-2
     assert _rel(m.bias.grad, br.grad) < 2e-2
+
+
+def test_conv_phase_matches_gather(gpu):
+    """The phase-decomposed strided data-gradient equals the full-tap TRANS gather up to fp32
+    summation order (same products; the compacted K chunks group them differently)."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    C = _ext.require()
+    torch.manual_seed(5)
+    m = nn.Conv2d(34, 68, 3, 2, 1, bias=False).to(gpu)
+    plan = ConvPlan(3, 3, 34, 68, [Branch(m.weight)], stride=2, padding=(1, 1))
+    outs = []
+    for on in (True, False):
+        C.conv_set_phase(on)
+        xf = to_fm_reference(_bf(torch.randn(3, 34, 21, 19, device=gpu, generator=torch.Generator(gpu).manual_seed(0))))
+        xf.requires_grad_(True)
+        (y,), _ = conv(plan, [xf])
+        y.backward(torch.ones_like(y))
+        outs.append(xf.grad.clone())
+    C.conv_set_phase(True)
+    assert _rel(outs[0], outs[1]) < 2e-3
 
 
 @pytest.mark.parametrize('C,k', [(17, 1), (34, 2), (136, 6), (3, 1)])

@@ -88,3 +88,17 @@ def test_activation_hub():
         assert Activation(name)(torch.randn(2, 4)).shape == (2, 4)
     with pytest.raises(NotImplementedError):
         Activation('nope')
+
+
+def test_backbones_and_modules_alias():
+    """reference models/backbone.py (ResNet / Mobilenetv2 4-stage extractors) and models/modules.py path."""
+    from medical_segmentation_pytorch_amd.models import modules
+    from medical_segmentation_pytorch_amd.models.backbone import Mobilenetv2, ResNet
+    assert modules.ConvBNAct is not None and modules.SegHead is not None
+    x = torch.randn(1, 3, 64, 64)
+    r = ResNet('resnet18', pretrained=False)
+    assert [f.shape[1] for f in r(x)] == [64, 128, 256, 512]
+    assert sum(p.numel() for p in r.parameters()) == 11176512          # torchvision resnet18 minus fc
+    assert [f.shape[-1] for f in Mobilenetv2(pretrained=False)(x)] == [16, 8, 4, 2]
+    with pytest.raises(ValueError):
+        ResNet('resnet7')
