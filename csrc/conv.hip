@@ -445,13 +445,16 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   int offA[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) { offA[i][0] = dw_elem(plo, i, p4); offA[i][1] = dw_elem(phi, i, p4); }
-  // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32
-  const int npairs = 2 * g.T;
+  // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32.
+  // Only the 16-channel halves that hold real channels are paired (a 40-channel input's second chunk
+  // has one), and the co half past `rows` is skipped: no MFMA runs on all-padding tiles.
+  const int nhv = min(2, (Cip - ci0 + 15) >> 4), nco = min(2, (rows - co0 + 15) >> 4);
+  const int npairs = nhv * g.T;
   int offB[NPW][2];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
     const int pr = wave + kDwWaves * j;
-    const int t = pr < npairs ? pr >> 1 : 0, cf = pr & 1;
+    const int t = pr < npairs ? pr / nhv : 0, cf = pr < npairs ? pr - t * nhv : 0;
     const int2 d = s_tap[t];
     offB[j][0] = dw_elem((ry_lo + d.x) * tl.HWd + cx_lo + d.y, cf, p4);
     offB[j][1] = dw_elem((ry_hi + d.x) * tl.HWd + cx_hi + d.y, cf, p4);
@@ -509,9 +512,11 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
       uint4 fa[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const uint2 lo = tr_read(&sY[sa + offA[i][0]]);
-        const uint2 hi = tr_read(&sY[sa + offA[i][1]]);
-        fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        if (i < nco) {
+          const uint2 lo = tr_read(&sY[sa + offA[i][0]]);
+          const uint2 hi = tr_read(&sY[sa + offA[i][1]]);
+          fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
       }
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
@@ -520,7 +525,7 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
           const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
           acc[0][j] = mfma16x16x32(fa[0], fb, acc[0][j]);
-          acc[1][j] = mfma16x16x32(fa[1], fb, acc[1][j]);
+          if (nco == 2) acc[1][j] = mfma16x16x32(fa[1], fb, acc[1][j]);
         }
       }
     }
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   for (int j = 0; j < NPW; ++j) {
     const int pr = wave + kDwWaves * j;
     if (pr >= npairs) continue;
-    const int t = pr >> 1, cf = pr & 1;
+    const int t = pr / nhv, cf = pr - t * nhv;
     const int ci = ci0 + 16 * cf + lr;
     if (ci >= Cip) continue;
 #pragma unroll
