@@ -303,6 +303,32 @@ void kd_kl_fwd_bwd_t(const at::Tensor& s, const at::Tensor& t, const at::Tensor&
   kd_kl_fwd_bwd(f32(s), f32(t), f32(grad), f32(part), N, C, HW, (float)T, cur_stream());
 }
 
+void mse_fwd_bwd_t(const at::Tensor& s, const at::Tensor& t, const at::Tensor& grad, const at::Tensor& part) {
+  CHECK_F32(s); CHECK_F32(t); CHECK_F32(grad); CHECK_F32(part);
+  TORCH_CHECK(s.sizes() == t.sizes() && grad.numel() == s.numel() && part.numel() == ce_blocks(s.numel()));
+  mse_fwd_bwd(f32(s), f32(t), f32(grad), f32(part), s.numel(), cur_stream());
+}
+
+void bce_dice_stats_t(const at::Tensor& x, const at::Tensor& t, const at::Tensor& part) {
+  CHECK_F32(x); CHECK_F32(t); CHECK_F32(part);
+  TORCH_CHECK(x.dim() >= 2 && x.numel() == t.numel(), "logits [N, ...] and targets of the same numel");
+  const int N = x.size(0);
+  const long HW = x.numel() / N;
+  TORCH_CHECK(part.numel() == (int64_t)N * bce_dice_splits(HW) * 4, "part must be [N, splits, 4]");
+  bce_dice_stats(f32(x), f32(t), f32(part), N, HW, cur_stream());
+}
+
+void bce_dice_grad_t(const at::Tensor& x, const at::Tensor& t, const at::Tensor& coef, const at::Tensor& gup,
+                     const at::Tensor& grad, double bw, double dw) {
+  CHECK_F32(x); CHECK_F32(t); CHECK_F32(coef); CHECK_F32(gup); CHECK_F32(grad);
+  const int N = x.size(0);
+  const long HW = x.numel() / N;
+  TORCH_CHECK(t.numel() == x.numel() && grad.numel() == x.numel() && coef.numel() == 2 * N && gup.numel() == 1);
+  bce_dice_grad(f32(x), f32(t), f32(coef), f32(gup), f32(grad), N, HW, (float)bw, (float)dw, cur_stream());
+}
+
+int64_t bce_dice_splits_t(int64_t HW) { return bce_dice_splits(HW); }
+
 void adam_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
                  const at::Tensor& hyper, bool adamw) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(hyper);
@@ -375,6 +401,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("ce_blocks", &ce_blocks_t);
   m.def("ce_fwd_bwd", &ce_fwd_bwd_t);
   m.def("kd_kl_fwd_bwd", &kd_kl_fwd_bwd_t);
+  m.def("mse_fwd_bwd", &mse_fwd_bwd_t);
+  m.def("bce_dice_stats", &bce_dice_stats_t);
+  m.def("bce_dice_grad", &bce_dice_grad_t);
+  m.def("bce_dice_splits", &bce_dice_splits_t);
   m.def("adam_step", &adam_step_t);
   m.def("sgd_step", &sgd_step_t);
   m.def("ema_update", &ema_update_t);

@@ -104,6 +104,13 @@ void ce_fwd_bwd(const float* logits, const int64_t* target, const float* weight,
                 float* pix_loss, float* part, int N, int C, long HW, int ignore_index, hipStream_t s);
 void kd_kl_fwd_bwd(const float* s_logits, const float* t_logits, float* grad, float* part, int N, int C,
                    long HW, float T, hipStream_t s);
+// part[ce_blocks(n)] = partial sums of (s - t)^2; grad = 2 (s - t) / n
+void mse_fwd_bwd(const float* s_, const float* t, float* grad, float* part, long n, hipStream_t s);
+// binary logits / targets fp32 [N, HW]: part [N][bce_dice_splits(HW)][4]; coef [N][2]; gup device scalar
+int bce_dice_splits(long HW);
+void bce_dice_stats(const float* x, const float* t, float* part, int N, long HW, hipStream_t s);
+void bce_dice_grad(const float* x, const float* t, const float* coef, const float* gup, float* grad, int N, long HW,
+                   float bw, float dw, hipStream_t s);
 
 // optim.hip  (flat fp32 buffers; hyper = device fp32 array, see optim.hip for the layout)
 void adam_step(float* p, const float* g, float* m, float* v, const float* hyper, long n, int adamw,

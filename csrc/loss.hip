@@ -3,6 +3,10 @@
 //                   per-pixel loss for OHEM (reference core/loss.py:6-31).
 //   kd_kl_fwd_bwd : F.kl_div(log_softmax(s/T), softmax(t/T)) * T^2, elementwise-mean reduction
 //                   (reference core/loss.py:42-46).
+//   mse_fwd_bwd   : F.mse_loss(s, t) (KD 'mse', reference core/loss.py:47-48).
+//   bce_dice_*    : binary (num_class == 1) BCE-with-logits + per-sample soft Dice on the sigmoid
+//                   (SURVEY Appendix E.1): a per-sample reduction pass, then the gradient pass once the
+//                   sample's Dice sums are known.
 // Partials are per block ([nblk][2] = {weighted loss sum, weight sum}); the host sums them.
 #include "common.h"
 #include "launchers.h"
@@ -90,6 +94,75 @@ __global__ __launch_bounds__(kBlock) void kd_kl_kernel(const float* __restrict__
     part[blockIdx.x] = a;
   }
 }
+__global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                     float* __restrict__ grad, float* __restrict__ part, long n) {
+  __shared__ float red[kBlock / 64];
+  const float gs = 2.f / (float)n;
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) {
+    const float d = s[i] - t[i];
+    acc += d * d;
+    grad[i] = gs * d;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f;
+    for (int w = 0; w < kBlock / 64; ++w) a += red[w];
+    part[blockIdx.x] = a;
+  }
+}
+
+DEVI float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// grid (splits, N): block (b, n) reduces its slice of sample n into part[n][b][4] =
+// {sum BCE, sum p*t, sum p, sum t}.
+__global__ __launch_bounds__(kBlock) void bce_dice_stats_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                                                float* __restrict__ part, long HW) {
+  __shared__ float red[4][kBlock / 64];
+  const int n = blockIdx.y;
+  const float* xs = x + (long)n * HW;
+  const float* ts = t + (long)n * HW;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < HW; i += (long)gridDim.x * kBlock) {
+    const float v = xs[i], y = ts[i];
+    const float p = sigmoidf(v);
+    a[0] += fmaxf(v, 0.f) - v * y + log1pf(__expf(-fabsf(v)));
+    a[1] += p * y;
+    a[2] += p;
+    a[3] += y;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float w = wave_sum(a[k]);
+    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+    for (int w = 0; w < kBlock / 64; ++w) v += red[threadIdx.x][w];
+    part[((long)n * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = v;
+  }
+}
+
+// d/dx of  bw * mean(BCE) + dw * (1 - mean_n (2 I_n + s) / (D_n + s)),  scaled by the upstream
+// gradient *gup (a device scalar: no host sync).  coef[n] = {D_n + s, 2 I_n + s}.
+__global__ __launch_bounds__(kBlock) void bce_dice_grad_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                                               const float* __restrict__ coef,
+                                                               const float* __restrict__ gup, float* __restrict__ grad,
+                                                               int N, long HW, float bw, float dw) {
+  const long total = (long)N * HW;
+  const float g0 = gup[0];
+  const float kb = bw / (float)total, kd = dw / (float)N;
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int n = (int)(i / HW);
+    const float den = coef[2 * n], num = coef[2 * n + 1];
+    const float p = sigmoidf(x[i]), y = t[i];
+    const float gd = -kd * p * (1.f - p) * (2.f * y * den - num) / (den * den);
+    grad[i] = g0 * (kb * (p - y) + gd);
+  }
+}
 }  // namespace
 
 long ce_blocks(long P) {
@@ -110,4 +183,25 @@ void kd_kl_fwd_bwd(const float* s_logits, const float* t_logits, float* grad, fl
                    float T, hipStream_t s) {
   hipLaunchKernelGGL(kd_kl_kernel, dim3(ce_blocks((long)N * HW)), dim3(kBlock), 0, s, s_logits, t_logits, grad,
                      part, N, C, HW, T);
+}
+
+void mse_fwd_bwd(const float* s_, const float* t, float* grad, float* part, long n, hipStream_t s) {
+  hipLaunchKernelGGL(mse_kernel, dim3(ce_blocks(n)), dim3(kBlock), 0, s, s_, t, grad, part, n);
+}
+
+int bce_dice_splits(long HW) {
+  long b = (HW + kBlock * 16 - 1) / (kBlock * 16);
+  if (b > 256) b = 256;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+void bce_dice_stats(const float* x, const float* t, float* part, int N, long HW, hipStream_t s) {
+  hipLaunchKernelGGL(bce_dice_stats_kernel, dim3(bce_dice_splits(HW), N), dim3(kBlock), 0, s, x, t, part, HW);
+}
+
+void bce_dice_grad(const float* x, const float* t, const float* coef, const float* gup, float* grad, int N, long HW,
+                   float bw, float dw, hipStream_t s) {
+  hipLaunchKernelGGL(bce_dice_grad_kernel, dim3(ce_blocks((long)N * HW)), dim3(kBlock), 0, s, x, t, coef, gup, grad,
+                     N, HW, bw, dw);
 }

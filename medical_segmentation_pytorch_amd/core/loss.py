@@ -63,6 +63,9 @@ class BceDiceLoss(nn.Module):
     def forward(self, logits, labels):
         logits = logits.float()
         target = labels.float().view_as(logits) if labels.dim() == logits.dim() else labels.float().unsqueeze(1)
+        if _fused_ok(logits):
+            from ..ops.losses import bce_dice
+            return bce_dice(logits, target, self.bw, self.dw, self.smooth)
         bce = F.binary_cross_entropy_with_logits(logits, target)
         p = torch.sigmoid(logits)
         inter = (p * target).flatten(1).sum(1)
@@ -94,5 +97,8 @@ def kd_loss_fn(config, outputs, outputsT):
         return F.kl_div(F.log_softmax(outputs / T, dim=1), F.softmax(outputsT.detach() / T, dim=1),
                         reduction='mean') * T ** 2
     if config.kd_loss_type == 'mse':
+        if _fused_ok(outputs):
+            from ..ops.losses import kd_mse
+            return kd_mse(outputs.float(), outputsT.detach().float())
         return F.mse_loss(outputs, outputsT.detach())
     raise NotImplementedError(f'Unsupport kd loss type: {config.kd_loss_type}')

@@ -7,6 +7,10 @@
   losses come from the same fused kernel; selection (threshold, top-k fallback) uses torch.
 * :func:`kd_kl_div` == ``F.kl_div(log_softmax(s/T), softmax(t/T)) * T**2`` with the default
   elementwise-mean reduction (reference ``core/loss.py:42-46``).
+* :func:`kd_mse` == ``F.mse_loss(s, t)`` (reference ``core/loss.py:47-48``), one fused pass.
+* :func:`bce_dice` == ``bw * BCEWithLogits + dw * (1 - mean_n soft-Dice_n)`` for binary heads
+  (``num_class == 1``): a per-sample reduction kernel in forward, the gradient
+  kernel in backward (it needs the sample's Dice sums), upstream gradient read on the device.
 """
 from __future__ import annotations
 
@@ -99,3 +103,56 @@ class _KDKL(torch.autograd.Function):
 
 def kd_kl_div(student, teacher, T=4.0):
     return _KDKL.apply(student, teacher, float(T))
+
+
+class _MSE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t):
+        C = require()
+        s = s.contiguous().float()
+        t = t.detach().contiguous().float()
+        grad = torch.empty_like(s)
+        part = torch.empty(C.ce_blocks(s.numel()), dtype=torch.float32, device=s.device)
+        C.mse_fwd_bwd(s, t, grad, part)
+        ctx.save_for_backward(grad)
+        return part.sum() / s.numel()
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None
+
+
+def kd_mse(student, teacher):
+    return _MSE.apply(student, teacher)
+
+
+class _BCEDice(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, bw, dw, smooth):
+        C = require()
+        x = logits.contiguous().float()
+        t = target.contiguous().float().view_as(x)
+        n = x.shape[0]
+        hw = x.numel() // n
+        part = torch.empty(n, C.bce_dice_splits(hw), 4, dtype=torch.float32, device=x.device)
+        C.bce_dice_stats(x, t, part)
+        sums = part.sum(1)                                    # [N, 4]: BCE, p*t, p, t
+        den = sums[:, 2] + sums[:, 3] + smooth
+        num = 2 * sums[:, 1] + smooth
+        loss = bw * sums[:, 0].sum() / x.numel() + dw * (1 - (num / den).mean())
+        ctx.save_for_backward(x, t, torch.stack([den, num], 1).contiguous())
+        ctx.bw, ctx.dw = bw, dw
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        x, t, coef = ctx.saved_tensors
+        grad = torch.empty_like(x)
+        C.bce_dice_grad(x, t, coef, g.detach().float().reshape(1).contiguous(), grad, ctx.bw, ctx.dw)
+        return grad, None, None, None, None
+
+
+def bce_dice(logits, target, bce_weight=1.0, dice_weight=1.0, smooth=1.0):
+    return _BCEDice.apply(logits, target, float(bce_weight), float(dice_weight), float(smooth))

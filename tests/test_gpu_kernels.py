@@ -263,6 +263,30 @@ def test_ohem_and_kd(gpu):
     assert _rel(s.grad, sr.grad) < 1e-4
 
 
+def test_kd_mse_and_bce_dice(gpu):
+    from medical_segmentation_pytorch_amd.ops.losses import bce_dice, kd_mse
+    torch.manual_seed(9)
+    s = torch.randn(2, 3, 8, 8, device=gpu, requires_grad=True)
+    t = torch.randn(2, 3, 8, 8, device=gpu)
+    sr = s.detach().clone().requires_grad_(True)
+    a, b = kd_mse(s, t), F.mse_loss(sr, t)
+    assert abs(a.item() - b.item()) < 1e-5
+    (3 * a).backward(); (3 * b).backward()
+    assert _rel(s.grad, sr.grad) < 1e-5
+    # binary head: fused kernels vs the plain-torch BceDiceLoss formula (upstream grad != 1)
+    x = torch.randn(3, 1, 20, 24, device=gpu, requires_grad=True)
+    y = (torch.rand(3, 20, 24, device=gpu) > 0.6).float()
+    xr = x.detach().clone().requires_grad_(True)
+    got = bce_dice(x, y.unsqueeze(1), 1.0, 1.0, 1.0)
+    p = torch.sigmoid(xr)
+    inter = (p * y.unsqueeze(1)).flatten(1).sum(1)
+    den = p.flatten(1).sum(1) + y.flatten(1).sum(1)
+    ref = F.binary_cross_entropy_with_logits(xr, y.unsqueeze(1)) + 1 - ((2 * inter + 1) / (den + 1)).mean()
+    assert abs(got.item() - ref.item()) < 1e-5
+    (0.5 * got).backward(); (0.5 * ref).backward()
+    assert _rel(x.grad, xr.grad) < 1e-4
+
+
 def test_optim_and_ema(gpu):
     from medical_segmentation_pytorch_amd import _C
     torch.manual_seed(8)
