@@ -1115,7 +1115,12 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
     // Blocks split the tiles and add their dW slab with fp32 atomics (into nrep replicas): atomic bytes
     // = nsplit * rows * KT * 4, so one 8-wave block per CU that software-pipelines its ~8 tiles beats
     // more, shorter-lived blocks.
-    long nsplit = kDwSplitTarget / ((long)gy * gz);
+    static long split_target = -1;   // blocks in the grid; env MSP_DW_SPLIT overrides (tuning)
+    if (split_target < 0) {
+      const char* e = getenv("MSP_DW_SPLIT");
+      split_target = (e != nullptr && atol(e) > 0) ? atol(e) : kDwSplitTarget;
+    }
+    long nsplit = split_target / ((long)gy * gz);
     if (nsplit < 1) nsplit = 1;
     if (nsplit > ntiles) nsplit = ntiles;
     const size_t lds = wgrad_halo_lds(tl);

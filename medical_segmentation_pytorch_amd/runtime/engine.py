@@ -104,12 +104,20 @@ class GradBucketer:
     """DDP-equivalent gradient averaging over RCCL: buckets are contiguous slices of the grad arena
     in REVERSE parameter order (backward produces the last layers first); a bucket is all-reduced
     as soon as all of its parameters reported ready (SUM; the 1/world factor is folded into the
-    optimizer's grad scale)."""
+    optimizer's grad scale).
 
-    def __init__(self, arena: Arena, group=None, bucket_cap_mb=64.0, first_bucket_mb=4.0):
+    ``compress='bf16'`` (config ``grad_compress``; torch DDP's ``bf16_compress_hook``): a ready bucket
+    is rounded into a persistent bf16 shadow of the arena, all-reduced at half the xGMI bytes, and
+    widened back into the fp32 arena in :meth:`finish`."""
+
+    def __init__(self, arena: Arena, group=None, bucket_cap_mb=64.0, first_bucket_mb=4.0, compress=None):
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group)
+        if compress not in (None, 'bf16'):
+            raise ValueError(f'grad_compress must be None or "bf16", got {compress!r}')
+        self.shadow = torch.empty(arena.numel, dtype=torch.bfloat16, device=arena.grad.device) \
+            if compress == 'bf16' else None
         idx = list(range(len(arena.params)))[::-1]
         buckets, cur, cur_bytes, cap = [], [], 0, first_bucket_mb * 2 ** 20
         for i in idx:
@@ -149,14 +157,21 @@ class GradBucketer:
     def _launch(self, b):
         lo, hi, _ = self.buckets[b]
         self.launched[b] = True
-        self.works.append(dist.all_reduce(self.arena.grad[lo:hi], group=self.group, async_op=True))
+        buf = self.arena.grad[lo:hi]
+        if self.shadow is not None:
+            buf = self.shadow[lo:hi]
+            buf.copy_(self.arena.grad[lo:hi])
+        self.works.append((b, dist.all_reduce(buf, group=self.group, async_op=True)))
 
     def finish(self):
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for w in self.works:
+        for b, w in self.works:
             w.wait()
+            if self.shadow is not None:
+                lo, hi, _ = self.buckets[b]
+                self.arena.grad[lo:hi].copy_(self.shadow[lo:hi])
         self.reset()
 
 

@@ -99,7 +99,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
         bucketer = None
         if group is not None and dist.get_world_size(group) > 1 and arena is not None:
             from ..runtime.engine import GradBucketer
-            bucketer = GradBucketer(arena, group, config.bucket_cap_mb)
+            bucketer = GradBucketer(arena, group, config.bucket_cap_mb,
+                                    compress=getattr(config, 'grad_compress', None))
             optimizer.attach_bucketer(bucketer)
         from ..runtime.engine import stat_group
         return FusedModel(model, group=stat_group(group) if config.synBN else None,
@@ -114,6 +115,9 @@ def parallel_model(config, model, rank, device, optimizer=None):
                         bucket_cap_mb=config.bucket_cap_mb, process_group=pg)
         else:
             model = DDP(model, process_group=pg)
+        if getattr(config, 'grad_compress', None) == 'bf16':
+            from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+            model.register_comm_hook(pg, default_hooks.bf16_compress_hook)
     elif device.type == 'cuda' and torch.cuda.device_count() > 1:
         model = nn.DataParallel(model)
         model.to(device)

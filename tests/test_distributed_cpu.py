@@ -23,13 +23,13 @@ def _init(rank, world, port):
     dist.init_process_group('gloo', rank=rank, world_size=world)
 
 
-def _bucketer_worker(rank, world, port, q):
+def _bucketer_worker(rank, world, port, q, compress=None):
     _init(rank, world, port)
     from medical_segmentation_pytorch_amd.runtime.engine import Arena, GradBucketer
     torch.manual_seed(0)
     model = nn.Sequential(nn.Linear(300, 200), nn.ReLU(), nn.Linear(200, 100), nn.Linear(100, 7))
     arena = Arena(model, torch.device('cpu'))
-    b = GradBucketer(arena, None, bucket_cap_mb=0.1, first_bucket_mb=0.05)
+    b = GradBucketer(arena, None, bucket_cap_mb=0.1, first_bucket_mb=0.05, compress=compress)
     for i, p in enumerate(arena.params):
         p.grad.fill_(float(rank + 1) * (i + 1))
     # report readiness in backward order, as the fused ops do
@@ -41,11 +41,13 @@ def _bucketer_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_grad_bucketer_allreduce():
+@pytest.mark.parametrize('compress', [None, 'bf16'])
+def test_grad_bucketer_allreduce(compress):
+    """Bucketed all-reduce (SUM) of the grad arena; values 1*(i+1) + 2*(i+1) are exact in bf16 too."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    mp.spawn(_bucketer_worker, args=(2, port, q), nprocs=2, join=True)
+    mp.spawn(_bucketer_worker, args=(2, port, q, compress), nprocs=2, join=True)
     res = [q.get() for _ in range(2)]
     assert all(ok for _, ok, _ in res) and all(nb > 1 for _, _, nb in res)
 
