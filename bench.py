@@ -8,6 +8,11 @@ bucketed all-reduce + SyncBN), optimizer step (Adam, MyConfig default), OneCycle
 EMA update.  W untimed warmup steps, then K steps bracketed by barrier + synchronize; the MAX
 elapsed over ranks is reported.  Data: synthetic 352x352 polyp images/masks, random-init weights.
 
+Per-GPU micro-batch defaults to 128 images (the north star sizes micro-batches to fill the 288 GB of
+HBM3E; 128 x 352^2 DUCKNet-17 needs ~103 GiB): at the reference's 16 the step is dominated by ~2.7k
+fixed-cost launches and, under DDP, 584 SyncBN exchanges.  ``--batch 16`` reproduces MyConfig's
+per-process batch (measured 265 img/s vs 376 img/s at 128 on one MI355X, ``profiles/r01_fused_v8_*``).
+
 ``--impl fused`` (default) runs the MI355X-native engine (HIP kernels + hipGraph); ``--impl eager``
 runs the same step with stock PyTorch-ROCm (MIOpen convs, torch DDP/SyncBN) = the in-house
 "reference speed" of BASELINE.md.
@@ -30,7 +35,8 @@ def parse_args(argv=None):
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--batch', type=int, default=16, help='per-GPU micro-batch (images)')
+    p.add_argument('--batch', type=int, default=128,
+                   help='per-GPU micro-batch (images); 128 x 352^2 uses ~103 GiB of the 288 GiB HBM3E')
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
     p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
