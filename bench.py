@@ -40,11 +40,24 @@ def parse_args(argv=None):
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
     p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
-    p.add_argument('--model', choices=['ducknet', 'unet'], default='ducknet')
+    p.add_argument('--model', default='ducknet',
+                   help="ducknet | unet | smp-<resnet encoder> (e.g. smp-resnet101, BASELINE config #3)")
+    p.add_argument('--teacher', default=None,
+                   help='KD teacher (e.g. smp-resnet101; BASELINE config #4 = --base-channel 34 --teacher smp-resnet101)')
     p.add_argument('--graph-ddp', action='store_true', help='also capture the multi-GPU step in a hipGraph')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
     return p.parse_args(argv)
+
+
+def model_label(args):
+    if args.model == 'ducknet':
+        name = f'DUCKNet-{args.base_channel}'
+    elif args.model == 'unet':
+        name = f'UNet-{args.base_channel}'
+    else:
+        name = f'smp-Unet({args.model[4:]})'
+    return name + (f' + KD teacher {args.teacher}' if args.teacher else '')
 
 
 def main(argv=None):
@@ -68,10 +81,15 @@ def main(argv=None):
     step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
                             base_channel=args.base_channel, device=device,
                             channels_last=args.channels_last, use_graph=use_graph,
-                            distributed=world > 1)
+                            distributed=world > 1, model_name=args.model, teacher_name=args.teacher)
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
         step()
+        if rank == 0:   # progress on stderr (first eager steps can spend minutes in MIOpen's kernel search)
+            torch.cuda.synchronize()
+            print(f'[bench] warmup {i + 1}/{args.warmup} done at {time.perf_counter() - t_w:.1f}s', file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -101,12 +119,14 @@ def main(argv=None):
         pass
     if rank == 0:
         print(json.dumps({
-            'metric': 'images/sec (whole node) + val Dice, DUCKNet-17 352x352 at 1/2/4/8 MI355X',
+            'metric': ('images/sec (whole node) + val Dice, DUCKNet-17 352x352 at 1/2/4/8 MI355X'
+                       if args.model == 'ducknet' and args.base_channel == 17 and not args.teacher
+                       else f'images/sec (whole node), {model_label(args)} {args.size}x{args.size}'),
             'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': (value / baseline) if baseline else None,
             'dtype': 'bf16', 'data': 'synthetic 352x352 polyp images/masks, random-init weights',
-            'config': {'model': f'DUCKNet-{args.base_channel}', 'global_batch': global_batch,
+            'config': {'model': model_label(args), 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
                        'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph,

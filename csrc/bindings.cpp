@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "launchers.h"
@@ -271,6 +272,103 @@ void add_n_t(std::vector<at::Tensor> inputs, const at::Tensor& out) {
   add_n(ptrs.data(), (int)ptrs.size(), bf(out), out.numel(), cur_stream());
 }
 
+inline uint8_t* u8(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kByte, "idx must be a contiguous uint8 GPU tensor");
+  return t.data_ptr<uint8_t>();
+}
+
+void maxpool_fwd_t(const at::Tensor& x, const at::Tensor& y, const at::Tensor& idx, int64_t k, int64_t s, int64_t p) {
+  CHECK_BF16(x); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3) && x.size(3) % 8 == 0);
+  TORCH_CHECK(idx.numel() == y.numel() && k >= 1 && k * k <= 255 && s >= 1 && 2 * p <= k);
+  TORCH_CHECK(y.size(1) == (x.size(1) + 2 * p - k) / s + 1 && y.size(2) == (x.size(2) + 2 * p - k) / s + 1, "maxpool out shape");
+  maxpool_fwd(bf(x), bf(y), u8(idx), x.size(0), x.size(1), x.size(2), y.size(1), y.size(2), x.size(3), k, s, p, cur_stream());
+}
+
+void maxpool_bwd_t(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& dx, int64_t k, int64_t s, int64_t p) {
+  CHECK_BF16(dy); CHECK_BF16(dx);
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && dy.size(3) == dx.size(3) && idx.numel() == dy.numel());
+  TORCH_CHECK(dy.size(1) == (dx.size(1) + 2 * p - k) / s + 1 && dy.size(2) == (dx.size(2) + 2 * p - k) / s + 1, "maxpool shape");
+  maxpool_bwd(bf(dy), u8(idx), bf(dx), dx.size(0), dx.size(1), dx.size(2), dy.size(1), dy.size(2), dx.size(3), k, s, p,
+              cur_stream());
+}
+
+void up2_cat_t(const at::Tensor& low, const c10::optional<at::Tensor>& skip, const at::Tensor& out, int64_t Cl,
+               int64_t Cs) {
+  CHECK_BF16(low); CHECK_BF16(out);
+  const int64_t N = low.size(0), h = low.size(1), w = low.size(2), Cpl = low.size(3), Cpo = out.size(3);
+  TORCH_CHECK(out.size(0) == N && out.size(1) == 2 * h && out.size(2) == 2 * w && Cpo % 8 == 0 && Cpl % 8 == 0);
+  TORCH_CHECK(Cl <= Cpl && Cl + Cs <= Cpo, "channel ranges");
+  const uint16_t* sp = nullptr;
+  int64_t Cps = 8;
+  if (Cs > 0) {
+    TORCH_CHECK(skip.has_value() && skip->defined(), "skip required when Cs > 0");
+    CHECK_BF16(*skip);
+    TORCH_CHECK(skip->size(0) == N && skip->size(1) == 2 * h && skip->size(2) == 2 * w && skip->size(3) >= Cs);
+    Cps = skip->size(3);
+    sp = bf(*skip);
+  }
+  up2_cat(bf(low), sp, bf(out), N, h, w, Cl, Cpl, Cs, Cps, Cpo, cur_stream());
+}
+
+void up2_cat_bwd_t(const at::Tensor& g, const at::Tensor& dlow, const c10::optional<at::Tensor>& dskip, int64_t Cl,
+                   int64_t Cs) {
+  CHECK_BF16(g); CHECK_BF16(dlow);
+  const int64_t N = dlow.size(0), h = dlow.size(1), w = dlow.size(2), Cpl = dlow.size(3), Cpo = g.size(3);
+  TORCH_CHECK(g.size(0) == N && g.size(1) == 2 * h && g.size(2) == 2 * w && Cl <= Cpl && Cl + Cs <= Cpo);
+  uint16_t* dp = nullptr;
+  int64_t Cps = 8;
+  if (Cs > 0) {
+    TORCH_CHECK(dskip.has_value() && dskip->defined());
+    CHECK_BF16(*dskip);
+    TORCH_CHECK(dskip->size(0) == N && dskip->size(1) == 2 * h && dskip->size(2) == 2 * w && dskip->size(3) >= Cs);
+    Cps = dskip->size(3);
+    dp = bf(*dskip);
+  }
+  up2_cat_bwd(bf(g), bf(dlow), dp, N, h, w, Cl, Cpl, Cs, Cps, Cpo, cur_stream());
+}
+
+void add_act_t(const at::Tensor& a, const at::Tensor& b, const at::Tensor& z, bool relu) {
+  CHECK_BF16(a); CHECK_BF16(b); CHECK_BF16(z);
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() == z.numel() && a.numel() % 8 == 0);
+  add_act(bf(a), bf(b), bf(z), a.numel(), relu ? 1 : 0, cur_stream());
+}
+
+void relu_bwd_t(const at::Tensor& dz, const at::Tensor& z, const at::Tensor& g) {
+  CHECK_BF16(dz); CHECK_BF16(z); CHECK_BF16(g);
+  TORCH_CHECK(dz.numel() == z.numel() && z.numel() == g.numel() && z.numel() % 8 == 0);
+  relu_bwd(bf(dz), bf(z), bf(g), z.numel(), cur_stream());
+}
+
+// ---- GPU augmentation (augment.hip)
+void aug_batch_t(const at::Tensor& images, const at::Tensor& masks, const at::Tensor& meta, const at::Tensor& ip,
+                 const at::Tensor& fp, const at::Tensor& work, const at::Tensor& mean, const at::Tensor& out,
+                 const at::Tensor& mask_out, std::vector<int64_t> stages, std::vector<int64_t> contrast_stages,
+                 std::vector<double> norm_mean, std::vector<double> norm_std) {
+  TORCH_CHECK(images.is_cuda() && images.scalar_type() == at::kByte && images.is_contiguous());
+  TORCH_CHECK(masks.is_cuda() && masks.scalar_type() == at::kByte && masks.is_contiguous());
+  CHECK_I64(meta); CHECK_I64(mask_out); CHECK_F32(fp); CHECK_F32(work); CHECK_F32(mean); CHECK_F32(out);
+  TORCH_CHECK(ip.is_cuda() && ip.scalar_type() == at::kInt && ip.is_contiguous());
+  TORCH_CHECK(out.dim() == 4 && out.size(1) == 3, "out must be [B, 3, H, W]");
+  const int B = out.size(0), H = out.size(2), W = out.size(3);
+  TORCH_CHECK(ip.numel() == (int64_t)B * kAugIParams && fp.numel() == (int64_t)B * 4 && mean.numel() >= B);
+  TORCH_CHECK(work.numel() == (int64_t)B * H * W * 3 && mask_out.numel() == (int64_t)B * H * W);
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == 4 && norm_mean.size() == 3 && norm_std.size() == 3);
+  auto s = cur_stream();
+  aug_geometry(images.data_ptr<uint8_t>(), masks.data_ptr<uint8_t>(), meta.data_ptr<int64_t>(), ip.data_ptr<int>(),
+               f32(work), mask_out.data_ptr<int64_t>(), B, H, W, s);
+  for (size_t k = 0; k < stages.size(); ++k) {
+    const int st = (int)stages[k];
+    TORCH_CHECK(st >= 0 && st < 4);
+    if (std::find(contrast_stages.begin(), contrast_stages.end(), stages[k]) != contrast_stages.end())
+      aug_gray_mean(f32(work), f32(mean), B, H * W, s);
+    aug_color(f32(work), ip.data_ptr<int>(), f32(fp), f32(mean), B, H * W, st, s);
+  }
+  const float m3[3] = {(float)norm_mean[0], (float)norm_mean[1], (float)norm_mean[2]};
+  const float s3[3] = {(float)norm_std[0], (float)norm_std[1], (float)norm_std[2]};
+  aug_finalize(f32(work), ip.data_ptr<int>(), f32(out), B, H * W, m3, s3, s);
+}
+
 void scale_f32_t(const at::Tensor& x, const c10::optional<at::Tensor>& scalar, double mult) {
   CHECK_F32(x);
   scale_f32(f32(x), f32_opt(scalar), (float)mult, x.numel(), cur_stream());
@@ -398,6 +496,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool2_sum", &pool2_sum_t);
   m.def("add_n", &add_n_t);
   m.def("scale_f32", &scale_f32_t);
+  m.def("aug_batch", &aug_batch_t);
+  m.def("aug_iparams", []() { return kAugIParams; });
+  m.def("maxpool_fwd", &maxpool_fwd_t);
+  m.def("maxpool_bwd", &maxpool_bwd_t);
+  m.def("up2_cat", &up2_cat_t);
+  m.def("up2_cat_bwd", &up2_cat_bwd_t);
+  m.def("add_act", &add_act_t);
+  m.def("relu_bwd", &relu_bwd_t);
   m.def("ce_blocks", &ce_blocks_t);
   m.def("ce_fwd_bwd", &ce_fwd_bwd_t);
   m.def("kd_kl_fwd_bwd", &kd_kl_fwd_bwd_t);

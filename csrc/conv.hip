@@ -919,7 +919,7 @@ static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
 static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   if (trans || g.stride != 1 || g.OH != g.IH || g.OW != g.IW) return false;
   const int rows = g.Go * g.Cgo;
-  if (rows > kHaloMaxRows || g.T > kMaxTaps) return false;
+  if (rows > kHaloMaxRows || g.T > 16) return false;
   const int Cip = g.Gi * g.Cgi;
   if (Cip % 8 != 0 || g.Cgi % 8 != 0) return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;

@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-constexpr int kMaxTaps = 16;
+constexpr int kMaxTaps = 49;   // up to 7x7 (ResNet stem)
 
 // Convolution geometry shared by the forward / data-gradient / weight-gradient kernels.
 // Inputs and outputs may be split into up to 8 channel GROUPS, each its own NHWC tensor with the
@@ -97,6 +97,28 @@ void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, in
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s);
 void add_n(const uint16_t* const* inputs, int k, uint16_t* out, long n_elem, hipStream_t s);
 void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s);
+
+// pool.hip  (NHWC bf16; idx = one byte per element = winning tap r*k+c)
+void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int IH, int IW, int OH, int OW, int Cp, int k,
+                 int s, int p, hipStream_t st);
+void maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int IH, int IW, int OH, int OW, int Cp,
+                 int k, int s, int p, hipStream_t st);
+void up2_cat(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cl, int Cpl, int Cs,
+             int Cps, int Cpo, hipStream_t st);
+void up2_cat_bwd(const uint16_t* g, uint16_t* dlow, uint16_t* dskip, int N, int h, int w, int Cl, int Cpl, int Cs,
+                 int Cps, int Cpo, hipStream_t st);
+void add_act(const uint16_t* a, const uint16_t* b, uint16_t* z, long n_elem, int relu, hipStream_t st);
+void relu_bwd(const uint16_t* dz, const uint16_t* z, uint16_t* g, long n_elem, hipStream_t st);
+
+// augment.hip  (HBM-resident uint8 dataset; see augment.hip for the per-sample parameter layout)
+constexpr int kAugIParams = 14;
+void aug_geometry(const uint8_t* images, const uint8_t* masks, const int64_t* meta, const int* ip, float* work,
+                  int64_t* mask_out, int B, int CH, int CW, hipStream_t s);
+void aug_gray_mean(const float* work, float* mean, int B, int HW, hipStream_t s);
+void aug_color(float* work, const int* ip, const float* fp, const float* mean, int B, int HW, int stage,
+               hipStream_t s);
+void aug_finalize(const float* work, const int* ip, float* out, int B, int HW, const float* mean3, const float* std3,
+                  hipStream_t s);
 
 // loss.hip  (logits NCHW fp32 [N, C, HW]; targets int64 [N, HW])
 long ce_blocks(long P);

@@ -114,6 +114,7 @@ def get_parser():
     _flag(p, 'synthetic_num', type=int, nargs=3)
     _flag(p, 'synthetic_size', type=int)
     _flag(p, 'graph_ddp', action='store_true')
+    _flag(p, 'gpu_augment', action='store_false')
     _flag(p, 'graph_warmup', type=int)
     _flag(p, 'log_interval', type=int)
     _flag(p, 'no_progress_bar', action='store_true')

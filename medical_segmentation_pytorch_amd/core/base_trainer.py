@@ -62,7 +62,7 @@ class BaseTrainer:
         else:
             self.writer = get_writer(config, self.main_rank)
             self.loss_fn = get_loss_fn(config, self.device)
-            self.train_loader = get_loader(config, self.local_rank, 'train')
+            self.train_loader = get_loader(config, self.local_rank, 'train', device=self.device)
             self.val_loader = get_loader(config, self.local_rank, 'val')
             if config.use_test_set:
                 self.test_loader = get_loader(config, self.local_rank, 'test')

@@ -90,6 +90,12 @@ class SegTrainer(BaseTrainer):
             self.colormap = torch.tensor(get_colormap(config)).to(self.device)
         else:
             self.teacher_model = get_teacher_model(config, self.device)
+            if self.teacher_model is not None and self.fused:
+                from ..runtime.fused_model import supports
+                if supports(self.teacher_model):   # KD teacher fwd on the HIP kernels (eval-mode BN)
+                    for p in self.teacher_model.parameters():
+                        p.requires_grad_(False)
+                    self.teacher_model = FusedModel(self.teacher_model).eval()
             self.metrics = [get_seg_metrics(config, m).to(self.device) for m in config.metrics]
         self.graph_step = None
         self._ema_exec = (None, None)

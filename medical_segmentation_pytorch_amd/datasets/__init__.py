@@ -41,7 +41,17 @@ def get_dataset(config, mode):
     raise NotImplementedError('Unsupported dataset!')
 
 
-def get_loader(config, rank, mode, pin_memory=True, drop_last=True):
+def _device_loader_ok(config, mode, dataset, device):
+    if mode != 'train' or not getattr(config, 'gpu_augment', False) or device is None or device.type != 'cuda':
+        return False
+    from ..ops import _ext
+    from ..utils.transforms import SegAugment
+    return _ext.available() and isinstance(getattr(dataset, 'transform', None), SegAugment)
+
+
+def get_loader(config, rank, mode, pin_memory=True, drop_last=True, device=None):
+    """Host ``DataLoader`` (reference semantics), or -- train split on a GPU with ``gpu_augment`` --
+    the HBM-resident :class:`DeviceAugLoader` (same sampler order, same augmentation draws)."""
     dataset = get_dataset(config, mode)
     if mode == 'train':
         config.train_num = int(len(dataset) // config.train_bs * config.train_bs)
@@ -53,6 +63,18 @@ def get_loader(config, rank, mode, pin_memory=True, drop_last=True):
     bs = config.train_bs if mode == 'train' else config.val_bs
     workers = config.num_workers
     common = dict(num_workers=workers, worker_init_fn=seed_worker, persistent_workers=workers > 0)
+    if _device_loader_ok(config, mode, dataset, device):
+        from .device_loader import DeviceAugLoader
+        sampler = None
+        grank = 0
+        if config.DDP:
+            from torch.utils.data.distributed import DistributedSampler
+            from ..utils.parallel import group_rank
+            grank = group_rank(config) if dist.is_initialized() else max(rank, 0)
+            sampler = DistributedSampler(dataset, num_replicas=config.gpu_num, rank=grank, shuffle=True,
+                                         seed=config.random_seed)
+        return DeviceAugLoader(dataset, bs, device, sampler=sampler, shuffle=True, drop_last=drop_last,
+                               seed=config.random_seed + grank, binary_float=config.num_class == 1)
     if config.DDP:
         from torch.utils.data.distributed import DistributedSampler
         from ..utils.parallel import group_rank

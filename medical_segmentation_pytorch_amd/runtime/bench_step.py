@@ -40,14 +40,15 @@ class _OneCycle:
 
 
 def build_eager_step(batch, size, base_channel, device, channels_last=False, distributed=False,
-                     lr=1e-3, total_steps=100000):
-    from ..models.ducknet import DuckNet
+                     lr=1e-3, total_steps=100000, model_name='ducknet', teacher_name=None, kd_temperature=4.0):
+    from .trainer_engine import make_model
     torch.manual_seed(1)
-    model = DuckNet(num_class=2, n_channel=3, base_channel=base_channel).to(device)
+    model = make_model(model_name, base_channel).to(device)
     fmt = torch.channels_last if channels_last else torch.contiguous_format
     model = model.to(memory_format=fmt)
-    ema = DuckNet(num_class=2, n_channel=3, base_channel=base_channel).to(device).eval()
+    ema = make_model(model_name, base_channel).to(device).eval()
     ema.load_state_dict(model.state_dict())
+    teacher = make_model(teacher_name).to(device).to(memory_format=fmt).eval() if teacher_name else None
     if distributed:
         model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
         model = nn.parallel.DistributedDataParallel(model, device_ids=[device.index],
@@ -64,6 +65,12 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
         with torch.autocast('cuda', dtype=torch.bfloat16):
             preds = model(images)
             loss = loss_fn(preds, masks)
+            if teacher is not None:   # reference core/seg_trainer.py:69-79 + core/loss.py:42-49
+                with torch.no_grad():
+                    t_out = teacher(images)
+                T = kd_temperature
+                loss = loss + nn.functional.kl_div(nn.functional.log_softmax(preds.float() / T, 1),
+                                                   nn.functional.softmax(t_out.float() / T, 1)) * T * T
         loss.backward()
         opt.step()
         sched.step()
@@ -77,9 +84,11 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
 
 
 def build_bench_step(impl, batch, size, base_channel, device, channels_last=False,
-                     use_graph=True, distributed=False):
+                     use_graph=True, distributed=False, model_name='ducknet', teacher_name=None):
     if impl == 'eager':
-        return build_eager_step(batch, size, base_channel, device, channels_last, distributed)
+        return build_eager_step(batch, size, base_channel, device, channels_last, distributed,
+                                model_name=model_name, teacher_name=teacher_name)
     from .trainer_engine import build_fused_step
     return build_fused_step(batch=batch, size=size, base_channel=base_channel, device=device,
-                            use_graph=use_graph, distributed=distributed)
+                            use_graph=use_graph, distributed=distributed, model_name=model_name,
+                            teacher_name=teacher_name)

@@ -22,6 +22,7 @@ import torch.nn as nn
 from ..ops.bn import BNState, bn_act
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
+from ..ops.pool import add_act, maxpool, up2_cat
 
 
 def _is_relu(act_mod):
@@ -199,7 +200,6 @@ class FusedExecutor:
         return self.head(model.seg_head, x, model.num_class)
 
     def unet(self, model, images, training):
-        import torch.nn.functional as F
         x = to_fm(images)
         skips = []
         for i in range(1, 5):
@@ -208,8 +208,7 @@ class FusedExecutor:
             f = self.cba(st.conv[1], f, training)
             skips.append(f)
             p = st.pool
-            x = F.max_pool2d(f.permute(0, 3, 1, 2), p.kernel_size, p.stride, p.padding).permute(0, 2, 3, 1)
-            x = x.contiguous()
+            x = maxpool(f, p.kernel_size, p.stride, p.padding)
         x = self.cba(model.mid_stage[0], x, training)
         x = self.cba(model.mid_stage[1], x, training)
         for i in range(4, 0, -1):
@@ -222,6 +221,49 @@ class FusedExecutor:
             x = self.cba(st.conv[1], x, training)
         return self.head(model.seg_head, x, model.num_class)
 
+    # -- smp Unet with a ResNet encoder (reference models/__init__.py:23-25; KD teacher :42-62) ---------
+    def conv_bn(self, conv_mod, bn_mod, x, training, relu):
+        plan = self.plan_conv(conv_mod)
+        (y,), part = conv(plan, [x], want_stats=training)
+        return bn_act([y], self.bn(bn_mod), relu, training, (part, plan.rows, 0) if training else None)
+
+    def resnet_block(self, blk, x, training):
+        """torchvision BasicBlock / Bottleneck: ``relu(bn_last(conv_last(...)) + identity)``."""
+        if blk.downsample is not None:
+            idt = self.conv_bn(blk.downsample[0], blk.downsample[1], x, training, relu=False)
+        else:
+            idt = x
+        o = self.conv_bn(blk.conv1, blk.bn1, x, training, relu=True)
+        if hasattr(blk, 'conv3'):
+            o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=True)
+            o = self.conv_bn(blk.conv3, blk.bn3, o, training, relu=False)
+        else:
+            o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=False)
+        return add_act(o, idt, relu=True)
+
+    def resnet_unet(self, model, images, training):
+        enc, dec = model.encoder, model.decoder
+        x = to_fm(images)
+        f1 = self.conv_bn(enc.conv1, enc.bn1, x, training, relu=True)
+        mp = enc.maxpool
+        x = maxpool(f1, _pair(mp.kernel_size)[0], _pair(mp.stride)[0], _pair(mp.padding)[0])
+        feats = [f1]
+        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+            for blk in layer:
+                x = self.resnet_block(blk, x, training)
+            feats.append(x)
+        chans = list(enc.out_channels[1:])
+        skips, skip_ch = feats[:-1][::-1], chans[:-1][::-1]
+        cx = chans[-1]
+        for i, blk in enumerate(dec.blocks):
+            skip = skips[i] if i < len(skips) else None
+            cs = skip_ch[i] if skip is not None else 0
+            x = up2_cat(x, skip, cx, cs)
+            x = self.cba(blk.conv1, x, training)
+            x = self.cba(blk.conv2, x, training)
+            cx = blk.conv2[0].out_channels
+        return self.head(model.segmentation_head[0], x, model.segmentation_head[0].out_channels)
+
     def forward(self, images, training=None):
         model = self.model
         training = model.training if training is None else training
@@ -230,10 +272,30 @@ class FusedExecutor:
             return self.ducknet(model, images, training)
         if name == 'UNet':
             return self.unet(model, images, training)
+        if _is_resnet_unet(model):
+            return self.resnet_unet(model, images, training)
         raise NotImplementedError(f'no fused executor for {name}')
 
     __call__ = forward
 
 
+def _is_resnet_unet(model) -> bool:
+    """smp ``Unet`` over a (non-grouped, stride-32) ResNet encoder with BatchNorm decoder blocks."""
+    from ..models.smp import ResNetEncoder, SegmentationModel, UnetDecoder
+    if not isinstance(model, SegmentationModel):
+        return False
+    enc, dec = getattr(model, 'encoder', None), getattr(model, 'decoder', None)
+    if not isinstance(enc, ResNetEncoder) or not isinstance(dec, UnetDecoder) or enc._depth != 5:
+        return False
+    if any(isinstance(m, nn.Conv2d) and m.groups != 1 for m in enc.modules()):
+        return False
+    if any(_pair(m.dilation) != (1, 1) for m in enc.modules() if isinstance(m, nn.Conv2d)):
+        return False
+    head = model.segmentation_head
+    if not isinstance(head[1], nn.Identity):
+        return False
+    return all(isinstance(b.conv1[1], nn.BatchNorm2d) for b in dec.blocks)
+
+
 def supports(model) -> bool:
-    return type(model).__name__ in ('DuckNet', 'UNet')
+    return type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_unet(model)

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops._ext import require
-from ..ops.losses import cross_entropy
+from ..ops.losses import cross_entropy, kd_kl_div
 from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, stat_group
 from .fused_model import FusedExecutor
 
@@ -22,7 +22,8 @@ from .fused_model import FusedExecutor
 class FusedStep:
     def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
                  total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
-                 syncbn=True, bucket_cap_mb=64.0, ignore_index=255):
+                 syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
+                 kd_coef=1.0):
         require()
         dev = images.device
         self.model = model
@@ -50,6 +51,9 @@ class FusedStep:
         self.use_graph = use_graph
         self.graph = None
         self.loss = None
+        # KD (reference core/seg_trainer.py:69-79): frozen eval-mode teacher on the same fused kernels
+        self.teacher = FusedExecutor(teacher) if teacher is not None else None
+        self.kd_temperature, self.kd_coef = kd_temperature, kd_coef
 
     def _body(self):
         C = require()
@@ -57,6 +61,10 @@ class FusedStep:
         self.ex.repack()
         out = self.ex(self.images, training=True)
         loss = cross_entropy(out, self.masks, None, self.ignore_index)
+        if self.teacher is not None:
+            with torch.no_grad():
+                t_out = self.teacher(self.images, training=False)
+            loss = loss + self.kd_coef * kd_kl_div(out, t_out, self.kd_temperature)
         loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
@@ -104,20 +112,36 @@ class FusedStep:
         return self.loss
 
 
-def build_fused_step(batch, size, base_channel, device, use_graph=True, distributed=False, optimizer='adam',
-                     lr=1e-3, model_name='ducknet', syncbn=True):
+def make_model(model_name, base_channel=17, num_class=2):
+    """Bench/test model zoo: 'ducknet' (DUCKNet-<base_channel>), 'unet' (UNet-<base_channel>),
+    'smp-<encoder>' (smp Unet over a ResNet encoder, e.g. 'smp-resnet18', 'smp-resnet101')."""
     from ..models.ducknet import DuckNet
+    from ..models.smp import Unet
     from ..models.unet import UNet
+    if model_name == 'ducknet':
+        return DuckNet(num_class=num_class, n_channel=3, base_channel=base_channel)
+    if model_name == 'unet':
+        return UNet(num_class=num_class, n_channel=3, base_channel=base_channel)
+    if model_name.startswith('smp-'):
+        return Unet(encoder_name=model_name[4:], encoder_weights=None, in_channels=3, classes=num_class)
+    raise ValueError(f'unknown model {model_name!r}')
+
+
+def build_fused_step(batch, size, base_channel, device, use_graph=True, distributed=False, optimizer='adam',
+                     lr=1e-3, model_name='ducknet', syncbn=True, teacher_name=None):
     from .bench_step import synthetic_batch
     torch.manual_seed(1)
-    if model_name == 'ducknet':
-        model = DuckNet(num_class=2, n_channel=3, base_channel=base_channel)
-    else:
-        model = UNet(num_class=2, n_channel=3, base_channel=base_channel)
-    model = model.to(device).train()
+    model = make_model(model_name, base_channel).to(device).train()
+    teacher = make_model(teacher_name).to(device).eval() if teacher_name else None
     if distributed:   # identical initial weights on every rank (DDP broadcast semantics)
-        for t in list(model.parameters()) + list(model.buffers()):
-            dist.broadcast(t.data, 0)
+        for m in (model, teacher):
+            if m is None:
+                continue
+            for t in list(m.parameters()) + list(m.buffers()):
+                dist.broadcast(t.data, 0)
+    if teacher is not None:
+        for p in teacher.parameters():
+            p.requires_grad_(False)
     images, masks = synthetic_batch(batch, size, device, seed=dist.get_rank() if distributed else 0)
     return FusedStep(model, images, masks, optimizer=optimizer, lr=lr, use_graph=use_graph, distributed=distributed,
-                     syncbn=syncbn)
+                     syncbn=syncbn, teacher=teacher)

@@ -120,31 +120,26 @@ class SegAugment:
     def seed(self, s):
         self.rng.seed(s)
 
-    def __call__(self, image, mask):
+    def sample_params(self, h, w):
+        """Draw every random number of one sample (same calls, same order as the pixel pipeline), for
+        an ``h x w`` source.  The CPU pipeline (:meth:`__call__`) and the GPU one
+        (``datasets.device_loader``) both evaluate these records, so a seed gives the same batch."""
         rng = self.rng
-        img, msk = to_numpy(image), to_numpy(mask)
+        prm = {'nh': h, 'nw': w, 'scaled': False}
         if self.scale_range != (1.0, 1.0) and rng.random() < self.scale_p:
             f = rng.uniform(*self.scale_range)
-            h, w = img.shape[:2]
-            nh, nw = max(int(round(h * f)), 1), max(int(round(w * f)), 1)
-            img = resize(img, nh, nw, 'bilinear')
-            msk = resize(msk, nh, nw, 'nearest')
+            prm.update(nh=max(int(round(h * f)), 1), nw=max(int(round(w * f)), 1), scaled=True)
         ch, cw = self.crop
-        h, w = img.shape[:2]
-        if h < ch or w < cw:
-            ph, pw = max(ch - h, 0), max(cw - w, 0)
-            t, l = ph // 2, pw // 2
-            img = _reflect101_pad(img, t, ph - t, l, pw - l)
-            msk = _reflect101_pad(msk, t, ph - t, l, pw - l)
-            h, w = img.shape[:2]
-        y0 = rng.randint(0, h - ch)
-        x0 = rng.randint(0, w - cw)
-        img = img[y0:y0 + ch, x0:x0 + cw]
-        msk = msk[y0:y0 + ch, x0:x0 + cw]
-        img = img.astype(np.float32)
+        h2, w2 = prm['nh'], prm['nw']
+        ph, pw = max(ch - h2, 0), max(cw - w2, 0)
+        prm['pad'] = (ph // 2, ph - ph // 2, pw // 2, pw - pw // 2)
+        h2, w2 = h2 + ph, w2 + pw
+        prm['y0'] = rng.randint(0, h2 - ch)
+        prm['x0'] = rng.randint(0, w2 - cw)
+        ops = []
         b, c, s, hue = self.jitter
-        if (b or c or s or hue) and rng.random() < self.jitter_p:
-            ops = []
+        jittered = bool(b or c or s or hue) and rng.random() < self.jitter_p
+        if jittered:
             if b:
                 ops.append(('b', rng.uniform(max(0.0, 1 - b), 1 + b)))
             if c:
@@ -154,7 +149,28 @@ class SegAugment:
             if hue:
                 ops.append(('h', rng.uniform(-hue, hue)))
             rng.shuffle(ops)
-            for op, v in ops:
+        prm['jittered'], prm['ops'] = jittered, ops
+        prm['hflip'] = rng.random() < self.h_flip
+        prm['vflip'] = rng.random() < self.v_flip
+        return prm
+
+    def __call__(self, image, mask):
+        img, msk = to_numpy(image), to_numpy(mask)
+        prm = self.sample_params(*img.shape[:2])
+        if prm['scaled']:
+            img = resize(img, prm['nh'], prm['nw'], 'bilinear')
+            msk = resize(msk, prm['nh'], prm['nw'], 'nearest')
+        if any(prm['pad']):
+            t, bt, l, r = prm['pad']
+            img = _reflect101_pad(img, t, bt, l, r)
+            msk = _reflect101_pad(msk, t, bt, l, r)
+        ch, cw = self.crop
+        y0, x0 = prm['y0'], prm['x0']
+        img = img[y0:y0 + ch, x0:x0 + cw]
+        msk = msk[y0:y0 + ch, x0:x0 + cw]
+        img = img.astype(np.float32)
+        if prm['jittered']:
+            for op, v in prm['ops']:
                 if op == 'b':
                     img = np.clip(img * v, 0, 255)
                 elif op == 'c':
@@ -166,9 +182,9 @@ class SegAugment:
                 else:
                     img = np.clip(_adjust_hue(img, v), 0, 255)
             img = np.round(img)
-        if rng.random() < self.h_flip:
+        if prm['hflip']:
             img, msk = img[:, ::-1], msk[:, ::-1]
-        if rng.random() < self.v_flip:
+        if prm['vflip']:
             img, msk = img[::-1], msk[::-1]
         return normalize_to_tensor(img, self.mean, self.std), torch.from_numpy(np.ascontiguousarray(msk)).long()
 

@@ -36,6 +36,7 @@ CONV_CASES = [
     (3, 9, 7, 40, 72, (3, 3), 1, (1, 1), (1, 1)),
     (2, 17, 15, 17, 34, (3, 3), 2, (1, 1), (1, 1)),    # odd sizes: uneven output phases in the dgrad
     (2, 16, 16, 64, 128, (1, 1), 2, (0, 0), (1, 1)),   # ResNet downsample: 3 of 4 dgrad phases are empty
+    (2, 32, 32, 3, 64, (7, 7), 2, (3, 3), (1, 1)),     # ResNet stem: 49 taps
 ]
 
 
@@ -219,6 +220,47 @@ def test_elementwise(gpu):
     a, b, c = [to_fm_reference(torch.randn(2, 5, 4, 4, device=gpu)) for _ in range(3)]
     s = add_n(a, b, c)
     assert _rel(s.float(), a.float() + b.float() + c.float()) < 1e-2
+
+
+@pytest.mark.parametrize('k,s,p,hw', [(3, 2, 1, (16, 16)), (3, 2, 1, (17, 11)), (2, 2, 0, (8, 8))])
+def test_maxpool(gpu, k, s, p, hw):
+    from medical_segmentation_pytorch_amd.ops.pool import maxpool, maxpool_reference
+    torch.manual_seed(7)
+    x = to_fm_reference(torch.randn(2, 20, *hw, device=gpu)).requires_grad_(True)
+    y = maxpool(x, k, s, p)
+    assert torch.equal(y, maxpool_reference(x.detach(), k, s, p))    # max is exact in bf16
+    g = to_fm_reference(torch.randn(2, 20, y.shape[1], y.shape[2], device=gpu))
+    y.backward(g)
+    xr = x.detach().permute(0, 3, 1, 2).float().requires_grad_(True)
+    F.max_pool2d(xr, k, s, p).backward(g.permute(0, 3, 1, 2).float())
+    ref = xr.grad.permute(0, 2, 3, 1)
+    assert _rel(x.grad.float(), ref) < 1e-2
+    assert x.grad[..., 20:].abs().sum() == 0
+
+
+@pytest.mark.parametrize('cl,cs', [(64, 32), (20, 12), (16, 0)])
+def test_up2_cat_and_add_act(gpu, cl, cs):
+    from medical_segmentation_pytorch_amd.ops.pool import add_act, up2_cat, up2_cat_reference
+    torch.manual_seed(8)
+    low = to_fm_reference(torch.randn(2, cl, 5, 6, device=gpu)).requires_grad_(True)
+    skip = to_fm_reference(torch.randn(2, cs, 10, 12, device=gpu)).requires_grad_(True) if cs else None
+    out = up2_cat(low, skip, cl, cs)
+    assert torch.equal(out, up2_cat_reference(low.detach(), skip.detach() if cs else None, cl, cs))
+    g = to_fm_reference(torch.randn(2, cl + cs, 10, 12, device=gpu))
+    out.backward(g)
+    gl = F.avg_pool2d(from_fm_reference(g, cl + cs)[:, :cl], 2) * 4
+    assert _rel(from_fm_reference(low.grad, cl), gl) < 1e-2
+    if cs:
+        assert torch.equal(from_fm_reference(skip.grad, cs), from_fm_reference(g, cl + cs)[:, cl:])
+    a = to_fm_reference(torch.randn(2, 12, 4, 4, device=gpu)).requires_grad_(True)
+    b = to_fm_reference(torch.randn(2, 12, 4, 4, device=gpu)).requires_grad_(True)
+    z = add_act(a, b, relu=True)
+    zr = torch.relu(a.detach().float() + b.detach().float())
+    assert _rel(z.float(), zr) < 1e-2
+    dz = torch.randn_like(z)
+    z.backward(dz)
+    ref = dz.float() * (z.float() > 0)
+    assert _rel(a.grad.float(), ref) < 1e-2 and torch.equal(a.grad, b.grad)
 
 
 @pytest.mark.parametrize('weighted', [False, True])

@@ -21,7 +21,14 @@ def _eager_bf16(model, x):
         return model(x).float()
 
 
-@pytest.mark.parametrize('model_fn,size,batch', [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64, 2)])
+def _smp_unet(encoder):
+    from medical_segmentation_pytorch_amd.models.smp import Unet
+    return Unet(encoder_name=encoder, encoder_weights=None, in_channels=3, classes=2)
+
+
+@pytest.mark.parametrize('model_fn,size,batch', [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64, 2),
+                                                 (lambda: _smp_unet('resnet18'), 64, 4),
+                                                 (lambda: _smp_unet('resnet50'), 64, 2)])
 def test_fused_matches_eager(gpu, model_fn, size, batch):
     """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is."""
     torch.manual_seed(0)
