@@ -84,6 +84,14 @@ def main(argv=None):
                             distributed=world > 1, model_name=args.model, teacher_name=args.teacher)
 
     t_w = time.perf_counter()
+    if rank == 0:   # heartbeat: MIOpen's first-call kernel search (eager impl) can be silent for minutes
+        import threading
+
+        def _beat():
+            while True:
+                time.sleep(30)
+                print(f'[bench] alive {time.perf_counter() - t_w:.0f}s', file=sys.stderr, flush=True)
+        threading.Thread(target=_beat, daemon=True).start()
     for i in range(args.warmup):
         step()
         if rank == 0:   # progress on stderr (first eager steps can spend minutes in MIOpen's kernel search)

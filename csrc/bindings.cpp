@@ -340,6 +340,23 @@ void relu_bwd_t(const at::Tensor& dz, const at::Tensor& z, const at::Tensor& g) 
   relu_bwd(bf(dz), bf(z), bf(g), z.numel(), cur_stream());
 }
 
+// ---- inference glue (metrics.hip)
+void bilinear_resize_t(const at::Tensor& x, const at::Tensor& y, bool align_corners) {
+  CHECK_F32(x); CHECK_F32(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1));
+  bilinear_resize(f32(x), f32(y), x.size(0) * x.size(1), x.size(2), x.size(3), y.size(2), y.size(3),
+                  align_corners ? 1 : 0, cur_stream());
+}
+
+void colorize_t(const at::Tensor& logits, const at::Tensor& lut, const at::Tensor& rgb) {
+  CHECK_F32(logits);
+  TORCH_CHECK(lut.is_cuda() && lut.scalar_type() == at::kByte && lut.is_contiguous() && lut.size(1) == 3);
+  TORCH_CHECK(rgb.is_cuda() && rgb.scalar_type() == at::kByte && rgb.is_contiguous());
+  const int64_t N = logits.size(0), C = logits.size(1), HW = logits.size(2) * logits.size(3);
+  TORCH_CHECK(lut.size(0) >= (C == 1 ? 2 : C) && rgb.numel() == N * HW * 3);
+  colorize(f32(logits), lut.data_ptr<uint8_t>(), rgb.data_ptr<uint8_t>(), N, C, HW, cur_stream());
+}
+
 // ---- GPU augmentation (augment.hip)
 void aug_batch_t(const at::Tensor& images, const at::Tensor& masks, const at::Tensor& meta, const at::Tensor& ip,
                  const at::Tensor& fp, const at::Tensor& work, const at::Tensor& mean, const at::Tensor& out,
@@ -497,6 +514,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_n", &add_n_t);
   m.def("scale_f32", &scale_f32_t);
   m.def("aug_batch", &aug_batch_t);
+  m.def("bilinear_resize", &bilinear_resize_t);
+  m.def("colorize", &colorize_t);
   m.def("aug_iparams", []() { return kAugIParams; });
   m.def("maxpool_fwd", &maxpool_fwd_t);
   m.def("maxpool_bwd", &maxpool_bwd_t);

@@ -14,6 +14,7 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kPartUnroll = 4;   // pixels per trip of the backward partial-sum pass
 
 struct SumInputs { const uint16_t* p[kMaxSumInputs]; };
 
@@ -29,23 +30,40 @@ __global__ __launch_bounds__(kBlock) void sum_stats_kernel(SumInputs in, int k, 
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
   if (r < R) {
-    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
-      const long off = p * Cp + 8 * cg;
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(in.p[0] + off), v);
+    // two pixels per trip: every input's vectors for both are issued before the sums (2k loads in flight)
+    const long stride = (long)gridDim.x * R;
+    for (long p = (long)blockIdx.x * R + r; p < P; p += 2 * stride) {
+      const long p1 = p + stride;
+      const bool ok1 = p1 < P;
+      const long off0 = p * Cp + 8 * cg, off1 = p1 * Cp + 8 * cg;
+      float v0[8], v1[8];
+      {
+        const uint4 a0 = *reinterpret_cast<const uint4*>(in.p[0] + off0);
+        const uint4 a1 = ok1 ? *reinterpret_cast<const uint4*>(in.p[0] + off1) : make_uint4(0, 0, 0, 0);
+        unpack8(a0, v0);
+        unpack8(a1, v1);
+      }
       for (int i = 1; i < k; ++i) {
-        float u[8];
-        unpack8(*reinterpret_cast<const uint4*>(in.p[i] + off), u);
+        const uint4 b0 = *reinterpret_cast<const uint4*>(in.p[i] + off0);
+        const uint4 b1 = ok1 ? *reinterpret_cast<const uint4*>(in.p[i] + off1) : make_uint4(0, 0, 0, 0);
+        float u0[8], u1[8];
+        unpack8(b0, u0);
+        unpack8(b1, u1);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += u[e];
+        for (int e = 0; e < 8; ++e) { v0[e] += u0[e]; v1[e] += u1[e]; }
       }
       if (out != nullptr) {
-        uint4 pk = pack8(v);
-        *reinterpret_cast<uint4*>(out + off) = pk;
-        unpack8(pk, v);  // statistics of the stored (rounded) tensor
+        const uint4 pk0 = pack8(v0), pk1 = pack8(v1);
+        *reinterpret_cast<uint4*>(out + off0) = pk0;
+        if (ok1) *reinterpret_cast<uint4*>(out + off1) = pk1;
+        unpack8(pk0, v0);  // statistics of the stored (rounded) tensor
+        unpack8(pk1, v1);
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { s[e] += v[e]; q[e] += v[e] * v[e]; }
+      for (int e = 0; e < 8; ++e) {   // the out-of-range slot holds zeros: adds nothing
+        s[e] += v0[e] + v1[e];
+        q[e] += v0[e] * v0[e] + v1[e] * v1[e];
+      }
     }
   }
 #pragma unroll
@@ -250,16 +268,29 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
   load8f(shift + 8 * cg, b);
   load8f(mean + 8 * cg, mu);
   if (r < R) {
-    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
-      const long off = p * Cp + 8 * cg;
-      float g[8], v[8];
-      unpack8(*reinterpret_cast<const uint4*>(dz + off), g);
-      unpack8(*reinterpret_cast<const uint4*>(y + off), v);
+    // kPartUnroll pixels' (dz, y) vectors issued before any is consumed: 2*kPartUnroll 16-B loads in
+    // flight per thread (one pair per trip left the pass latency-bound at ~1 block per CU).
+    const long stride = (long)gridDim.x * R;
+    for (long p = (long)blockIdx.x * R + r; p < P; p += kPartUnroll * stride) {
+      uint4 gin[kPartUnroll], yin[kPartUnroll];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
-        s[e] += gr;
-        q[e] += gr * (v[e] - mu[e]);
+      for (int u = 0; u < kPartUnroll; ++u) {
+        const long q = p + u * stride;
+        const bool ok = q < P;
+        gin[u] = ok ? *reinterpret_cast<const uint4*>(dz + q * Cp + 8 * cg) : make_uint4(0, 0, 0, 0);
+        yin[u] = ok ? *reinterpret_cast<const uint4*>(y + q * Cp + 8 * cg) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kPartUnroll; ++u) {
+        float g[8], v[8];
+        unpack8(gin[u], g);   // out-of-range slots are zero: gr = 0 adds nothing
+        unpack8(yin[u], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
+          s[e] += gr;
+          q[e] += gr * (v[e] - mu[e]);
+        }
       }
     }
   }

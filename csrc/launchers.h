@@ -143,3 +143,6 @@ void ema_update(float* ema, const float* model, const float* hyper, long n, hipS
 // metrics.hip
 void confmat_update(const float* logits, const int64_t* target, int64_t* confmat, int N, int C, long HW,
                     int ignore_index, hipStream_t s);
+void bilinear_resize(const float* x, float* y, long NC, int IH, int IW, int OH, int OW, int align_corners,
+                     hipStream_t s);
+void colorize(const float* logits, const uint8_t* lut, uint8_t* rgb, int N, int C, long HW, hipStream_t s);

@@ -18,12 +18,12 @@ import os
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 from PIL import Image
 
 from ..models import get_teacher_model
 from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
 from .base_trainer import BaseTrainer
+from ..ops.resample import colorize, resize_bilinear
 from .loss import kd_loss_fn
 
 
@@ -190,11 +190,11 @@ class SegTrainer(BaseTrainer):
             stride = config.val_img_stride
             resized = H % stride != 0 or W % stride != 0
             if resized:
-                images = F.interpolate(images, (H // stride * stride, W // stride * stride), mode='bilinear')
+                images = resize_bilinear(images, (H // stride * stride, W // stride * stride))
             masks = masks.to(self.device, dtype=torch.long)
             preds = self._ema_forward(images)
             if resized:
-                preds = F.interpolate(preds, masks.size()[1:], mode='bilinear', align_corners=True)
+                preds = resize_bilinear(preds, masks.size()[1:], align_corners=True)
             if preds.shape[1] == 1:   # binary (sigmoid) path -> two-class logits for the confmat
                 preds = torch.cat([torch.zeros_like(preds), preds], 1)
             for metric in self.metrics:
@@ -233,11 +233,7 @@ class SegTrainer(BaseTrainer):
         for images, images_aug, img_names in _tqdm(self.test_loader, config.progress_bar):
             images_aug = images_aug.to(self.device, dtype=torch.float32)
             preds = fwd(images_aug)
-            if preds.shape[1] == 1:
-                idx = (preds[:, 0] > 0).long()
-            else:
-                idx = preds.max(dim=1)[1]
-            preds = self.colormap[idx].cpu().numpy()
+            preds = colorize(preds, self.colormap).cpu().numpy()
             images = images.cpu().numpy()
             for i in range(preds.shape[0]):
                 save_path = os.path.join(config.save_dir, img_names[i])

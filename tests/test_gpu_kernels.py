@@ -429,3 +429,19 @@ def test_conv_halo_matches_gather(gpu, case):
     assert _rel(dxh, dxg) < 5e-3
     for a, b in zip(wh, wg):
         assert _rel(a, b) < 5e-3
+
+
+@pytest.mark.parametrize('ac', [False, True])
+def test_bilinear_and_colorize(gpu, ac):
+    from medical_segmentation_pytorch_amd.ops.resample import colorize, resize_bilinear
+    torch.manual_seed(11)
+    x = torch.randn(2, 3, 37, 50, device=gpu)
+    for size in [(32, 64), (74, 100), (37, 50)]:
+        y = resize_bilinear(x, size, align_corners=ac)
+        ref = F.interpolate(x, size, mode='bilinear', align_corners=ac)
+        assert (y - ref).abs().max().item() < 1e-5
+    lut = torch.randint(0, 256, (4, 3), device=gpu, dtype=torch.uint8)
+    logits = torch.randn(2, 4, 9, 7, device=gpu)
+    assert torch.equal(colorize(logits, lut), lut[logits.argmax(1)])
+    b = torch.randn(2, 1, 9, 7, device=gpu)
+    assert torch.equal(colorize(b, lut), lut[(b[:, 0] > 0).long()])
