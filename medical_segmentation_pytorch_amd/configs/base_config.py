@@ -133,6 +133,9 @@ class BaseConfig:
         self.graph_warmup = 3          # eager iterations before the hipGraph capture
         self.graph_ddp = False         # also capture multi-GPU steps (RCCL inside the graph)
         self.progress_bar = True
+        self.trace = False             # roctx ranges around step phases + per-phase HIP-event timing
+        self.watchdog_timeout_s = 0    # >0: dump stacks + exit(75) after this long without a step
+        self.dist_timeout_min = 30     # process-group timeout (a dead peer errors instead of hanging)
         self.dist_group = None         # process sub-group (concurrent HPO trials); None = WORLD
 
     # ------------------------------------------------------------------

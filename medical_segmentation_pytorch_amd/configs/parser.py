@@ -115,6 +115,9 @@ def get_parser():
     _flag(p, 'synthetic_size', type=int)
     _flag(p, 'graph_ddp', action='store_true')
     _flag(p, 'gpu_augment', action='store_false')
+    _flag(p, 'trace', action='store_true')
+    _flag(p, 'watchdog_timeout_s', type=float)
+    _flag(p, 'dist_timeout_min', type=float)
     _flag(p, 'graph_warmup', type=int)
     _flag(p, 'log_interval', type=int)
     _flag(p, 'no_progress_bar', action='store_true')

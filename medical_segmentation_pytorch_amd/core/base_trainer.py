@@ -82,10 +82,17 @@ class BaseTrainer:
 
     # ------------------------------------------------------------------------------------------------
     def run(self, config):
+        from ..utils.tracing import set_tracing
+        from ..utils.watchdog import StepWatchdog
         self.parallel_model(config)
         if self.main_rank:
             save_config(config)
             log_config(config, self.logger)
+        set_tracing(getattr(config, 'trace', False))
+        self.watchdog = None
+        if getattr(config, 'watchdog_timeout_s', 0):
+            rank = int(os.getenv('RANK', 0))
+            self.watchdog = StepWatchdog(config.watchdog_timeout_s, config.save_dir, rank).start()
         start_epoch = self.cur_epoch
         for cur_epoch in range(start_epoch, config.total_epoch):
             self.cur_epoch = cur_epoch
@@ -109,6 +116,8 @@ class BaseTrainer:
             best_score = self.val_best(config, self.val_loader)
             if config.use_test_set:
                 self.test_score = self.val_best(config, self.test_loader)
+        if self.watchdog is not None:
+            self.watchdog.stop()
         destroy_ddp_process(config)
         return best_score
 

@@ -24,6 +24,8 @@ from ..models import get_teacher_model
 from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
 from .base_trainer import BaseTrainer
 from ..ops.resample import colorize, resize_bilinear
+from ..utils.tracing import trace_range
+from ..utils.watchdog import check_finite
 from .loss import kd_loss_fn
 
 
@@ -131,6 +133,7 @@ class SegTrainer(BaseTrainer):
         if not self._loss_hist:
             return
         vals = torch.stack([v for _, v, _ in self._loss_hist]).float().cpu().tolist()
+        check_finite(vals, self._loss_hist[-1][0])
         kds = [k for _, _, k in self._loss_hist]
         kdv = torch.stack(kds).float().cpu().tolist() if all(k is not None for k in kds) else None
         if config.use_tb and self.main_rank and self.writer is not None:
@@ -152,19 +155,25 @@ class SegTrainer(BaseTrainer):
         if self.graph_step is None and self._use_graph(config) and isinstance(self.model, FusedModel):
             self.graph_step = GraphedStep(self, config)
         pbar = _tqdm(self.train_loader, self.main_rank and config.progress_bar)
+        wd = getattr(self, 'watchdog', None)
         for cur_itrs, (images, masks) in enumerate(pbar):
             self.cur_itrs = cur_itrs
             self.train_itrs += 1
-            images = images.to(self.device, dtype=torch.float32, non_blocking=True)
-            masks = masks.to(self.device, dtype=torch.float32 if config.num_class == 1 else torch.long,
-                             non_blocking=True)
+            with trace_range('train/h2d'):
+                images = images.to(self.device, dtype=torch.float32, non_blocking=True)
+                masks = masks.to(self.device, dtype=torch.float32 if config.num_class == 1 else torch.long,
+                                 non_blocking=True)
             self._last_kd = None
-            if self.graph_step is not None:
-                loss = self.graph_step(images, masks)
-            else:
-                loss = self.eager_step(images, masks)
-            self.scheduler.step()
-            self.ema_model.update(self.model, self.train_itrs)
+            with trace_range('train/step'):
+                if self.graph_step is not None:
+                    loss = self.graph_step(images, masks)
+                else:
+                    loss = self.eager_step(images, masks)
+            with trace_range('train/sched_ema'):
+                self.scheduler.step()
+                self.ema_model.update(self.model, self.train_itrs)
+            if wd is not None:
+                wd.beat()
             self._loss_hist.append((self.train_itrs, loss.clone(), self._last_kd))
             if len(self._loss_hist) >= config.log_interval:
                 self._flush_logs(config, pbar)
@@ -192,7 +201,8 @@ class SegTrainer(BaseTrainer):
             if resized:
                 images = resize_bilinear(images, (H // stride * stride, W // stride * stride))
             masks = masks.to(self.device, dtype=torch.long)
-            preds = self._ema_forward(images)
+            with trace_range('val/forward'):
+                preds = self._ema_forward(images)
             if resized:
                 preds = resize_bilinear(preds, masks.size()[1:], align_corners=True)
             if preds.shape[1] == 1:   # binary (sigmoid) path -> two-class logits for the confmat

@@ -68,6 +68,10 @@ def set_device(config, rank):
         if not dist.is_initialized():
             backend = config.dist_backend or ('nccl' if use_gpu else 'gloo')
             kw = {'device_id': torch.device('cuda', rank)} if (use_gpu and backend == 'nccl') else {}
+            from .watchdog import process_group_timeout
+            timeout = process_group_timeout(config)
+            if timeout is not None:
+                kw['timeout'] = timeout
             dist.init_process_group(backend=backend, init_method='env://', **kw)
         device = torch.device('cuda', rank) if use_gpu else torch.device('cpu')
         config.gpu_num = group_size(config)
