@@ -402,34 +402,47 @@ constexpr int DW_CH = 32;               // co rows and ci channels per block
 struct DwTile { int TH, TW, tw_shift, ey0, ex0, HH, HWd, HWv, tiles_y, tiles_x; float inv_hwv; };
 
 constexpr int kDwWaves = 8;      // waves per block: each owns <= 3 (tap, ci16) pairs of a 3x3
-constexpr int kDwStage = 7;      // staging elements per thread: (256 + halo) / (16 * kDwWaves) for every T <= 9 tap set
+constexpr int kDwMaxHalo = 640;  // halo pixels the staging registers cover (every T <= 9 tap set)
 constexpr long kDwSplitTarget = 256;
+constexpr int kDwMaxNcb = 3;     // 32-row dY sub-tiles per block, all sharing ONE staged input halo
+constexpr int kDwMaxLds = 120 * 1024;
+// staging elements per thread: NCB dY sub-tiles (2 slots of 128 pixels each) + the halo
+constexpr int dw_stage(int ncb) { return 2 * ncb + kDwMaxHalo / (16 * kDwWaves); }
 
 DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 16-ch half, 4-ch sub)
   return pix * DW_CH + 16 * (half ^ ((pix >> 3) & 1)) + 4 * sub4;
 }
 
-template <int NPW>
+// NCB > 1 (wide dY: horizontally fused convs, wide layers): the block owns NCB consecutive 32-row co
+// sub-tiles.  The input halo is staged, and every B fragment read from LDS, ONCE per slice for all of
+// them: one input pass per NCB sub-tiles instead of per sub-tile, and fewer LDS reads/writes per MFMA.
+template <int NPW, int NCB>
 __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
                                                               DwTile tl, int KT, long ntiles, int nrep) {
+  constexpr int NST = dw_stage(NCB);
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
-  constexpr int NPX = 256, NSL = 8;
-  uint16_t* sY = dsm;                       // [256][32]  swizzled
-  uint16_t* sX = dsm + NPX * DW_CH;         // [HH * HWd][32]  swizzled
+  constexpr int NPX = 256, NSL = 8, SUB = NPX * DW_CH;
+  uint16_t* sY = dsm;                       // [NCB][256][32]  swizzled
+  uint16_t* sX = dsm + NCB * SUB;           // [HH * HWd][32]  swizzled
   __shared__ int2 s_tap[kMaxTaps];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, p4 = lr & 3;
-  const int co0 = blockIdx.y * DW_CH, ci0 = blockIdx.z * DW_CH;
+  const int co0 = blockIdx.y * DW_CH * NCB, ci0 = blockIdx.z * DW_CH;
   const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
 
   // per-thread loader roles: vector vv = tid & 3 (8 channels), pixel lane vp = tid >> 2 (16 per wave)
   const int vv = tid & 3, vp = tid >> 2;
-  const int yco = co0 + 8 * vv;
-  const bool y_ok = yco < rows;
-  const int y_g = y_ok ? yco / g.Cgo : 0;
-  const uint16_t* y_base = P.dy[y_g] + (yco - y_g * g.Cgo);
+  const uint16_t* y_base[NCB];
+  bool y_ok[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int yco = co0 + DW_CH * cb + 8 * vv;
+    y_ok[cb] = yco < rows;
+    const int y_g = y_ok[cb] ? yco / g.Cgo : 0;
+    y_base[cb] = P.dy[y_g] + (y_ok[cb] ? yco - y_g * g.Cgo : 0);
+  }
   const int xci = ci0 + 8 * vv;
   const bool x_ok = xci < Cip;
   const int x_g = x_ok ? xci / g.Cgi : 0;
@@ -447,8 +460,11 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   for (int i = 0; i < 2; ++i) { offA[i][0] = dw_elem(plo, i, p4); offA[i][1] = dw_elem(phi, i, p4); }
   // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32.
   // Only the 16-channel halves that hold real channels are paired (a 40-channel input's second chunk
-  // has one), and the co half past `rows` is skipped: no MFMA runs on all-padding tiles.
-  const int nhv = min(2, (Cip - ci0 + 15) >> 4), nco = min(2, (rows - co0 + 15) >> 4);
+  // has one), and co halves past `rows` are skipped: no MFMA runs on all-padding tiles.
+  const int nhv = min(2, (Cip - ci0 + 15) >> 4);
+  int nco[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) nco[cb] = max(0, min(2, (rows - co0 - DW_CH * cb + 15) >> 4));
   const int npairs = nhv * g.T;
   int offB[NPW][2];
 #pragma unroll
@@ -460,42 +476,47 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
     offB[j][1] = dw_elem((ry_hi + d.x) * tl.HWd + cx_hi + d.y, cf, p4);
   }
 
-  f32x4_t acc[2][NPW];
+  f32x4_t acc[NCB][2][NPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) acc[cb][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nh = tl.HH * tl.HWv;
-  // Software pipeline over the block's tiles: a tile's staging loads (<= kDwStage x 16 B per thread,
+  // Software pipeline over the block's tiles: a tile's staging loads (NST x 16 B per thread,
   // host-checked) are issued into registers before the previous tile's MFMA phase and written to LDS
-  // after it, so HBM latency hides under the MFMAs.
-  uint4 sv[kDwStage];
-  int sd[kDwStage];
+  // after it, so HBM latency hides under the MFMAs.  Slot u < 2*NCB is dY sub-tile u/2 (pixels
+  // vp + 128*(u&1)); the other slots walk the halo.
+  uint4 sv[NST];
+  int sd[NST];
   auto stage_load = [&](long tix) {
     const int per_img = tl.tiles_y * tl.tiles_x;
     const int n = (int)(tix / per_img);
     const int rem = (int)(tix - (long)n * per_img);
     const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
-    const uint16_t* yim = y_base + (long)n * g.OH * g.OW * g.Cgo;
+    const long yoff = (long)n * g.OH * g.OW * g.Cgo;
     const uint16_t* xim = x_base + (long)n * g.IH * g.IW * g.Cgi;
 #pragma unroll
-    for (int u = 0; u < kDwStage; ++u) {
-      const int e = vp + 16 * kDwWaves * u;
+    for (int u = 0; u < NST; ++u) {
       sv[u] = make_uint4(0, 0, 0, 0);
       sd[u] = -1;
-      if (e < NPX) {
+      if (u < 2 * NCB) {
+        const int cb = u >> 1, e = vp + 16 * kDwWaves * (u & 1);
         const int oy = y0 + (e >> tl.tw_shift), ox = x0 + (e & (tl.TW - 1));
-        sd[u] = dw_elem(e, vv >> 1, 2 * (vv & 1));
-        if (y_ok && oy < g.OH && ox < g.OW)
-          sv[u] = *reinterpret_cast<const uint4*>(yim + (oy * g.OW + ox) * g.Cgo);
-      } else if (e < NPX + nh) {
-        const int hp = e - NPX;
-        const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
-        const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
-        sd[u] = NPX * DW_CH + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
-        if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
-          sv[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
+        sd[u] = cb * SUB + dw_elem(e, vv >> 1, 2 * (vv & 1));
+        if (y_ok[cb] && oy < g.OH && ox < g.OW)
+          sv[u] = *reinterpret_cast<const uint4*>(y_base[cb] + yoff + (oy * g.OW + ox) * g.Cgo);
+      } else {
+        const int hp = vp + 16 * kDwWaves * (u - 2 * NCB);
+        if (hp < nh) {
+          const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
+          const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
+          sd[u] = NCB * SUB + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
+          if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+            sv[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
+        }
       }
     }
   };
@@ -503,29 +524,35 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
     __syncthreads();   // previous tile's LDS reads are done
 #pragma unroll
-    for (int u = 0; u < kDwStage; ++u)
+    for (int u = 0; u < NST; ++u)
       if (sd[u] >= 0) *reinterpret_cast<uint4*>(&sY[sd[u]]) = sv[u];
     __syncthreads();
     if (tix + gridDim.x < ntiles) stage_load(tix + gridDim.x);   // in flight during the MFMAs
     for (int sl = 0; sl < NSL; ++sl) {
       const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
-      uint4 fa[2];
+      uint4 fa[NCB][2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (i < nco) {
-          const uint2 lo = tr_read(&sY[sa + offA[i][0]]);
-          const uint2 hi = tr_read(&sY[sa + offA[i][1]]);
-          fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          fa[cb][i] = make_uint4(0, 0, 0, 0);
+          if (i < nco[cb]) {   // block-uniform: EXEC stays all ones for the transposed reads
+            const uint2 lo = tr_read(&sY[cb * SUB + sa + offA[i][0]]);
+            const uint2 hi = tr_read(&sY[cb * SUB + sa + offA[i][1]]);
+            fa[cb][i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          }
         }
-      }
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
         if (wave + kDwWaves * j < npairs) {
           const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
           const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          acc[0][j] = mfma16x16x32(fa[0], fb, acc[0][j]);
-          if (nco == 2) acc[1][j] = mfma16x16x32(fa[1], fb, acc[1][j]);
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+              if (i < nco[cb]) acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb, acc[cb][i][j]);
         }
       }
     }
@@ -541,12 +568,14 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
     const int ci = ci0 + 16 * cf + lr;
     if (ci >= Cip) continue;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + 16 * i + 4 * lg + r;
-        if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dwr[(long)co * KT + t * Cip + ci], acc[i][j][r]);
-      }
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + DW_CH * cb + 16 * i + 4 * lg + r;
+          if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dwr[(long)co * KT + t * Cip + ci], acc[cb][i][j][r]);
+        }
   }
 }
 
@@ -1065,7 +1094,9 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   else dispatch_igemm<false>(a, mi, nj, wpx, s);
 }
 
-static size_t wgrad_halo_lds(const DwTile& tl) { return ((size_t)256 + (size_t)tl.HH * tl.HWd) * DW_CH * 2; }
+static size_t wgrad_halo_lds(const DwTile& tl, int ncb) {
+  return ((size_t)256 * ncb + (size_t)tl.HH * tl.HWd) * DW_CH * 2;
+}
 
 static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
   if (g.stride != 1 || g.T > 9) return false;
@@ -1086,8 +1117,8 @@ static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
   tl.inv_hwv = 1.0f / (float)tl.HWv;
   tl.tiles_y = cdiv(g.OH, tl.TH);
   tl.tiles_x = cdiv(g.OW, tl.TW);
-  if (256 + tl.HH * tl.HWv > 16 * kDwWaves * kDwStage) return false;   // the pipelined staging registers
-  return wgrad_halo_lds(tl) <= 64 * 1024;
+  if (tl.HH * tl.HWv > kDwMaxHalo) return false;   // the pipelined staging registers
+  return wgrad_halo_lds(tl, 1) <= 64 * 1024;
 }
 
 // dW replicas for the halo path: as many as fit in ~4 MB (at most 16)
@@ -1111,7 +1142,15 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
   DwTile tl{};
   if (!trans && wgrad_halo_ok(g, tl)) {
     const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;
-    const int gy = cdiv(rows, DW_CH), gz = cdiv(g.Gi * g.Cgi, DW_CH);
+    // co sub-tiles per block: as many as the LDS budget allows (<= kDwMaxNcb; env MSP_DW_NCB caps it)
+    static int max_ncb = -1;
+    if (max_ncb < 0) {
+      const char* e = getenv("MSP_DW_NCB");
+      max_ncb = (e != nullptr && atoi(e) > 0) ? std::min(atoi(e), kDwMaxNcb) : kDwMaxNcb;
+    }
+    int ncb = std::min(max_ncb, cdiv(rows, DW_CH));
+    while (ncb > 1 && wgrad_halo_lds(tl, ncb) > (size_t)kDwMaxLds) --ncb;
+    const int gy = cdiv(rows, DW_CH * ncb), gz = cdiv(g.Gi * g.Cgi, DW_CH);
     // Blocks split the tiles and add their dW slab with fp32 atomics (into nrep replicas): atomic bytes
     // = nsplit * rows * KT * 4, so one 8-wave block per CU that software-pipelines its ~8 tiles beats
     // more, shorter-lived blocks.
@@ -1123,11 +1162,24 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
     long nsplit = split_target / ((long)gy * gz);
     if (nsplit < 1) nsplit = 1;
     if (nsplit > ntiles) nsplit = ntiles;
-    const size_t lds = wgrad_halo_lds(tl);
+    const size_t lds = wgrad_halo_lds(tl, ncb);
     dim3 grid((unsigned)nsplit, gy, gz);
     const int npw = cdiv(2 * g.T, kDwWaves);
-#define HW_(N_) if (npw == N_) { hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, tl, KT, ntiles, nrep); return; }
-    HW_(1) HW_(2) HW_(3)
+    // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU) is opted into once per instantiation, before any
+    // graph capture (the first call of every shape runs eagerly)
+#define HW_(N_, C_)                                                                                      \
+    if (npw == N_ && ncb == C_) {                                                                       \
+      static bool lds_attr = false;                                                                     \
+      if (!lds_attr) {                                                                                  \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_halo_kernel<N_, C_>),       \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwMaxLds);               \
+        lds_attr = true;                                                                                \
+      }                                                                                                 \
+      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, tl, KT, \
+                         ntiles, nrep);                                                                 \
+      return;                                                                                           \
+    }
+    HW_(1, 1) HW_(2, 1) HW_(3, 1) HW_(1, 2) HW_(2, 2) HW_(3, 2) HW_(1, 3) HW_(2, 3) HW_(3, 3)
 #undef HW_
   }
   const long M = (long)g.N * g.OH * g.OW;

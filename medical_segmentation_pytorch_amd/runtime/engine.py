@@ -175,6 +175,41 @@ class GradBucketer:
         self.reset()
 
 
+class StagedScalars:
+    """A small device fp32 tensor refreshed from pinned host memory once per step, race-free.
+
+    The host runs ahead of the GPU (hipGraph replays / eager launches are asynchronous), so a single
+    pinned staging buffer could be overwritten with step k+1's values before the DMA of step k's
+    copy has read it.  The staging buffers form a ring; a slot is rewritten only after the event
+    recorded behind its previous copy completed (a stall only if the host is ``depth`` steps ahead).
+    ``dev`` keeps its address, so graphs that captured it stay valid."""
+
+    def __init__(self, n, device, depth=8):
+        self.dev = torch.zeros(n, dtype=torch.float32, device=device)
+        self.cuda = self.dev.is_cuda
+        self.ring = [torch.zeros(n, dtype=torch.float32).pin_memory() if self.cuda else torch.zeros(n)
+                     for _ in range(depth)]
+        self.events = [None] * depth
+        self.i = 0
+
+    def host(self):
+        """The next writable pinned buffer (waits for its previous copy if still in flight)."""
+        ev = self.events[self.i]
+        if ev is not None:
+            ev.synchronize()
+        return self.ring[self.i]
+
+    def push(self):
+        """Enqueue the H2D copy of the buffer returned by :meth:`host` on the current stream."""
+        buf = self.ring[self.i]
+        self.dev.copy_(buf, non_blocking=True)
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[self.i] = ev
+        self.i = (self.i + 1) % len(self.ring)
+
+
 class FlatOptimizer:
     """Adam / AdamW / SGD(momentum, wd) over the arena in one kernel (torch.optim semantics)."""
 
@@ -190,15 +225,14 @@ class FlatOptimizer:
         else:
             self.buf = torch.zeros(n, device=dev)
         self.step_count = 0
-        self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
-        self.hyper_host = torch.zeros(8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() \
-            else torch.zeros(8, dtype=torch.float32)
+        self.staged = StagedScalars(8, dev)
+        self.hyper = self.staged.dev
         self.grad_scale = 1.0
 
     def prepare(self):
         """Host-side: advance step count, write hyper-parameters, H2D copy (outside any graph)."""
         self.step_count += 1
-        h = self.hyper_host
+        h = self.staged.host()
         if self.kind in ('adam', 'adamw'):
             b1, b2 = self.betas
             h[0], h[1], h[2], h[3], h[4] = self.lr, b1, b2, self.eps, self.wd
@@ -207,7 +241,7 @@ class FlatOptimizer:
             h[7] = self.grad_scale
         else:
             h[0], h[1], h[2], h[3] = self.lr, self.momentum, self.wd, self.grad_scale
-        self.hyper.copy_(h, non_blocking=True)
+        self.staged.push()
 
     def step(self):
         C = require()

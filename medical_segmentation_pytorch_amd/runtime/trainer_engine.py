@@ -15,7 +15,7 @@ import torch.distributed as dist
 
 from ..ops._ext import require
 from ..ops.losses import cross_entropy, kd_kl_div
-from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, stat_group
+from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, StagedScalars, stat_group
 from .fused_model import FusedExecutor
 
 
@@ -44,8 +44,8 @@ class FusedStep:
         # EMA: flat copy of the parameter arena + running statistics (reference ModelEmaV2)
         self.ema_arena = Arena(self.ema_model, dev, with_grad=False)
         self.use_ema = use_ema
-        self.ema_hyper = torch.zeros(1, device=dev)
-        self.ema_hyper_host = torch.zeros(1).pin_memory()
+        self.ema_staged = StagedScalars(1, dev)
+        self.ema_hyper = self.ema_staged.dev
         self.total_steps = total_steps
         self.itrs = 0
         self.use_graph = use_graph
@@ -84,8 +84,8 @@ class FusedStep:
         self.opt.prepare()
         self.itrs += 1
         d = min(max(self.itrs / self.total_steps, 0.0), 1.0) if self.use_ema else 0.0
-        self.ema_hyper_host[0] = d
-        self.ema_hyper.copy_(self.ema_hyper_host, non_blocking=True)
+        self.ema_staged.host()[0] = d
+        self.ema_staged.push()
         self.sched.step()
 
     def __call__(self):

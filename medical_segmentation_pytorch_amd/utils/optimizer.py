@@ -42,10 +42,9 @@ class FusedOptimizer(torch.optim.Optimizer):
                 self.state[p] = {'step': torch.tensor(0.0), 'exp_avg': self.m[o:o + k].view_as(p),
                                  'exp_avg_sq': self.v[o:o + k].view_as(p)}
         self.step_count = 0
-        self.hyper = torch.zeros(8, dtype=torch.float32, device=device)
-        self.hyper_host = torch.zeros(8, dtype=torch.float32)
-        if device.type == 'cuda':
-            self.hyper_host = self.hyper_host.pin_memory()
+        from ..runtime.engine import StagedScalars
+        self.staged = StagedScalars(8, device)
+        self.hyper = self.staged.dev
         self.bucketer = None
         self.grad_scale = 1.0
 
@@ -60,7 +59,7 @@ class FusedOptimizer(torch.optim.Optimizer):
         """Write this step's hyper-parameters to the device (host work, outside any hipGraph)."""
         self.step_count += 1
         g = self.param_groups[0]
-        h = self.hyper_host
+        h = self.staged.host()
         if self.kind == 'sgd':
             h[0], h[1], h[2], h[3] = g['lr'], g['momentum'], g['weight_decay'], self.grad_scale
         else:
@@ -69,7 +68,7 @@ class FusedOptimizer(torch.optim.Optimizer):
             h[5] = 1 - b1 ** self.step_count
             h[6] = 1 - b2 ** self.step_count
             h[7] = self.grad_scale
-        self.hyper.copy_(h, non_blocking=True)
+        self.staged.push()
 
     def launch(self):
         """Device work of a step (capturable): all-reduce wait + one optimizer kernel."""
