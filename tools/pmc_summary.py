@@ -14,7 +14,7 @@ import collections
 import re
 import sqlite3
 
-N_CU, N_SIMD = 256, 1024
+N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
 def short(name):
@@ -49,6 +49,8 @@ def main():
         out.append((t * n, k, n, t, avg))
     for tot, k, n, t, avg in sorted(out, reverse=True)[:a.top]:
         g = avg.get('GRBM_GUI_ACTIVE')
+        if g:
+            g = g / N_XCD   # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD busy cycles of the dispatch
         der = []
         if g and 'SQ_VALU_MFMA_BUSY_CYCLES' in avg:
             der.append(f"mfma_util={avg['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * N_SIMD):.3f}")
