@@ -70,6 +70,40 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   conv_igemm(a, trans, cur_stream());
 }
 
+// Data-gradient launch with the BN-backward epilogue (see ConvArgs::bn_y): stat_part receives the
+// channel partials of the BatchNorm whose output z was this conv's only input.
+void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys, const at::Tensor& stat_part,
+                 std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, const at::Tensor& bn_y,
+                 const at::Tensor& bn_coef, bool relu) {
+  ConvGeom g = make_geom(dims, dy, dx);
+  TORCH_CHECK(g.Go == 1 && (int)ys.size() == 1 && (int)xs.size() == g.Gi, "BN epilogue: one output group");
+  ConvArgs a{};
+  for (int i = 0; i < g.Gi; ++i) {
+    CHECK_BF16(xs[i]);
+    TORCH_CHECK(xs[i].numel() == (int64_t)g.N * g.IH * g.IW * g.Cgi, "x numel mismatch");
+    a.x[i] = bf(xs[i]);
+  }
+  CHECK_BF16(ys[0]);
+  TORCH_CHECK(ys[0].numel() == (int64_t)g.N * g.OH * g.OW * g.Cgo, "y numel mismatch");
+  a.y[0] = bf(ys[0]);
+  CHECK_BF16(wp);
+  TORCH_CHECK(wp.numel() == (int64_t)conv_rows_alloc(g.Go * g.Cgo) * g.Kp, "packed weight numel mismatch");
+  CHECK_F32(stat_part);
+  TORCH_CHECK(stat_part.numel() == conv_stat_blocks(g) * 2 * g.Cgo, "stat_part numel mismatch");
+  CHECK_BF16(bn_y);
+  TORCH_CHECK(bn_y.numel() == ys[0].numel(), "bn_y must have the data-gradient's shape");
+  CHECK_F32(bn_coef);
+  TORCH_CHECK(bn_coef.numel() >= 3 * (int64_t)g.Cgo, "bn_coef = [scale; shift; mean] rows of Cgo");
+  TORCH_CHECK(g.stride == 1, "BN epilogue: stride-1 data-gradients only");
+  a.w = bf(wp);
+  a.stat_part = f32(stat_part);
+  a.bn_y = bf(bn_y);
+  a.bn_coef = f32(bn_coef);
+  a.bn_relu = relu ? 1 : 0;
+  a.g = g;
+  conv_igemm(a, false, cur_stream());
+}
+
 void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const at::Tensor& dw,
                   std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
   ConvGeom g = make_geom(dims, dy, dx);
@@ -479,6 +513,7 @@ void confmat_update_t(const at::Tensor& logits, const at::Tensor& target, const 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_wgrad", &conv_wgrad_t);
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);

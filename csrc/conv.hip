@@ -74,7 +74,7 @@ DEVI int in_pixel(int pn, int ph, int pw, int2 d, const ConvGeom& g) {
 // the Tv valid taps (a 3x3 s2 data-gradient does 2.25 of 9 taps' work on average, not 9).
 struct PhaseArgs { int s, py, px, OHp, OWp, Kloop; int tA[kMaxTaps]; };
 
-template <int MI, int NJ, int WPX, bool TRANS, bool PH = false>
+template <int MI, int NJ, int WPX, bool TRANS, bool PH = false, bool BNE = false>
 __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseArgs pa) {
   const ConvGeom& g = a.g;
   __shared__ int2 s_tap[kMaxTaps];
@@ -213,8 +213,27 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
         for (int r = 0; r < 4; ++r) {
           const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
           v[r] = bf2f(f2bf(o));
-          csum[i][r] += v[r];
-          csq[i][r] += v[r] * v[r];
+        }
+        if constexpr (BNE) {   // BN-backward partials (Go == 1: cl == cb)
+          const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
+          const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
+          const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
+          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + mo * g.Cgo + cb);
+          const float y4[4] = {__uint_as_float(yy.x << 16), __uint_as_float(yy.x & 0xffff0000u),
+                               __uint_as_float(yy.y << 16), __uint_as_float(yy.y & 0xffff0000u)};
+          const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w}, m4[4] = {mu.x, mu.y, mu.z, mu.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gr = (!a.bn_relu || fmaf(y4[r], s4[r], h4[r]) > 0.f) ? v[r] : 0.f;
+            csum[i][r] += gr;
+            csq[i][r] += gr * (y4[r] - m4[r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            csum[i][r] += v[r];
+            csq[i][r] += v[r] * v[r];
+          }
         }
         *reinterpret_cast<uint2*>(yb + mo * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
@@ -665,7 +684,7 @@ constexpr int kHaloLd = 8;       // 16-B loads in flight per thread while stagin
 // convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
-template <int MI, int NJ, bool CHUNKED>
+template <int MI, int NJ, bool CHUNKED, bool BNE = false>
 __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
@@ -838,8 +857,26 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
         *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
         const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
         const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
-        cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
-        cq[i][0] += v0 * v0; cq[i][1] += v1 * v1; cq[i][2] += v2 * v2; cq[i][3] += v3 * v3;
+        if constexpr (BNE) {   // BN-backward partials (Go == 1: the row IS the channel)
+          const int cb = co0 + 16 * i + 4 * lg;
+          const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
+          const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
+          const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
+          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + img * g.Cgo + cb + pm);
+          const float y0 = __uint_as_float(yy.x << 16), y1 = __uint_as_float(yy.x & 0xffff0000u);
+          const float y2 = __uint_as_float(yy.y << 16), y3 = __uint_as_float(yy.y & 0xffff0000u);
+          const bool rl = a.bn_relu != 0;
+          const float g0 = (!rl || fmaf(y0, sc.x, sh.x) > 0.f) ? v0 : 0.f;
+          const float g1 = (!rl || fmaf(y1, sc.y, sh.y) > 0.f) ? v1 : 0.f;
+          const float g2 = (!rl || fmaf(y2, sc.z, sh.z) > 0.f) ? v2 : 0.f;
+          const float g3 = (!rl || fmaf(y3, sc.w, sh.w) > 0.f) ? v3 : 0.f;
+          cs[i][0] += g0; cs[i][1] += g1; cs[i][2] += g2; cs[i][3] += g3;
+          cq[i][0] += g0 * (y0 - mu.x); cq[i][1] += g1 * (y1 - mu.y);
+          cq[i][2] += g2 * (y2 - mu.z); cq[i][3] += g3 * (y3 - mu.w);
+        } else {
+          cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
+          cq[i][0] += v0 * v0; cq[i][1] += v1 * v1; cq[i][2] += v2 * v2; cq[i][3] += v3 * v3;
+        }
       }
     }
     if (a.stat_part != nullptr) {
@@ -869,19 +906,19 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
   }
 }
 
-template <int MI, int NJ, int WPX, bool TRANS, bool PH>
+template <int MI, int NJ, int WPX, bool TRANS, bool PH, bool BNE = false>
 void launch_igemm(const ConvArgs& a, const PhaseArgs& pa, hipStream_t s) {
   const long M = PH ? (long)a.g.N * pa.OHp * pa.OWp : (long)a.g.N * a.g.OH * a.g.OW;
   const long blocks = (long)cdiv(M, 16 * NJ * WPX) * cdiv(a.g.Go * a.g.Cgo, 16 * MI);
-  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS, PH>), dim3((unsigned)blocks), dim3(64 * WPX), 0, s, a,
+  hipLaunchKernelGGL((conv_igemm_kernel<MI, NJ, WPX, TRANS, PH, BNE>), dim3((unsigned)blocks), dim3(64 * WPX), 0, s, a,
                      pa);
 }
 
-template <bool TRANS>
+template <bool TRANS, bool BNE = false>
 void dispatch_igemm(const ConvArgs& a, int mi, int nj, int wpx, hipStream_t s) {
   const PhaseArgs pa{};
 #define CASE(MI_, NJ_, WPX_)                                                  \
-  if (mi == MI_ && nj == NJ_ && wpx == WPX_) { launch_igemm<MI_, NJ_, WPX_, TRANS, false>(a, pa, s); return; }
+  if (mi == MI_ && nj == NJ_ && wpx == WPX_) { launch_igemm<MI_, NJ_, WPX_, TRANS, false, BNE>(a, pa, s); return; }
   CASE(1, 4, 4) CASE(2, 4, 4) CASE(3, 4, 4) CASE(4, 4, 4)
   CASE(1, 4, 2) CASE(2, 4, 2) CASE(3, 4, 2) CASE(4, 4, 2)
   CASE(1, 4, 1) CASE(2, 4, 1) CASE(3, 4, 1) CASE(4, 4, 1)
@@ -1075,22 +1112,25 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
     const unsigned blocks = (unsigned)((long)a.g.N * hg.tiles_y * hg.tiles_x);
     const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo);
-#define HC_(MI_)                                                                                             \
-    if (mi == MI_) {                                                                                         \
+    // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers
+#define HC_(MI_, BNE_)                                                                                       \
+    if (mi == MI_ && bne == BNE_) {                                                                          \
       if (hg.nch > 1)                                                                                        \
-        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true>), dim3(blocks), dim3(64 * kHaloWaves), \
-                           lds, s, a, hg);                                                                   \
+        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>), dim3(blocks),           \
+                           dim3(64 * kHaloWaves), lds, s, a, hg);                                           \
       else                                                                                                   \
-        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false>), dim3(blocks), dim3(64 * kHaloWaves), \
-                           lds, s, a, hg);                                                                   \
+        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>), dim3(blocks),          \
+                           dim3(64 * kHaloWaves), lds, s, a, hg);                                           \
       return;                                                                                                \
     }
-    HC_(1) HC_(2) HC_(3) HC_(4)
+    const bool bne = a.bn_y != nullptr;
+    HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
 #undef HC_
   }
   const int nj = conv_pick_nj(a.g, mi);
   const int wpx = conv_pick_wpx(a.g, mi, nj);
   if (trans) dispatch_igemm<true>(a, mi, nj, wpx, s);
+  else if (a.bn_y != nullptr) dispatch_igemm<false, true>(a, mi, nj, wpx, s);
   else dispatch_igemm<false>(a, mi, nj, wpx, s);
 }
 

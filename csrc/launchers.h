@@ -31,6 +31,12 @@ struct ConvArgs {
   const uint16_t* w;    // packed [conv_rows_alloc(Go*Cgo)][Kp]
   const float* bias;    // nullable, [Cgo_l] (Go == 1 only)
   float* stat_part;     // nullable, [conv_stat_blocks][2][Go*Cgo]
+  // BN-backward epilogue (data-gradient of a stride-1 conv whose input is the output z of a BatchNorm
+  // (+ReLU) read by no other op; Go == 1): the stored output IS dL/dz, and stat_part receives
+  // (sum g, sum g*(y - mean)) with g = dz * relu'(y*scale + shift) -- the BN backward's channel partials.
+  const uint16_t* bn_y;  // nullable: that BN's input y, [N, OH, OW, Cgo]
+  const float* bn_coef;  // [3][Cgo]: scale, shift, mean
+  int bn_relu;
   ConvGeom g;
 };
 

@@ -50,6 +50,18 @@ class BNState:
                        bn.num_batches_tracked)
 
 
+class BwdStatsHandle:
+    """Links a training-mode BN output ``z`` that exactly ONE stride-1 conv reads (nothing else) to
+    that conv: the conv's data-gradient launch -- whose output is dL/dz -- also emits the BN backward's
+    channel partials (``conv_fwd_bn``), and the BN backward then skips its own partial-sum pass over
+    (dz, y).  Only the executor, which knows every consumer of ``z``, creates handles."""
+    __slots__ = ('y', 'stats', 'relu', 'part')
+
+    def __init__(self):
+        self.y = self.stats = self.part = None
+        self.relu = False
+
+
 def _world(group):
     if group is None or not dist.is_available() or not dist.is_initialized():
         return 1
@@ -86,7 +98,7 @@ class _BNAct(torch.autograd.Function):
     # inputs: st, relu, training, part_info, gamma, beta, *xs  (gamma/beta are inputs so that their
     # grads reach autograd when the engine gives no grad sink)
     @staticmethod
-    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, gamma, beta, *xs):
+    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, gamma, beta, *xs):
         C = require()
         xs = [x.contiguous() for x in xs]
         y0 = xs[0]
@@ -128,6 +140,9 @@ class _BNAct(torch.autograd.Function):
         z = torch.empty_like(y)
         C.bn_act_apply(y, stats, z, P, Cp, relu)
         ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
+        ctx.handle = handle if training else None
+        if ctx.handle is not None:
+            handle.y, handle.stats, handle.relu, handle.part = y, stats, relu, None
         ctx.save_for_backward(y, stats)
         return z
 
@@ -140,14 +155,19 @@ class _BNAct(torch.autograd.Function):
         Cp = y.shape[-1]
         P = y.numel() // Cp
         dev = y.device
-        nblk = C.bn_partial_blocks(P, Cp)
-        part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
-        C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
+        h = ctx.handle
+        if h is not None and h.part is not None:   # partials came with dz from the consumer's dgrad
+            part, h.part = h.part, None
+            nblk = part.shape[0]
+        else:
+            nblk = C.bn_partial_blocks(P, Cp)
+            part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+            C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
         world = _world(st.group) if ctx.training else 1
         fused = ctx.training and world == 1
         sums = None if fused else _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
-        need_g = ctx.needs_input_grad[4] and st.weight_sink is None
-        need_b = ctx.needs_input_grad[5] and st.bias_sink is None
+        need_g = ctx.needs_input_grad[5] and st.weight_sink is None
+        need_b = ctx.needs_input_grad[6] and st.bias_sink is None
         dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
         dbeta = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_b else None
         g_t = st.weight_sink if st.weight_sink is not None else dgamma
@@ -173,17 +193,17 @@ class _BNAct(torch.autograd.Function):
         C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
         if st.ready_hook is not None:
             st.ready_hook([t for t in (st.weight, st.bias) if t is not None])
-        return (None, None, None, None,
+        return (None, None, None, None, None,
                 dgamma[:st.C] if dgamma is not None else None,
                 dbeta[:st.C] if dbeta is not None else None) + (dy,) * ctx.k
 
 
-def bn_act(xs, st: BNState, relu=True, training=True, part_info=None):
+def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None):
     """act(BN(sum(xs))) for NHWC bf16 feature maps.  ``part_info = (part, width, col_off)`` reuses
-    conv-epilogue channel partials (single input only)."""
+    conv-epilogue channel partials (single input only); ``handle``: see :class:`BwdStatsHandle`."""
     if isinstance(xs, torch.Tensor):
         xs = [xs]
-    return _BNAct.apply(st, relu, training, part_info, st.weight, st.bias, *xs)
+    return _BNAct.apply(st, relu, training, part_info, handle, st.weight, st.bias, *xs)
 
 
 # ------------------------------------------------------------------------------------------------

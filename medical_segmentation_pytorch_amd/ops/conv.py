@@ -194,7 +194,7 @@ def _taps(tl):
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, *args):
+    def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, bn_handle, *args):
         C = require()
         xs = [a.contiguous() for a in args[:nx]]
         n, ih, iw, _ = xs[0].shape
@@ -217,6 +217,8 @@ class _ConvFn(torch.autograd.Function):
         C.conv_fwd(xs, wp, ys, bias, part, dims, dy, dx, trans)
         ctx.plan = plan
         ctx.nx = nx
+        ctx.bn_handle = bn_handle if (bn_handle is not None and plan.stride == 1 and not plan.transposed
+                                      and plan.Gi == 1) else None
         ctx.shape = (n, ih, iw, oh, ow)
         ctx.save_for_backward(*xs)
         if part is None:
@@ -236,7 +238,7 @@ class _ConvFn(torch.autograd.Function):
             gys.append(torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None
                        else g.contiguous())
         dxs = [None] * ctx.nx
-        if any(ctx.needs_input_grad[3:3 + ctx.nx]):
+        if any(ctx.needs_input_grad[4:4 + ctx.nx]):
             wd, Kp_d = plan.pack_dgrad(dev)
             dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
             dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
@@ -246,7 +248,15 @@ class _ConvFn(torch.autograd.Function):
             else:
                 dy, dx = _taps(plan.taps_bwd)
                 trans = plan.stride > 1
-            C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
+            h = ctx.bn_handle
+            if h is not None and h.y is not None and not trans:
+                # dL/dx is the BN output's gradient: emit the BN backward partials in the epilogue
+                nblk = C.conv_stat_blocks(dims_d, dy, dx)
+                part = torch.empty(nblk, 2, plan.Gi * plan.Cgi, dtype=torch.float32, device=dev)
+                C.conv_fwd_bn(gys, wd, dxs, part, dims_d, dy, dx, h.y, h.stats, h.relu)
+                h.part = part
+            else:
+                C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
         wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev)
         bgrad = None
         if plan.bias is not None:
@@ -257,8 +267,8 @@ class _ConvFn(torch.autograd.Function):
                 bgrad = bg
         if plan.ready_hook is not None:
             plan.ready_hook([b.weight for b in plan.branches] + ([plan.bias] if plan.bias is not None else []))
-        # inputs of forward: plan, want_stats, nx, *xs, *weights, bias
-        out = [None, None, None] + dxs + wgrads
+        # inputs of forward: plan, want_stats, nx, bn_handle, *xs, *weights, bias
+        out = [None, None, None, None] + dxs + wgrads
         if plan.bias is not None:
             out.append(bgrad)
         return tuple(out)
@@ -304,14 +314,15 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
     return res
 
 
-def conv(plan: ConvPlan, xs, want_stats=False):
-    """Run ``plan`` on input group tensors ``xs``; returns (list of Go output tensors, stat partials)."""
+def conv(plan: ConvPlan, xs, want_stats=False, bn_handle=None):
+    """Run ``plan`` on input group tensors ``xs``; returns (list of Go output tensors, stat partials).
+    ``bn_handle``: the input is a BN output read by this conv only (see ``ops.bn.BwdStatsHandle``)."""
     if isinstance(xs, torch.Tensor):
         xs = [xs]
     assert len(xs) == plan.Gi
     weights = [b.weight for b in plan.branches]
     extra = [plan.bias] if plan.bias is not None else []
-    out = _ConvFn.apply(plan, want_stats, len(xs), *xs, *weights, *extra)
+    out = _ConvFn.apply(plan, want_stats, len(xs), bn_handle, *xs, *weights, *extra)
     return list(out[:plan.Go]), (out[plan.Go] if want_stats else None)
 
 

@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BNState, bn_act
+from ..ops.bn import BNState, BwdStatsHandle, bn_act
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
@@ -50,6 +50,9 @@ class FusedExecutor:
         self._plans = {}
         self._bns = {}
         self.pack_program = None
+        # BN outputs read by exactly one stride-1 conv: id(z) -> (z, BwdStatsHandle); the consuming conv
+        # pops its input's handle (see ops.bn.BwdStatsHandle).  Reset every forward.
+        self._handles = {}
 
     def build_pack_program(self, device):
         """After one forward created every plan: pack all weights in one launch per step."""
@@ -118,30 +121,44 @@ class FusedExecutor:
             self._plans[key] = p
         return p
 
+    # -- single-consumer BN outputs ------------------------------------------------------------------
+    def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
+        """bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
+        h = BwdStatsHandle() if (single and training) else None
+        z = bn_act(xs, st, relu, training, part_info, handle=h)
+        if h is not None:
+            self._handles[id(z)] = (z, h)
+        return z
+
+    def _conv(self, plan, xs, training):
+        h = self._handles.pop(id(xs[0]), (None, None))[1] if len(xs) == 1 else None
+        return conv(plan, xs, want_stats=training, bn_handle=h)
+
     # -- blocks -------------------------------------------------------------------------------------
-    def cba(self, m, xs, training):
+    def cba(self, m, xs, training, single=False):
         """ConvBNAct: Sequential(conv, BN, act)."""
         if isinstance(xs, torch.Tensor):
             xs = [xs]
         plan = self.plan_conv(m[0], gi=len(xs))
-        (y,), part = conv(plan, xs, want_stats=training)
-        return bn_act([y], self.bn(m[1]), _is_relu(m[2]), training,
-                      (part, plan.rows, 0) if training else None)
+        (y,), part = self._conv(plan, xs, training)
+        return self._bn_out([y], self.bn(m[1]), _is_relu(m[2]), training,
+                            (part, plan.rows, 0) if training else None, single)
 
-    def bn_from_group(self, bn_mod, act, ys, part, plan, g, training):
-        return bn_act([ys[g]], self.bn(bn_mod), _is_relu(act), training,
-                      (part, plan.rows, g * plan.Cgo) if training else None)
+    def bn_from_group(self, bn_mod, act, ys, part, plan, g, training, single=False):
+        return self._bn_out([ys[g]], self.bn(bn_mod), _is_relu(act), training,
+                            (part, plan.rows, g * plan.Cgo) if training else None, single)
 
-    def residual(self, m, x, training):
+    def residual(self, m, x, training, single_out=False):
         plan = self.plan_fused3x3(('res', id(m)), [m.lower_branch[0][0]], [m.upper_branch])
-        ys, part = conv(plan, [x], want_stats=training)
-        low = self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0, training)
+        ys, part = self._conv(plan, [x], training)
+        low = self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0, training,
+                                 single=True)
         low = self.cba(m.lower_branch[1], low, training)
-        return bn_act([ys[1], low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training)
+        return self._bn_out([ys[1], low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training, single=single_out)
 
-    def _residual_tail(self, m, upper_y, low_z, training):
+    def _residual_tail(self, m, upper_y, low_z, training, single_out=False):
         low = self.cba(m.lower_branch[1], low_z, training)
-        return bn_act([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training)
+        return self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training, single=single_out)
 
     def duck(self, m, x, training):
         xb = bn_act([x], self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training)
@@ -151,23 +168,26 @@ class FusedExecutor:
         convs1 = [b3.upper_branch, r4.upper_branch, r5.upper_branch]
         plan = self.plan_fused3x3(('duck', id(m)), convs3, convs1)
         ys, part = conv(plan, [xb], want_stats=training)
-        bnz = lambda seq, g: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training)  # noqa: E731
+        # every first-conv BN output feeds one conv only (single=True); branch outputs feed the 6-way sum
+        bnz = lambda seq, g: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training, single=True)  # noqa: E731
         # widescope: d1 -> d2 -> d3 ; midscope: d1 -> d2
         o1 = bnz(b1[0], 0)
-        o1 = self.cba(b1[1], o1, training)
+        o1 = self.cba(b1[1], o1, training, single=True)
         o1 = self.cba(b1[2], o1, training)
         o2 = bnz(b2[0], 1)
         o2 = self.cba(b2[1], o2, training)
-        # residual x1 / x2 / x3 (first block's two convs come from the fused launch)
+        # residual x1 / x2 / x3 (first block's two convs come from the fused launch); inside a chain
+        # a block's output feeds only the next block's fused conv
         o3 = self._residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training)
-        o4 = self._residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training)
-        for blk in list(b4)[1:]:
-            o4 = self.residual(blk, o4, training)
-        o5 = self._residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training)
-        for blk in list(b5)[1:]:
-            o5 = self.residual(blk, o5, training)
+        rest4, rest5 = list(b4)[1:], list(b5)[1:]
+        o4 = self._residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training, single_out=bool(rest4))
+        for k, blk in enumerate(rest4):
+            o4 = self.residual(blk, o4, training, single_out=k + 1 < len(rest4))
+        o5 = self._residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training, single_out=bool(rest5))
+        for k, blk in enumerate(rest5):
+            o5 = self.residual(blk, o5, training, single_out=k + 1 < len(rest5))
         # separated 1x7 -> 7x1
-        o6 = self.cba(b6[0], xb, training)
+        o6 = self.cba(b6[0], xb, training, single=True)
         o6 = self.cba(b6[1], o6, training)
         return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training)
 
@@ -192,8 +212,9 @@ class FusedExecutor:
             down = self.cba(st.conv1, skip, training)
             skips.append(skip)
         x = add_n(down, shortcut)
-        for blk in model.mid_stage:
-            x = self.residual(blk, x, training)
+        mids = list(model.mid_stage)
+        for k, blk in enumerate(mids):
+            x = self.residual(blk, x, training, single_out=k + 1 < len(mids))
         for st, skip in zip(model.up_stages(), reversed(skips)):
             x = up2_add(x, skip)
             x = self.duck(st.duck, x, training)
@@ -204,12 +225,12 @@ class FusedExecutor:
         skips = []
         for i in range(1, 5):
             st = getattr(model, f'down_stage{i}')
-            f = self.cba(st.conv[0], x, training)
+            f = self.cba(st.conv[0], x, training, single=True)
             f = self.cba(st.conv[1], f, training)
             skips.append(f)
             p = st.pool
             x = maxpool(f, p.kernel_size, p.stride, p.padding)
-        x = self.cba(model.mid_stage[0], x, training)
+        x = self.cba(model.mid_stage[0], x, training, single=True)
         x = self.cba(model.mid_stage[1], x, training)
         for i in range(4, 0, -1):
             st = getattr(model, f'up_stage{i}')
@@ -217,15 +238,16 @@ class FusedExecutor:
             plan = self.plan_deconv(dc[0])
             (u,), part = conv(plan, [x], want_stats=training)
             u = bn_act([u], self.bn(dc[1]), _is_relu(dc[2]), training, (part, plan.rows, 0) if training else None)
-            x = self.cba(st.conv[0], [u, skips[i - 1]], training)
+            x = self.cba(st.conv[0], [u, skips[i - 1]], training, single=True)
             x = self.cba(st.conv[1], x, training)
         return self.head(model.seg_head, x, model.num_class)
 
     # -- smp Unet with a ResNet encoder (reference models/__init__.py:23-25; KD teacher :42-62) ---------
-    def conv_bn(self, conv_mod, bn_mod, x, training, relu):
+    def conv_bn(self, conv_mod, bn_mod, x, training, relu, single=False):
         plan = self.plan_conv(conv_mod)
-        (y,), part = conv(plan, [x], want_stats=training)
-        return bn_act([y], self.bn(bn_mod), relu, training, (part, plan.rows, 0) if training else None)
+        (y,), part = self._conv(plan, [x], training)
+        return self._bn_out([y], self.bn(bn_mod), relu, training, (part, plan.rows, 0) if training else None,
+                            single)
 
     def resnet_block(self, blk, x, training):
         """torchvision BasicBlock / Bottleneck: ``relu(bn_last(conv_last(...)) + identity)``."""
@@ -233,9 +255,9 @@ class FusedExecutor:
             idt = self.conv_bn(blk.downsample[0], blk.downsample[1], x, training, relu=False)
         else:
             idt = x
-        o = self.conv_bn(blk.conv1, blk.bn1, x, training, relu=True)
+        o = self.conv_bn(blk.conv1, blk.bn1, x, training, relu=True, single=True)
         if hasattr(blk, 'conv3'):
-            o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=True)
+            o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=True, single=True)
             o = self.conv_bn(blk.conv3, blk.bn3, o, training, relu=False)
         else:
             o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=False)
@@ -259,12 +281,19 @@ class FusedExecutor:
             skip = skips[i] if i < len(skips) else None
             cs = skip_ch[i] if skip is not None else 0
             x = up2_cat(x, skip, cx, cs)
-            x = self.cba(blk.conv1, x, training)
+            x = self.cba(blk.conv1, x, training, single=True)
             x = self.cba(blk.conv2, x, training)
             cx = blk.conv2[0].out_channels
         return self.head(model.segmentation_head[0], x, model.segmentation_head[0].out_channels)
 
     def forward(self, images, training=None):
+        self._handles.clear()
+        try:
+            return self._forward(images, training)
+        finally:
+            self._handles.clear()
+
+    def _forward(self, images, training=None):
         model = self.model
         training = model.training if training is None else training
         name = type(model).__name__

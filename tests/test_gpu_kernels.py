@@ -445,3 +445,37 @@ def test_bilinear_and_colorize(gpu, ac):
     assert torch.equal(colorize(logits, lut), lut[logits.argmax(1)])
     b = torch.randn(2, 1, 9, 7, device=gpu)
     assert torch.equal(colorize(b, lut), lut[(b[:, 0] > 0).long()])
+
+
+@pytest.mark.parametrize('relu,halo', [(True, True), (False, True), (True, False)])
+def test_bn_partials_from_dgrad_epilogue(gpu, relu, halo):
+    """BN output feeding one stride-1 conv: the conv's data-gradient epilogue emits the BN backward
+    partials (conv_fwd_bn) -- gradients must match the separate partial-sum pass."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    from medical_segmentation_pytorch_amd.ops.bn import BwdStatsHandle
+    C = _ext.require()
+    torch.manual_seed(12)
+    n, h, w, c = 2, 20, 24, 17
+    bnm = nn.BatchNorm2d(c).to(gpu)
+    conv_m = nn.Conv2d(c, 34, 3, 1, 1, bias=False).to(gpu)
+    res = []
+    C.conv_set_halo(halo)
+    try:
+        for use in (False, True):
+            bnm.weight.grad = bnm.bias.grad = conv_m.weight.grad = None
+            st = BNState.from_module(bnm)
+            plan = ConvPlan(3, 3, c, 34, [Branch(conv_m.weight, 0, 0, 9)], padding=(1, 1))
+            y = to_fm_reference(_bf(torch.randn(n, c, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(3))))
+            y.requires_grad_(True)
+            hdl = BwdStatsHandle() if use else None
+            z = bn_act([y], st, relu, True, None, handle=hdl)
+            (o,), _ = conv(plan, [z], want_stats=False, bn_handle=hdl)
+            g = to_fm_reference(_bf(torch.randn(n, 34, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(4))))
+            o.backward(g)
+            if use:
+                assert hdl.part is None, 'BN backward must have consumed the epilogue partials'
+            res.append((y.grad.float().clone(), bnm.weight.grad.clone(), bnm.bias.grad.clone(), conv_m.weight.grad.clone()))
+    finally:
+        C.conv_set_halo(True)
+    for a, b in zip(res[0], res[1]):
+        assert _rel(b, a) < 1e-3, _rel(b, a)
