@@ -197,6 +197,14 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[r] = (a.bias != nullptr && cl + r < g.Cgo_l) ? a.bias[cl + r] : 0.f;
+    uint2 ypre[BNE ? NJ : 1];
+    if constexpr (BNE) {   // non-PH stride-1 data-gradient: output pixel index == m
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const long m = m0 + 16 * j + lr;
+        ypre[j] = m < M ? *reinterpret_cast<const uint2*>(a.bn_y + m * g.Cgo + cb) : make_uint2(0, 0);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const long m = m0 + 16 * j + lr;
@@ -214,11 +222,11 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
           const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
           v[r] = bf2f(f2bf(o));
         }
-        if constexpr (BNE) {   // BN-backward partials (Go == 1: cl == cb)
+        if constexpr (BNE) {   // BN-backward partials (Go == 1: cl == cb); y prefetched per row group
           const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
           const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
           const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
-          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + mo * g.Cgo + cb);
+          const uint2 yy = ypre[j];
           const float y4[4] = {__uint_as_float(yy.x << 16), __uint_as_float(yy.x & 0xffff0000u),
                                __uint_as_float(yy.y << 16), __uint_as_float(yy.y & 0xffff0000u)};
           const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w}, m4[4] = {mu.x, mu.y, mu.z, mu.w};
@@ -841,31 +849,39 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
         cs[i][r] = 0.f; cq[i][r] = 0.f;
       }
     }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int p = (wave * NJ + j) * 16 + lr;
-      const int ty = ty0 + (p >> hg.tw_shift), tx = tx0 + (p & (hg.TW - 1));
-      if (ty >= g.OH || tx >= g.OW) continue;
-      const int pm = (ty * g.OW + tx) * g.Cgo;   // OH == IH, OW == IW; within the image
+    if constexpr (BNE) {
+      // BN-backward partials (Go == 1: the row IS the channel).  Row group i outer: the NJ y vectors
+      // of a row group are issued together, so HBM latency is exposed once per row group, not per
+      // pixel group (the stores in between would otherwise order every y load behind them).
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if (yb[i] == nullptr) continue;
-        float o[4];
+        const int cb = co0 + 16 * i + 4 * lg;
+        const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
+        const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
+        const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
+        const bool rl = a.bn_relu != 0;
+        uint2 yy[NJ];
+        int pmj[NJ];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = rv[i][r] ? acc[i][j][r] + bv[i][r] : 0.f;
-        const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
-        *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
-        const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
-        const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
-        if constexpr (BNE) {   // BN-backward partials (Go == 1: the row IS the channel)
-          const int cb = co0 + 16 * i + 4 * lg;
-          const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
-          const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
-          const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
-          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + img * g.Cgo + cb + pm);
-          const float y0 = __uint_as_float(yy.x << 16), y1 = __uint_as_float(yy.x & 0xffff0000u);
-          const float y2 = __uint_as_float(yy.y << 16), y3 = __uint_as_float(yy.y & 0xffff0000u);
-          const bool rl = a.bn_relu != 0;
+        for (int j = 0; j < NJ; ++j) {
+          const int p = (wave * NJ + j) * 16 + lr;
+          const int ty = ty0 + (p >> hg.tw_shift), tx = tx0 + (p & (hg.TW - 1));
+          pmj[j] = (ty < g.OH && tx < g.OW) ? (ty * g.OW + tx) * g.Cgo : -1;
+          yy[j] = pmj[j] >= 0 ? *reinterpret_cast<const uint2*>(a.bn_y + img * g.Cgo + cb + pmj[j]) : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if (pmj[j] < 0) continue;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = rv[i][r] ? acc[i][j][r] + bv[i][r] : 0.f;
+          const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(yb[i] + pmj[j]) = make_uint2(lo, hi);
+          const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
+          const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
+          const float y0 = __uint_as_float(yy[j].x << 16), y1 = __uint_as_float(yy[j].x & 0xffff0000u);
+          const float y2 = __uint_as_float(yy[j].y << 16), y3 = __uint_as_float(yy[j].y & 0xffff0000u);
           const float g0 = (!rl || fmaf(y0, sc.x, sh.x) > 0.f) ? v0 : 0.f;
           const float g1 = (!rl || fmaf(y1, sc.y, sh.y) > 0.f) ? v1 : 0.f;
           const float g2 = (!rl || fmaf(y2, sc.z, sh.z) > 0.f) ? v2 : 0.f;
@@ -873,7 +889,25 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
           cs[i][0] += g0; cs[i][1] += g1; cs[i][2] += g2; cs[i][3] += g3;
           cq[i][0] += g0 * (y0 - mu.x); cq[i][1] += g1 * (y1 - mu.y);
           cq[i][2] += g2 * (y2 - mu.z); cq[i][3] += g3 * (y3 - mu.w);
-        } else {
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int p = (wave * NJ + j) * 16 + lr;
+        const int ty = ty0 + (p >> hg.tw_shift), tx = tx0 + (p & (hg.TW - 1));
+        if (ty >= g.OH || tx >= g.OW) continue;
+        const int pm = (ty * g.OW + tx) * g.Cgo;   // OH == IH, OW == IW; within the image
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          if (yb[i] == nullptr) continue;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = rv[i][r] ? acc[i][j][r] + bv[i][r] : 0.f;
+          const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
+          const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
+          const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
           cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
           cq[i][0] += v0 * v0; cq[i][1] += v1 * v1; cq[i][2] += v2 * v2; cq[i][3] += v3 * v3;
         }
