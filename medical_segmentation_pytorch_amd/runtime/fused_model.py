@@ -16,6 +16,8 @@ What is fused relative to the module graph (reference ``models/ducknet.py``, ``m
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -23,6 +25,10 @@ from ..ops.bn import BNState, BwdStatsHandle, bn_act
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
+
+
+# env MSP_BN_EPILOGUE=0 disables the dgrad-epilogue BN partials (A/B switch)
+_BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
 
 
 def _is_relu(act_mod):
@@ -124,7 +130,7 @@ class FusedExecutor:
     # -- single-consumer BN outputs ------------------------------------------------------------------
     def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
         """bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
-        h = BwdStatsHandle() if (single and training) else None
+        h = BwdStatsHandle() if (single and training and _BN_EPILOGUE) else None
         z = bn_act(xs, st, relu, training, part_info, handle=h)
         if h is not None:
             self._handles[id(z)] = (z, h)
