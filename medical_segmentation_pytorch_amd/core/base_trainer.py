@@ -52,6 +52,17 @@ class BaseTrainer:
         self.model = get_model(config).to(self.device)
         config._fused = use_fused(config, self.model, self.device)
         self.fused = config._fused
+        if self.fused and not config.DDP and config.gpu_num > 1:
+            # The reference's single-process DP (`train_bs *= gpu_num`, lr * gpu_num;
+            # reference utils/parallel.py:26-27,40-42) has no fused equivalent: the fused engine is one
+            # process per GPU.  Never train gpu_num x the batch on GPU 0 alone -- undo the scaling.
+            if self.main_rank and self.logger:
+                self.logger.warning(f'fused engine: {config.gpu_num} GPUs visible but no torchrun; training on '
+                                    f'{self.device} only. Launch `torchrun --nproc-per-node {config.gpu_num} '
+                                    f'main.py` for data-parallel training on every GPU.')
+            config.train_bs //= config.gpu_num
+            config.gpu_num = 1
+            config.num_workers = config.base_workers
         if self.main_rank and self.logger:
             self.logger.info(f'engine: {"fused MI355X HIP kernels" if self.fused else "eager PyTorch"} '
                              f'on {self.device}')

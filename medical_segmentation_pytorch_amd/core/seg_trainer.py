@@ -107,6 +107,9 @@ class SegTrainer(BaseTrainer):
     def eager_step(self, images, masks):
         config = self.config_ref
         self.optimizer.zero_grad()
+        ex = getattr(self.model, 'executor', None)
+        if ex is not None:   # prepacked conv weights must follow the last optimizer step
+            ex.repack()
         amp = config.amp_training and not self.fused and self.device.type == 'cuda'
         dtype = torch.float16 if config.amp_dtype == 'fp16' else torch.bfloat16
         with torch.autocast('cuda', dtype=dtype, enabled=amp):

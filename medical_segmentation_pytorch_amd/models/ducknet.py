@@ -20,7 +20,7 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .layers import Activation, ConvBNAct, conv1x1
+from .modules import Activation, ConvBNAct, conv1x1
 
 
 def _bn_act(channels, act_type):

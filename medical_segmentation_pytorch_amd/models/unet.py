@@ -9,7 +9,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .layers import ConvBNAct, DeConvBNAct, conv1x1
+from .modules import ConvBNAct, DeConvBNAct, conv1x1
 
 
 class ConvBlock(nn.Sequential):

@@ -61,8 +61,11 @@ class FusedExecutor:
         self._handles = {}
 
     def build_pack_program(self, device):
-        """After one forward created every plan: pack all weights in one launch per step."""
+        """After one forward created every plan: pack all weights in one launch per step.  The
+        persistent packed buffers start zeroed, so the program runs once right away: every later
+        forward -- eager or captured -- sees the current weights even before its own repack()."""
         self.pack_program = PackProgram(list(self._plans.values()), device)
+        self.pack_program.run()
         return self.pack_program
 
     def repack(self):

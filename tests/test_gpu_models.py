@@ -104,7 +104,7 @@ def test_block_duck(gpu):
 
 
 def test_block_cba(gpu):
-    from medical_segmentation_pytorch_amd.models.layers import ConvBNAct
+    from medical_segmentation_pytorch_amd.models.modules import ConvBNAct
     _block_check(gpu, ConvBNAct(17, 34, 3, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
     _block_check(gpu, ConvBNAct(17, 34, 2, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
     _block_check(gpu, ConvBNAct(17, 17, (1, 7)), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))

@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from medical_segmentation_pytorch_amd.models import DuckNet, UNet, count_params, decoder_hub, get_model
-from medical_segmentation_pytorch_amd.models.layers import Activation
+from medical_segmentation_pytorch_amd.models.modules import Activation
 from medical_segmentation_pytorch_amd.configs import MyConfig
 
 
