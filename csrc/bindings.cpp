@@ -27,6 +27,20 @@ inline const float* f32_opt(const c10::optional<at::Tensor>& t) {
 }
 inline float* f32_opt_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(f32_opt(t)); }
 
+using OptTensors = std::vector<c10::optional<at::Tensor>>;
+
+// deferred-BN prologue coefficient rows: entry i = that input's BN stats [4][ld] fp32 (or None)
+void fill_coefs(const OptTensors& cs, int n, const std::vector<int64_t>& ld, const float** out) {
+  TORCH_CHECK(cs.empty() || (int)cs.size() == n, "one prologue entry per input");
+  for (int i = 0; i < n; ++i) {
+    out[i] = nullptr;
+    if (cs.empty() || !cs[i].has_value() || !cs[i]->defined()) continue;
+    CHECK_F32(*cs[i]);
+    TORCH_CHECK(cs[i]->numel() >= 2 * ld[i], "prologue coefficients must hold [scale; shift] rows of the input width");
+    out[i] = cs[i]->data_ptr<float>();
+  }
+}
+
 ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>& dy, const std::vector<int64_t>& dx) {
   TORCH_CHECK(dims.size() == 13, "geom dims = [N, IH, IW, Gi, Cgi, OH, OW, Go, Cgo, Cgo_l, T, Kp, stride]");
   ConvGeom g{};
@@ -44,7 +58,8 @@ ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>&
 
 void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys,
               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& stat_part,
-              std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+              std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
+              OptTensors xc, int64_t xrelu) {
   ConvGeom g = make_geom(dims, dy, dx);
   TORCH_CHECK((int)xs.size() == g.Gi && (int)ys.size() == g.Go, "group count mismatch");
   ConvArgs a{};
@@ -66,6 +81,8 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   a.w = bf(wp);
   a.bias = f32_opt(bias);
   a.stat_part = f32_opt_mut(stat_part);
+  fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), a.xc);
+  a.xrelu = (unsigned)xrelu;
   a.g = g;
   conv_igemm(a, trans, cur_stream());
 }
@@ -105,7 +122,8 @@ void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<a
 }
 
 void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const at::Tensor& dw,
-                  std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+                  std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
+                  OptTensors xc, int64_t xrelu) {
   ConvGeom g = make_geom(dims, dy, dx);
   TORCH_CHECK((int)xs.size() == g.Gi && (int)dys.size() == g.Go, "group count mismatch");
   std::vector<const uint16_t*> px, pd;
@@ -114,7 +132,10 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   CHECK_F32(dw);
   const int64_t one = (int64_t)g.Go * g.Cgo * g.T * g.Gi * g.Cgi;
   TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans), "dw numel mismatch (replicas)");
-  conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cur_stream());
+  const float* cf[kMaxGroups];
+  fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), cf);
+  TORCH_CHECK(!trans || xc.empty(), "no BN prologue on transposed weight-gradients");
+  conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream());
 }
 
 int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
@@ -159,7 +180,7 @@ void pack_batch_t(const at::Tensor& jobs, const at::Tensor& prefix, int64_t tota
 }
 
 void sum_stats_t(std::vector<at::Tensor> inputs, const c10::optional<at::Tensor>& out, const at::Tensor& part,
-                 int64_t P, int64_t Cp) {
+                 int64_t P, int64_t Cp, OptTensors coefs, int64_t relu_mask) {
   TORCH_CHECK(!inputs.empty() && (int)inputs.size() <= kMaxSumInputs, "1..8 inputs");
   TORCH_CHECK(Cp % 8 == 0 && Cp <= 2048, "Cp must be a multiple of 8, <= 2048");
   std::vector<const uint16_t*> ptrs;
@@ -168,7 +189,10 @@ void sum_stats_t(std::vector<at::Tensor> inputs, const c10::optional<at::Tensor>
   if (out.has_value() && out->defined()) { CHECK_BF16(*out); TORCH_CHECK(out->numel() == P * Cp); o = bf(*out); }
   CHECK_F32(part);
   TORCH_CHECK(part.numel() == bn_partial_blocks(P, Cp) * 2 * Cp, "part numel mismatch");
-  sum_stats(ptrs.data(), (int)ptrs.size(), o, f32(part), P, Cp, cur_stream());
+  const float* cf[kMaxSumInputs];
+  fill_coefs(coefs, (int)ptrs.size(), std::vector<int64_t>(ptrs.size(), Cp), cf);
+  for (int i = 0; i < (int)ptrs.size(); ++i) TORCH_CHECK(cf[i] == nullptr || o != nullptr, "prologue needs out");
+  sum_stats(ptrs.data(), cf, (unsigned)relu_mask, (int)ptrs.size(), o, f32(part), P, Cp, cur_stream());
 }
 
 #define CHECK_F64(t) CHECK_DEV(t); TORCH_CHECK((t).scalar_type() == at::kDouble, #t " must be fp64")
@@ -285,10 +309,13 @@ void nhwc_to_nchw_t(const at::Tensor& x, const at::Tensor& y, int64_t Cp) {
 }
 
 void up2_add_t(const at::Tensor& low, const at::Tensor& skip, const at::Tensor& out, int64_t N, int64_t h, int64_t w,
-               int64_t Cp) {
+               int64_t Cp, OptTensors coefs, int64_t relu_mask) {
   CHECK_BF16(low); CHECK_BF16(skip); CHECK_BF16(out);
   TORCH_CHECK(low.numel() == N * h * w * Cp && skip.numel() == 4 * N * h * w * Cp && out.numel() == skip.numel());
-  up2_add(bf(low), bf(skip), bf(out), N, h, w, Cp, cur_stream());
+  const float* cf[2];
+  fill_coefs(coefs, 2, {Cp, Cp}, cf);   // [low, skip]
+  up2_add(bf(low), bf(skip), bf(out), N, h, w, Cp, cf[0], (int)(relu_mask & 1), cf[1], (int)((relu_mask >> 1) & 1),
+          cur_stream());
 }
 
 void pool2_sum_t(const at::Tensor& g, const at::Tensor& out, int64_t N, int64_t h, int64_t w, int64_t Cp) {
@@ -297,13 +324,17 @@ void pool2_sum_t(const at::Tensor& g, const at::Tensor& out, int64_t N, int64_t 
   pool2_sum(bf(g), bf(out), N, h, w, Cp, cur_stream());
 }
 
-void add_n_t(std::vector<at::Tensor> inputs, const at::Tensor& out) {
+void add_n_t(std::vector<at::Tensor> inputs, const at::Tensor& out, OptTensors coefs, int64_t relu_mask) {
   TORCH_CHECK(!inputs.empty() && (int)inputs.size() <= kMaxSumInputs);
   CHECK_BF16(out);
-  TORCH_CHECK(out.numel() % 8 == 0);
+  TORCH_CHECK(out.numel() % 8 == 0 && out.dim() >= 1);
+  const int64_t Cp = out.size(-1);
+  TORCH_CHECK(Cp % 8 == 0, "channel dim must be a multiple of 8");
   std::vector<const uint16_t*> ptrs;
   for (auto& t : inputs) { CHECK_BF16(t); TORCH_CHECK(t.numel() == out.numel()); ptrs.push_back(bf(t)); }
-  add_n(ptrs.data(), (int)ptrs.size(), bf(out), out.numel(), cur_stream());
+  const float* cf[kMaxSumInputs];
+  fill_coefs(coefs, (int)ptrs.size(), std::vector<int64_t>(ptrs.size(), Cp), cf);
+  add_n(ptrs.data(), cf, (unsigned)relu_mask, (int)ptrs.size(), bf(out), out.numel(), (int)Cp, cur_stream());
 }
 
 inline uint8_t* u8(const at::Tensor& t) {
@@ -512,9 +543,12 @@ void confmat_update_t(const at::Tensor& logits, const at::Tensor& target, const 
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("xs"), py::arg("wp"), py::arg("ys"), py::arg("bias"), py::arg("stat_part"),
+        py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{},
+        py::arg("xrelu") = 0);
   m.def("conv_fwd_bn", &conv_fwd_bn);
-  m.def("conv_wgrad", &conv_wgrad_t);
+  m.def("conv_wgrad", &conv_wgrad_t, py::arg("dys"), py::arg("xs"), py::arg("dw"), py::arg("dims"), py::arg("dy"),
+        py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{}, py::arg("xrelu") = 0);
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);
   m.def("conv_stat_blocks", &conv_stat_blocks_t);
@@ -529,7 +563,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_batch", &pack_batch_t);
   m.def("pack_per_block", &pack_per_block);
   m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });
-  m.def("sum_stats", &sum_stats_t);
+  m.def("sum_stats", &sum_stats_t, py::arg("inputs"), py::arg("out"), py::arg("part"), py::arg("P"), py::arg("Cp"),
+        py::arg("coefs") = OptTensors{}, py::arg("relu_mask") = 0);
   m.def("bn_reduce_partials", &bn_reduce_partials_t);
   m.def("bn_reduce_splits", [](int64_t nblk) { return bn_reduce_splits(nblk); });
   m.def("bn_collapse", &bn_collapse_t);
@@ -544,9 +579,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
   m.def("nchw_to_nhwc", &nchw_to_nhwc_t);
   m.def("nhwc_to_nchw", &nhwc_to_nchw_t);
-  m.def("up2_add", &up2_add_t);
+  m.def("up2_add", &up2_add_t, py::arg("low"), py::arg("skip"), py::arg("out"), py::arg("N"), py::arg("h"),
+        py::arg("w"), py::arg("Cp"), py::arg("coefs") = OptTensors{}, py::arg("relu_mask") = 0);
   m.def("pool2_sum", &pool2_sum_t);
-  m.def("add_n", &add_n_t);
+  m.def("add_n", &add_n_t, py::arg("inputs"), py::arg("out"), py::arg("coefs") = OptTensors{},
+        py::arg("relu_mask") = 0);
   m.def("scale_f32", &scale_f32_t);
   m.def("aug_batch", &aug_batch_t);
   m.def("bilinear_resize", &bilinear_resize_t);

@@ -16,7 +16,24 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPartUnroll = 4;   // pixels per trip of the backward partial-sum pass
 
-struct SumInputs { const uint16_t* p[kMaxSumInputs]; };
+struct SumInputs {
+  const uint16_t* p[kMaxSumInputs];
+  const float* c[kMaxSumInputs];   // deferred-BN prologue of input i (nullable; rows scale, shift; ld = Cp)
+  unsigned relu;
+};
+
+// input i's two vectors of this trip, with its BN prologue (bf16-rounded like a materialised z)
+DEVI void load_in2(const SumInputs& in, int i, long off0, long off1, bool ok1, int c0, int Cp, float* v0, float* v1) {
+  uint4 a0 = *reinterpret_cast<const uint4*>(in.p[i] + off0);
+  uint4 a1 = ok1 ? *reinterpret_cast<const uint4*>(in.p[i] + off1) : make_uint4(0, 0, 0, 0);
+  if (in.c[i] != nullptr) {
+    const bool relu = (in.relu >> i) & 1u;
+    a0 = xform8(a0, in.c[i], Cp, c0, relu);
+    if (ok1) a1 = xform8(a1, in.c[i], Cp, c0, relu);
+  }
+  unpack8(a0, v0);
+  unpack8(a1, v1);
+}
 
 // Thread layout for per-channel reductions over NHWC: cg = tid % CG (8-channel group), r = tid / CG.
 __global__ __launch_bounds__(kBlock) void sum_stats_kernel(SumInputs in, int k, uint16_t* __restrict__ out,
@@ -37,18 +54,10 @@ __global__ __launch_bounds__(kBlock) void sum_stats_kernel(SumInputs in, int k, 
       const bool ok1 = p1 < P;
       const long off0 = p * Cp + 8 * cg, off1 = p1 * Cp + 8 * cg;
       float v0[8], v1[8];
-      {
-        const uint4 a0 = *reinterpret_cast<const uint4*>(in.p[0] + off0);
-        const uint4 a1 = ok1 ? *reinterpret_cast<const uint4*>(in.p[0] + off1) : make_uint4(0, 0, 0, 0);
-        unpack8(a0, v0);
-        unpack8(a1, v1);
-      }
+      load_in2(in, 0, off0, off1, ok1, 8 * cg, Cp, v0, v1);
       for (int i = 1; i < k; ++i) {
-        const uint4 b0 = *reinterpret_cast<const uint4*>(in.p[i] + off0);
-        const uint4 b1 = ok1 ? *reinterpret_cast<const uint4*>(in.p[i] + off1) : make_uint4(0, 0, 0, 0);
         float u0[8], u1[8];
-        unpack8(b0, u0);
-        unpack8(b1, u1);
+        load_in2(in, i, off0, off1, ok1, 8 * cg, Cp, u0, u1);
 #pragma unroll
         for (int e = 0; e < 8; ++e) { v0[e] += u0[e]; v1[e] += u1[e]; }
       }
@@ -203,11 +212,6 @@ __global__ __launch_bounds__(kFinCols * kFinParts) void bn_finalize_kernel(const
   if (training) split_sum2(tmp, S, Cp, c, c < C, sm, sq);
   if (threadIdx.x >= kFinCols) return;
   fin_fwd_channel(c, C, Cp, training != 0, sm, sq, f);
-}
-
-DEVI void load8f(const float* p, float* d) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
 }
 
 // Elementwise BN passes: each thread owns ONE 8-channel group (cg = tid % CG) for all its pixels, so
@@ -435,9 +439,14 @@ long bn_partial_blocks(long P, int Cp) {
   return b;
 }
 
-void sum_stats(const uint16_t* const* inputs, int k, uint16_t* out, float* part, long P, int Cp, hipStream_t s) {
+void sum_stats(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
+               float* part, long P, int Cp, hipStream_t s) {
   SumInputs in{};
-  for (int i = 0; i < k; ++i) in.p[i] = inputs[i];
+  for (int i = 0; i < k; ++i) {
+    in.p[i] = inputs[i];
+    in.c[i] = coefs != nullptr ? coefs[i] : nullptr;
+  }
+  in.relu = relu_mask;
   hipLaunchKernelGGL(sum_stats_kernel, dim3(bn_partial_blocks(P, Cp)), dim3(kBlock), 0, s, in, k, out, part, P, Cp);
 }
 

@@ -45,6 +45,41 @@ DEVI f32x4_t mfma16x16x32(const uint4& a, const uint4& b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
 }
 
+DEVI void load8f(const float* p, float* d) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// Deferred BatchNorm(+ReLU) applied by a CONSUMER while it loads 8 channels [c, c+8) of an input
+// ("BN prologue"): z = act(scale*y + shift) with scale = coef[c..], shift = coef[ld + c..] (the BN's
+// [4][Cp] stats rows 0 and 1; ld = Cp).  Rounded to bf16 exactly like a materialised z, so consumers
+// see bit-identical inputs.  Padded channels carry scale = shift = 0 -> 0.  Callers apply it only to
+// in-image pixels (zero padding of a conv stays 0 in z space).
+DEVI uint4 xform8(const uint4& v, const float* coef, int ld, int c, bool relu) {
+  float f[8], s[8], h[8];
+  unpack8(v, f);
+  load8f(coef + c, s);
+  load8f(coef + ld + c, h);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float o = fmaf(f[e], s[e], h[e]);
+    f[e] = relu ? fmaxf(o, 0.f) : o;
+  }
+  return pack8(f);
+}
+
+// the same with the channel coefficients already in registers
+DEVI uint4 affine8(const uint4& v, const float* s, const float* h, bool relu) {
+  float f[8];
+  unpack8(v, f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float o = fmaf(f[e], s[e], h[e]);
+    f[e] = relu ? fmaxf(o, 0.f) : o;
+  }
+  return pack8(f);
+}
+
 DEVI float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -81,11 +81,12 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
   __shared__ int s_ta[PH ? kMaxTaps : 1];
   __shared__ const uint16_t* s_x[kMaxGroups];
   __shared__ uint16_t* s_y[kMaxGroups];
+  __shared__ const float* s_xc[kMaxGroups];
   __shared__ float s_stat[WPX][2][16 * MI];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid], g.dx[tid]);
   if (PH && tid < kMaxTaps) s_ta[tid] = pa.tA[tid];
-  if (tid < kMaxGroups) { s_x[tid] = a.x[tid]; s_y[tid] = a.y[tid]; }
+  if (tid < kMaxGroups) { s_x[tid] = a.x[tid]; s_y[tid] = a.y[tid]; s_xc[tid] = a.xc[tid]; }
   __syncthreads();
 
   const long OHW = PH ? (long)pa.OHp * pa.OWp : (long)g.OH * g.OW;
@@ -128,19 +129,39 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
 
   KPos kp = kpos_init(8 * lg, g);
 
-  auto load_b = [&](uint4* B, const KPos& p) {
+  // returns the NJ-bit mask of the in-image (actually loaded) pixels: the deferred-BN prologue
+  // (xform_b, applied once the loads have landed) must leave the zero padding at 0
+  auto load_b = [&](uint4* B, const KPos& p) -> unsigned {
     const bool kval = p.t < g.T;
     const int2 d = kval ? s_tap[p.t] : make_int2(0, 0);
     const uint16_t* xb = s_x[kval ? p.gi : 0] + p.cl;
+    unsigned ok = 0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (pn[j] >= 0 && kval) {
         const int pix = in_pixel<TRANS>(pn[j], ph[j], pw[j], d, g);
-        if (pix >= 0) v = *reinterpret_cast<const uint4*>(xb + (long)pix * g.Cgi);
+        if (pix >= 0) { v = *reinterpret_cast<const uint4*>(xb + (long)pix * g.Cgi); ok |= 1u << j; }
       }
       B[j] = v;
     }
+    return ok;
+  };
+  // the prologue coefficients of a k-step are fetched together with its B loads (so their latency
+  // hides under the same MFMAs); returns 0 (no prologue), 1 (affine) or 3 (affine + ReLU)
+  auto load_coef = [&](const KPos& p, float* sc, float* sh) -> int {
+    if (PH || p.t >= g.T) return 0;
+    const float* cf = s_xc[p.gi];
+    if (cf == nullptr) return 0;
+    load8f(cf + p.cl, sc);
+    load8f(cf + g.Cgi + p.cl, sh);
+    return 1 | (int)(((a.xrelu >> p.gi) & 1u) << 1);
+  };
+  auto xform_b = [&](uint4* B, unsigned ok, int mode, const float* sc, const float* sh) {
+    if (mode == 0) return;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if ((ok >> j) & 1u) B[j] = affine8(B[j], sc, sh, mode == 3);
   };
   auto load_a = [&](uint4* A, int k0, const KPos& p) {
     if (PH) {   // the lane's 8 k sit at tap s_ta[t] of the full packed row (zero past the valid taps)
@@ -161,21 +182,30 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   uint4 A[MI], B[NJ];
+  float csc[8], csh[8];
   load_a(A, 0, kp);
-  load_b(B, kp);
+  {
+    const unsigned ok0 = load_b(B, kp);
+    const int m0 = load_coef(kp, csc, csh);
+    xform_b(B, ok0, m0, csc, csh);
+  }
   for (int k0 = 0; k0 < Kloop; k0 += 32) {
     uint4 An[MI], Bn[NJ];
+    unsigned okn = 0;
+    int mode = 0;
     const bool more = k0 + 32 < Kloop;
     if (more) {
       kpos_advance(kp, 32, g);
       load_a(An, k0 + 32, kp);
-      load_b(Bn, kp);
+      okn = load_b(Bn, kp);
+      mode = load_coef(kp, csc, csh);
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
     if (more) {
+      xform_b(Bn, okn, mode, csc, csh);   // after the MFMAs: the prefetch stays in flight under them
 #pragma unroll
       for (int i = 0; i < MI; ++i) A[i] = An[i];
 #pragma unroll
@@ -288,7 +318,12 @@ DEVI uint2 tr_read(const uint16_t* p) {
   union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
 }
 
-struct WgradPtrs { const uint16_t* dy[kMaxGroups]; const uint16_t* x[kMaxGroups]; };
+struct WgradPtrs {
+  const uint16_t* dy[kMaxGroups];
+  const uint16_t* x[kMaxGroups];
+  const float* xc[kMaxGroups];   // deferred-BN prologue of the x groups (see ConvArgs::xc)
+  unsigned xrelu;
+};
 
 template <int CO_T, int K_T, bool TRANS>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g, int KT) {
@@ -323,8 +358,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
   const int2 btap = make_int2(g.dy[bp.t], g.dx[bp.t]);
   const uint16_t* b_base = P.x[bp.gi] + bp.cl;
   const int IHW = g.IH * g.IW;
+  // deferred-BN prologue: this thread's 8 x channels are fixed -> coefficients once, in registers
+  const float* bcf = b_valid ? P.xc[bp.gi] : nullptr;
+  const bool brelu = (P.xrelu >> bp.gi) & 1u;
+  float bsc[8], bsh[8];
+  if (bcf != nullptr) { load8f(bcf + bp.cl, bsc); load8f(bcf + g.Cgi + bp.cl, bsh); }
 
   uint4 ra[A_V], rb[B_V];
+  unsigned rbok = 0;   // in-image B rows of the staged chunk (the prologue leaves padding at 0)
   auto load = [&](long c) {
     const long mb = c * WG_M;
 #pragma unroll
@@ -334,6 +375,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
       if (m < M && a_valid) val = *reinterpret_cast<const uint4*>(a_base + m * g.Cgo);
       ra[v] = val;
     }
+    rbok = 0;
 #pragma unroll
     for (int v = 0; v < B_V; ++v) {
       const long m = mb + b_r + B_RS * v;
@@ -344,7 +386,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
         const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
         const int pix = TRANS ? in_pixel<true>(n * IHW, oh, ow, btap, g)
                               : in_pixel<false>(n * IHW, oh * g.stride, ow * g.stride, btap, g);
-        if (pix >= 0) val = *reinterpret_cast<const uint4*>(b_base + (long)pix * g.Cgi);
+        if (pix >= 0) { val = *reinterpret_cast<const uint4*>(b_base + (long)pix * g.Cgi); rbok |= 1u << v; }
       }
       rb[v] = val;
     }
@@ -366,7 +408,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
 #pragma unroll
     for (int v = 0; v < A_V; ++v) *reinterpret_cast<uint4*>(&sA[(a_r + A_RS * v) * SA_LD + 8 * a_c8]) = ra[v];
 #pragma unroll
-    for (int v = 0; v < B_V; ++v) *reinterpret_cast<uint4*>(&sB[(b_r + B_RS * v) * SB_LD + 8 * b_c8]) = rb[v];
+    for (int v = 0; v < B_V; ++v) {
+      uint4 val = rb[v];
+      if (bcf != nullptr && ((rbok >> v) & 1u)) val = affine8(val, bsc, bsh, brelu);
+      *reinterpret_cast<uint4*>(&sB[(b_r + B_RS * v) * SB_LD + 8 * b_c8]) = val;
+    }
     __syncthreads();
     if (c + gridDim.z < nchunks) load(c + gridDim.z);     // next chunk in flight during the MFMAs
     uint4 fa[FI];
@@ -474,6 +520,15 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   const bool x_ok = xci < Cip;
   const int x_g = x_ok ? xci / g.Cgi : 0;
   const uint16_t* x_base = P.x[x_g] + (xci - x_g * g.Cgi);
+  // deferred-BN prologue of the halo: the thread's 8 channels are fixed -> coefficients in registers
+  const float* x_cf = x_ok ? P.xc[x_g] : nullptr;
+  const bool x_relu = (P.xrelu >> x_g) & 1u;
+  float x_sc[8], x_sh[8];
+  if (x_cf != nullptr) {
+    const int x_ch = xci - x_g * g.Cgi;
+    load8f(x_cf + x_ch, x_sc);
+    load8f(x_cf + g.Cgi + x_ch, x_sh);
+  }
   __syncthreads();
 
   // lane pixel within a 32-pixel slice: lo = 8*lg + q, hi = lo + 4 (tile coords: row ry, column cx)
@@ -518,6 +573,7 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   // vp + 128*(u&1)); the other slots walk the halo.
   uint4 sv[NST];
   int sd[NST];
+  unsigned sx = 0;   // staged halo slots that hold in-image pixels (get the BN prologue)
   auto stage_load = [&](long tix) {
     const int per_img = tl.tiles_y * tl.tiles_x;
     const int n = (int)(tix / per_img);
@@ -525,6 +581,7 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
     const int y0 = (rem / tl.tiles_x) * tl.TH, x0 = (rem % tl.tiles_x) * tl.TW;
     const long yoff = (long)n * g.OH * g.OW * g.Cgo;
     const uint16_t* xim = x_base + (long)n * g.IH * g.IW * g.Cgi;
+    sx = 0;
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
       sv[u] = make_uint4(0, 0, 0, 0);
@@ -541,8 +598,10 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
           const int hy = fdiv(hp, tl.HWv, tl.inv_hwv), hx = hp - __mul24(hy, tl.HWv);
           const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
           sd[u] = NCB * SUB + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
-          if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW)
+          if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
             sv[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
+            sx |= 1u << u;
+          }
         }
       }
     }
@@ -551,8 +610,12 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   for (long tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
     __syncthreads();   // previous tile's LDS reads are done
 #pragma unroll
-    for (int u = 0; u < NST; ++u)
-      if (sd[u] >= 0) *reinterpret_cast<uint4*>(&sY[sd[u]]) = sv[u];
+    for (int u = 0; u < NST; ++u) {
+      if (sd[u] < 0) continue;
+      uint4 v = sv[u];
+      if (x_cf != nullptr && ((sx >> u) & 1u)) v = affine8(v, x_sc, x_sh, x_relu);
+      *reinterpret_cast<uint4*>(&sY[sd[u]]) = v;
+    }
     __syncthreads();
     if (tix + gridDim.x < ntiles) stage_load(tix + gridDim.x);   // in flight during the MFMAs
     for (int sl = 0; sl < NSL; ++sl) {
@@ -675,6 +738,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restri
 // Waves split the tile's pixels (NJ 16-pixel columns each) and loop over the 16*MI-row groups.
 struct HaloGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
+  int xtab;                          // deferred-BN prologue present: LDS coefficient table (3 x Cip fp32)
   float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
 };
 
@@ -682,6 +746,7 @@ constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel
 constexpr int kHaloWaves = 4;
 constexpr int kHaloMaxRows = 512;
 constexpr int kHaloLd = 8;       // 16-B loads in flight per thread while staging
+constexpr int kHaloMaxLds = 96 * 1024;   // tile (<= 64 KB by geometry) + stats + prologue table
 
 // K is walked in UNITS of (tap t, 8 channels c8) -- the lane group lg of k-step ks takes unit
 // 4*ks + lg.  Per unit: A offset t*Cip + 8*c8 (+ chunk base) into the packed weight row, B offset
@@ -706,6 +771,19 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
   const int hpx = hg.HH * hg.HWD;
   // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
   float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
+  // deferred-BN prologue table after them (hg.xtab): per input channel scale, shift and the ReLU floor
+  // (0 or -inf); groups without a prologue get the identity (exact on bf16 values)
+  float* s_coef = s_stat + kHaloWaves * 2 * rows;
+  if (!BNE && hg.xtab) {
+    for (int c = tid; c < Cip; c += 64 * kHaloWaves) {
+      const int gi = c / g.Cgi, cl = c - gi * g.Cgi;
+      const float* cf = a.xc[gi];
+      s_coef[c] = cf != nullptr ? cf[cl] : 1.f;
+      s_coef[Cip + c] = cf != nullptr ? cf[g.Cgi + cl] : 0.f;
+      s_coef[2 * Cip + c] = (cf != nullptr && ((a.xrelu >> gi) & 1u)) ? 0.f : -INFINITY;
+    }
+    __syncthreads();   // read by the first staging pass, before any other barrier
+  }
 
   // XCD-aware bijective remap: neighbouring tiles (shared halo rows) land on one XCD's L2.
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -750,6 +828,30 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
     for (int u = 0; u < kHaloLd; ++u)
       if (dst[u] >= 0) *reinterpret_cast<uint4*>(tile + dst[u]) = v[u];
   };
+  // Deferred-BN prologue as its own pass over the staged chunk (after the barrier that published it):
+  // every in-image vector is normalised (+ReLU) in place from the LDS table, the zero padding is left
+  // alone.  Kept out of load/store_batch: temporaries there stay live into the MFMA loop and spill.
+  auto xform_pass = [&](int c0) {
+    for (int idx = tid; idx < total; idx += 64 * kHaloWaves) {
+      const int hp = fdiv(idx, C8c, hg.inv_c8), c8 = idx - __mul24(hp, C8c);
+      const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
+      const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
+      if ((unsigned)iy >= (unsigned)g.IH || (unsigned)ix >= (unsigned)g.IW) continue;
+      uint4* tp = reinterpret_cast<uint4*>(tile + __mul24(hp, hg.pitch) + c8 * 8);
+      const float* cp = s_coef + c0 + c8 * 8;
+      const float4 s0 = *reinterpret_cast<const float4*>(cp), s1 = *reinterpret_cast<const float4*>(cp + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(cp + Cip), h1 = *reinterpret_cast<const float4*>(cp + Cip + 4);
+      const float4 l0 = *reinterpret_cast<const float4*>(cp + 2 * Cip);
+      const float4 l1 = *reinterpret_cast<const float4*>(cp + 2 * Cip + 4);
+      float f[8];
+      unpack8(*tp, f);
+      f[0] = fmaxf(fmaf(f[0], s0.x, h0.x), l0.x); f[1] = fmaxf(fmaf(f[1], s0.y, h0.y), l0.y);
+      f[2] = fmaxf(fmaf(f[2], s0.z, h0.z), l0.z); f[3] = fmaxf(fmaf(f[3], s0.w, h0.w), l0.w);
+      f[4] = fmaxf(fmaf(f[4], s1.x, h1.x), l1.x); f[5] = fmaxf(fmaf(f[5], s1.y, h1.y), l1.y);
+      f[6] = fmaxf(fmaf(f[6], s1.z, h1.z), l1.z); f[7] = fmaxf(fmaf(f[7], s1.w, h1.w), l1.w);
+      *tp = pack8(f);
+    }
+  };
 
   for (int e = tid; e < hg.KS * 4; e += 64 * kHaloWaves) {
     int ua = -1, ub = 0;
@@ -792,6 +894,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
         store_batch(pv, pd);
         __syncthreads();
         if (ch + 1 < hg.nch) load_batch(c0 + hg.CC, tid, pv, pd);   // in flight during the MFMAs
+        if (!BNE && hg.xtab) {   // prologues are forward-only, BNE data-gradient-only
+          xform_pass(c0);
+          __syncthreads();
+        }
       } else if (rg == 0) {
         for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
           uint4 v[kHaloLd];
@@ -800,6 +906,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
           store_batch(v, dst);
         }
         __syncthreads();
+        if (!BNE && hg.xtab) {
+          xform_pass(0);
+          __syncthreads();
+        }
       }
       auto load_a = [&](uint4* A, int ks) {
         if (CHUNKED) {
@@ -1145,21 +1255,33 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   HaloGeom hg;
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
     const unsigned blocks = (unsigned)((long)a.g.N * hg.tiles_y * hg.tiles_x);
-    const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo);
-    // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers
+    hg.xtab = 0;
+    for (int i = 0; i < a.g.Gi; ++i) hg.xtab |= a.xc[i] != nullptr;
+    if (hg.xtab && a.bn_y != nullptr) abort();   // BN prologue (forward) and BN epilogue (dgrad) never meet
+    const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) + (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0);
+    // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers.
+    // The prologue table may take the dynamic LDS past 64 KB: opted into once per instantiation,
+    // before any graph capture (the first call of every shape runs eagerly).
+#define HC_LAUNCH_(K_)                                                                                       \
+    {                                                                                                        \
+      static bool lds_attr = false;                                                                          \
+      if (!lds_attr) {                                                                                       \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&K_), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  kHaloMaxLds);                                                              \
+        lds_attr = true;                                                                                     \
+      }                                                                                                      \
+      hipLaunchKernelGGL((K_), dim3(blocks), dim3(64 * kHaloWaves), lds, s, a, hg);                         \
+    }
 #define HC_(MI_, BNE_)                                                                                       \
     if (mi == MI_ && bne == BNE_) {                                                                          \
-      if (hg.nch > 1)                                                                                        \
-        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>), dim3(blocks),           \
-                           dim3(64 * kHaloWaves), lds, s, a, hg);                                           \
-      else                                                                                                   \
-        hipLaunchKernelGGL((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>), dim3(blocks),          \
-                           dim3(64 * kHaloWaves), lds, s, a, hg);                                           \
+      if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))                  \
+      else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>))                             \
       return;                                                                                                \
     }
     const bool bne = a.bn_y != nullptr;
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
 #undef HC_
+#undef HC_LAUNCH_
   }
   const int nj = conv_pick_nj(a.g, mi);
   const int wpx = conv_pick_wpx(a.g, mi, nj);
@@ -1205,12 +1327,14 @@ int conv_wgrad_replicas(const ConvGeom& g, bool trans) {
 }
 
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-                hipStream_t s) {
+                const float* const* xc, unsigned xrelu, hipStream_t s) {
   const int KT = g.T * g.Gi * g.Cgi;
   const int rows = g.Go * g.Cgo;
   WgradPtrs P{};
   for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
   for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
+  for (int i = 0; i < g.Gi; ++i) P.xc[i] = xc != nullptr ? xc[i] : nullptr;
+  P.xrelu = xrelu;
   const int nrep = conv_wgrad_replicas(g, trans);
   (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT * nrep, s);
   DwTile tl{};

@@ -47,7 +47,8 @@ __global__ void nhwc_to_nchw_kernel(const uint16_t* __restrict__ x, float* __res
 }
 
 __global__ void up2_add_kernel(const uint16_t* __restrict__ low, const uint16_t* __restrict__ skip,
-                               uint16_t* __restrict__ out, int N, int h, int w, int Cp) {
+                               uint16_t* __restrict__ out, int N, int h, int w, int Cp, const float* __restrict__ lc,
+                               int lrelu, const float* __restrict__ sc, int srelu) {
   const int CG = Cp / 8, H = 2 * h, W = 2 * w;
   const long total = (long)N * H * W * CG;
   for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
@@ -58,8 +59,12 @@ __global__ void up2_add_kernel(const uint16_t* __restrict__ low, const uint16_t*
     const int Y = (int)(pix % H);
     const long n = pix / H;
     float a[8], b[8];
-    unpack8(*reinterpret_cast<const uint4*>(skip + i * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(low + ((n * h + (Y >> 1)) * w + (X >> 1)) * Cp + 8 * g), b);
+    uint4 va = *reinterpret_cast<const uint4*>(skip + i * 8);
+    uint4 vb = *reinterpret_cast<const uint4*>(low + ((n * h + (Y >> 1)) * w + (X >> 1)) * Cp + 8 * g);
+    if (sc != nullptr) va = xform8(va, sc, Cp, 8 * g, srelu != 0);   // deferred-BN prologues
+    if (lc != nullptr) vb = xform8(vb, lc, Cp, 8 * g, lrelu != 0);
+    unpack8(va, a);
+    unpack8(vb, b);
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] += b[e];
     *reinterpret_cast<uint4*>(out + i * 8) = pack8(a);
@@ -91,15 +96,21 @@ __global__ void pool2_sum_kernel(const uint16_t* __restrict__ gr, uint16_t* __re
   }
 }
 
-struct Ptrs { const uint16_t* p[kMaxSumInputs]; };
+struct Ptrs { const uint16_t* p[kMaxSumInputs]; const float* c[kMaxSumInputs]; unsigned relu; };
 
-__global__ void add_n_kernel(Ptrs in, int k, uint16_t* __restrict__ out, long nvec) {
+DEVI uint4 load_vec(const Ptrs& in, int j, long i, int CG) {
+  uint4 v = *reinterpret_cast<const uint4*>(in.p[j] + i * 8);
+  if (in.c[j] != nullptr) v = xform8(v, in.c[j], 8 * CG, 8 * (int)(i % CG), (in.relu >> j) & 1u);
+  return v;
+}
+
+__global__ void add_n_kernel(Ptrs in, int k, uint16_t* __restrict__ out, long nvec, int CG) {
   for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
     float a[8];
-    unpack8(*reinterpret_cast<const uint4*>(in.p[0] + i * 8), a);
+    unpack8(load_vec(in, 0, i, CG), a);
     for (int j = 1; j < k; ++j) {
       float b[8];
-      unpack8(*reinterpret_cast<const uint4*>(in.p[j] + i * 8), b);
+      unpack8(load_vec(in, j, i, CG), b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
     }
@@ -123,9 +134,11 @@ void nhwc_to_nchw(const uint16_t* x, float* y, int N, int C, int H, int W, int C
   hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, x, y, N, C, (long)H * W, Cp);
 }
 
-void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s) {
+void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cp,
+             const float* lc, int lrelu, const float* sc, int srelu, hipStream_t s) {
   const long total = (long)N * 4 * h * w * (Cp / 8);
-  hipLaunchKernelGGL(up2_add_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, low, skip, out, N, h, w, Cp);
+  hipLaunchKernelGGL(up2_add_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, low, skip, out, N, h, w, Cp, lc, lrelu,
+                     sc, srelu);
 }
 
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s) {
@@ -133,11 +146,16 @@ void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hi
   hipLaunchKernelGGL(pool2_sum_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, g, out, N, h, w, Cp);
 }
 
-void add_n(const uint16_t* const* inputs, int k, uint16_t* out, long n_elem, hipStream_t s) {
+void add_n(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
+           long n_elem, int Cp, hipStream_t s) {
   Ptrs in{};
-  for (int i = 0; i < k; ++i) in.p[i] = inputs[i];
+  for (int i = 0; i < k; ++i) {
+    in.p[i] = inputs[i];
+    in.c[i] = coefs != nullptr ? coefs[i] : nullptr;
+  }
+  in.relu = relu_mask;
   const long nvec = n_elem / 8;
-  hipLaunchKernelGGL(add_n_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, in, k, out, nvec);
+  hipLaunchKernelGGL(add_n_kernel, dim3(grid_for(nvec)), dim3(kBlock), 0, s, in, k, out, nvec, Cp / 8);
 }
 
 void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s) {

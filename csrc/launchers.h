@@ -37,6 +37,11 @@ struct ConvArgs {
   const uint16_t* bn_y;  // nullable: that BN's input y, [N, OH, OW, Cgo]
   const float* bn_coef;  // [3][Cgo]: scale, shift, mean
   int bn_relu;
+  // Deferred-BN input prologue (forward / weight-gradient of a conv whose input group i is the output
+  // of a training- or eval-mode BatchNorm(+ReLU) that was never materialised): xc[i] = that BN's
+  // [4][Cgi] stats (scale row 0, shift row 1) or nullptr; bit i of xrelu = the BN's ReLU.
+  const float* xc[kMaxGroups];
+  unsigned xrelu;
   ConvGeom g;
 };
 
@@ -50,8 +55,9 @@ long conv_stat_blocks(const ConvGeom& g);
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
 int conv_wgrad_replicas(const ConvGeom& g, bool trans);
+// xc / xrelu: the deferred-BN prologue of the x groups (see ConvArgs; xc may be nullptr)
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-                hipStream_t s);
+                const float* const* xc, unsigned xrelu, hipStream_t s);
 // dst[row][(t_base + t)*Cpk + c_base + c] = src[row*s_row + c*s_ch + t], row < nrow, c < nch, t < T
 void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base,
                  int c_base, long s_row, long s_ch, hipStream_t s);
@@ -66,8 +72,10 @@ void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cp
 // bn.hip  (P = number of pixels, Cp = padded channels; partial buffers are [nblk][2][Cp] fp32)
 constexpr int kMaxSumInputs = 8;
 long bn_partial_blocks(long P, int Cp);
-void sum_stats(const uint16_t* const* inputs, int k, uint16_t* out, float* part, long P, int Cp,
-               hipStream_t s);
+// coefs[i] (nullable array / entries): deferred-BN prologue of input i (stats rows, ld = Cp), bit i of
+// relu_mask its ReLU -- the branch sums that feed a BN read the branches' pre-BN tensors directly.
+void sum_stats(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
+               float* part, long P, int Cp, hipStream_t s);
 // Channel reductions of [nblk][2][width] partials (columns col_off .. col_off+Cp) into an fp64
 // workspace tmp[S][2*Cp], S = bn_reduce_splits(nblk); the finalize kernels sum the S rows themselves.
 // bn_collapse sums them into out[2*Cp] (fp64) -- the SyncBN path all-reduces that buffer (S = 1).
@@ -98,10 +106,13 @@ void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale,
 // elementwise.hip
 void nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t s);
 void nhwc_to_nchw(const uint16_t* x, float* y, int N, int C, int H, int W, int Cp, hipStream_t s);
+// lc / sc (nullable): deferred-BN prologues of low / skip (stats rows, ld = Cp)
 void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, int h, int w, int Cp,
-             hipStream_t s);
+             const float* lc, int lrelu, const float* sc, int srelu, hipStream_t s);
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s);
-void add_n(const uint16_t* const* inputs, int k, uint16_t* out, long n_elem, hipStream_t s);
+// coefs (nullable): deferred-BN prologue per input (ld = Cp, the channel width of every input)
+void add_n(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
+           long n_elem, int Cp, hipStream_t s);
 void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s);
 
 // pool.hip  (NHWC bf16; idx = one byte per element = winning tap r*k+c)

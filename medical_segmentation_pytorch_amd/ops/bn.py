@@ -50,6 +50,64 @@ class BNState:
                        bn.num_batches_tracked)
 
 
+class Deferred:
+    """A BatchNorm(+ReLU) output that is never materialised: ``z = act(stats[0] * t + stats[1])``
+    per channel.  ``t`` is an autograd alias of the BN's input ``y`` whose gradient is dL/dz; every
+    consumer kernel applies the affine+ReLU while it loads ``t`` (the "BN prologue": conv halo/igemm
+    staging, weight-gradient staging, branch sums), so no ``bn_act_apply`` pass ever writes ``z``.
+    :func:`materialize` turns it into a plain tensor for consumers without a prologue."""
+    __slots__ = ('t', 'stats', 'relu')
+
+    def __init__(self, t, stats, relu):
+        self.t, self.stats, self.relu = t, stats, relu
+
+    @property
+    def shape(self):
+        return self.t.shape
+
+    @property
+    def device(self):
+        return self.t.device
+
+
+def split_inputs(xs):
+    """(tensors, prologue coefficient list or [], relu bitmask) of a list of Tensor | Deferred."""
+    ts, cs, mask = [], [], 0
+    for i, x in enumerate(xs):
+        if isinstance(x, Deferred):
+            ts.append(x.t.contiguous())
+            cs.append(x.stats)
+            mask |= int(bool(x.relu)) << i
+        else:
+            ts.append(x.contiguous())
+            cs.append(None)
+    if all(c is None for c in cs):
+        cs = []
+    return ts, cs, mask
+
+
+class _Materialize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t, stats, relu):
+        C = require()
+        t = t.contiguous()
+        Cp = t.shape[-1]
+        z = torch.empty_like(t)
+        C.bn_act_apply(t, stats, z, t.numel() // Cp, Cp, relu)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):   # z and the alias t are the same logical tensor
+        return dz, None, None
+
+
+def materialize(x):
+    """Plain NHWC tensor of ``x`` (Deferred -> one bn_act_apply pass; tensors pass through)."""
+    if isinstance(x, Deferred):
+        return _Materialize.apply(x.t, x.stats, x.relu)
+    return x
+
+
 class BwdStatsHandle:
     """Links a training-mode BN output ``z`` that exactly ONE stride-1 conv reads (nothing else) to
     that conv: the conv's data-gradient launch -- whose output is dL/dz -- also emits the BN backward's
@@ -95,12 +153,15 @@ def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev):
 
 
 class _BNAct(torch.autograd.Function):
-    # inputs: st, relu, training, part_info, gamma, beta, *xs  (gamma/beta are inputs so that their
-    # grads reach autograd when the engine gives no grad sink)
+    # inputs: st, relu, training, part_info, handle, deferred, pro, gamma, beta, *xs  (gamma/beta are
+    # inputs so that their grads reach autograd when the engine gives no grad sink).  pro = (coefs,
+    # relu mask): inputs that are themselves Deferred BN outputs (their prologue runs in sum_stats).
+    # deferred: return the alias of y (the caller wraps it in a Deferred) instead of materialising z.
     @staticmethod
-    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, gamma, beta, *xs):
+    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, deferred, pro, gamma, beta, *xs):
         C = require()
         xs = [x.contiguous() for x in xs]
+        coefs, rmask = pro
         y0 = xs[0]
         Cp = y0.shape[-1]
         P = y0.numel() // Cp
@@ -108,15 +169,16 @@ class _BNAct(torch.autograd.Function):
         stats = torch.empty(4, Cp, dtype=torch.float32, device=dev)
         g_ = gamma.detach() if gamma is not None else None
         b_ = beta.detach() if beta is not None else None
-        y = torch.empty_like(y0) if len(xs) > 1 else y0
+        summed = len(xs) > 1 or bool(coefs)   # y must be written: a sum, or a transformed input
+        y = torch.empty_like(y0) if summed else y0
         if training:
-            if part_info is not None and len(xs) == 1:
+            if part_info is not None and not summed:
                 part, width, col_off = part_info
                 nblk = part.shape[0]
             else:
                 nblk = C.bn_partial_blocks(P, Cp)
                 part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
-                C.sum_stats(xs, y if len(xs) > 1 else None, part, P, Cp)
+                C.sum_stats(xs, y if summed else None, part, P, Cp, coefs, rmask)
                 width, col_off = Cp, 0
             world = _world(st.group)
             count = float(P * world)
@@ -131,23 +193,26 @@ class _BNAct(torch.autograd.Function):
             if st.count_nbt and st.num_batches_tracked is not None:
                 st.num_batches_tracked.add_(1)
         else:
-            if len(xs) > 1:
-                C.add_n(xs, y)
+            if summed:
+                C.add_n(xs, y, coefs, rmask)
             sums = torch.zeros(1, 2 * Cp, dtype=torch.float64, device=dev)
             C.bn_finalize(sums, st.C, Cp, 1.0, g_, b_, st.running_mean, st.running_var, st.momentum,
                           st.eps, False, stats)
             count = float(P)
-        z = torch.empty_like(y)
-        C.bn_act_apply(y, stats, z, P, Cp, relu)
         ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
         ctx.handle = handle if training else None
         if ctx.handle is not None:
             handle.y, handle.stats, handle.relu, handle.part = y, stats, relu, None
         ctx.save_for_backward(y, stats)
-        return z
+        ctx.mark_non_differentiable(stats)
+        if deferred:
+            return y, stats
+        z = torch.empty_like(y)
+        C.bn_act_apply(y, stats, z, P, Cp, relu)
+        return z, stats
 
     @staticmethod
-    def backward(ctx, dz):
+    def backward(ctx, dz, _dstats=None):
         C = require()
         y, stats = ctx.saved_tensors
         st: BNState = ctx.st
@@ -166,8 +231,8 @@ class _BNAct(torch.autograd.Function):
         world = _world(st.group) if ctx.training else 1
         fused = ctx.training and world == 1
         sums = None if fused else _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
-        need_g = ctx.needs_input_grad[5] and st.weight_sink is None
-        need_b = ctx.needs_input_grad[6] and st.bias_sink is None
+        need_g = ctx.needs_input_grad[7] and st.weight_sink is None
+        need_b = ctx.needs_input_grad[8] and st.bias_sink is None
         dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
         dbeta = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_b else None
         g_t = st.weight_sink if st.weight_sink is not None else dgamma
@@ -193,17 +258,21 @@ class _BNAct(torch.autograd.Function):
         C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
         if st.ready_hook is not None:
             st.ready_hook([t for t in (st.weight, st.bias) if t is not None])
-        return (None, None, None, None, None,
+        return (None, None, None, None, None, None, None,
                 dgamma[:st.C] if dgamma is not None else None,
                 dbeta[:st.C] if dbeta is not None else None) + (dy,) * ctx.k
 
 
-def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None):
-    """act(BN(sum(xs))) for NHWC bf16 feature maps.  ``part_info = (part, width, col_off)`` reuses
-    conv-epilogue channel partials (single input only); ``handle``: see :class:`BwdStatsHandle`."""
-    if isinstance(xs, torch.Tensor):
+def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None, deferred=False):
+    """act(BN(sum(xs))) for NHWC bf16 feature maps (``xs``: tensors and/or :class:`Deferred` BN
+    outputs).  ``part_info = (part, width, col_off)`` reuses conv-epilogue channel partials (single
+    plain input only); ``handle``: see :class:`BwdStatsHandle`.  ``deferred=True`` returns a
+    :class:`Deferred` (no normalise pass) -- only for callers whose consumers all take prologues."""
+    if isinstance(xs, (torch.Tensor, Deferred)):
         xs = [xs]
-    return _BNAct.apply(st, relu, training, part_info, handle, st.weight, st.bias, *xs)
+    ts, coefs, mask = split_inputs(xs)
+    out, stats = _BNAct.apply(st, relu, training, part_info, handle, deferred, (coefs, mask), st.weight, st.bias, *ts)
+    return Deferred(out, stats, relu) if deferred else out
 
 
 # ------------------------------------------------------------------------------------------------

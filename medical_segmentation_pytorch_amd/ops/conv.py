@@ -193,10 +193,13 @@ def _taps(tl):
 
 
 class _ConvFn(torch.autograd.Function):
+    # pro = (coefs, relu mask): deferred-BN prologue of the input groups (ops.bn.Deferred); the same
+    # prologue runs again in the weight-gradient staging, so z never exists in HBM
     @staticmethod
-    def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, bn_handle, *args):
+    def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, bn_handle, pro, *args):
         C = require()
         xs = [a.contiguous() for a in args[:nx]]
+        coefs, rmask = pro
         n, ih, iw, _ = xs[0].shape
         oh, ow = plan.out_hw(ih, iw)
         dev = xs[0].device
@@ -214,9 +217,10 @@ class _ConvFn(torch.autograd.Function):
             nblk = C.conv_stat_blocks(dims, dy, dx)
             part = torch.empty(nblk, 2, plan.rows, dtype=torch.float32, device=dev)
         bias = plan.bias.detach().float().contiguous() if plan.bias is not None else None
-        C.conv_fwd(xs, wp, ys, bias, part, dims, dy, dx, trans)
+        C.conv_fwd(xs, wp, ys, bias, part, dims, dy, dx, trans, coefs, rmask)
         ctx.plan = plan
         ctx.nx = nx
+        ctx.pro = pro
         ctx.bn_handle = bn_handle if (bn_handle is not None and plan.stride == 1 and not plan.transposed
                                       and plan.Gi == 1) else None
         ctx.shape = (n, ih, iw, oh, ow)
@@ -238,7 +242,7 @@ class _ConvFn(torch.autograd.Function):
             gys.append(torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None
                        else g.contiguous())
         dxs = [None] * ctx.nx
-        if any(ctx.needs_input_grad[4:4 + ctx.nx]):
+        if any(ctx.needs_input_grad[5:5 + ctx.nx]):
             wd, Kp_d = plan.pack_dgrad(dev)
             dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
             dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
@@ -257,7 +261,7 @@ class _ConvFn(torch.autograd.Function):
                 h.part = part
             else:
                 C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
-        wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev)
+        wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev, ctx.pro)
         bgrad = None
         if plan.bias is not None:
             bg = gys[0].view(-1, plan.Cgo)[:, :plan.co_l].float().sum(0)
@@ -267,15 +271,16 @@ class _ConvFn(torch.autograd.Function):
                 bgrad = bg
         if plan.ready_hook is not None:
             plan.ready_hook([b.weight for b in plan.branches] + ([plan.bias] if plan.bias is not None else []))
-        # inputs of forward: plan, want_stats, nx, bn_handle, *xs, *weights, bias
-        out = [None, None, None, None] + dxs + wgrads
+        # inputs of forward: plan, want_stats, nx, bn_handle, pro, *xs, *weights, bias
+        out = [None, None, None, None, None] + dxs + wgrads
         if plan.bias is not None:
             out.append(bgrad)
         return tuple(out)
 
 
-def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
+def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0)):
     C = require()
+    coefs, rmask = pro
     n, ih, iw, oh, ow = shape
     res = []
     need = [b.weight.requires_grad for b in plan.branches]
@@ -287,6 +292,7 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
         Kp_w = round_up(plan.T * plan.Cgo, 32)
         dims = [n, oh, ow, 1, plan.Cgo, ih, iw, 1, plan.Cgi, plan.ci_l, plan.T, Kp_w, plan.stride]
         dy, dx = _taps(plan.taps_fwd)
+        assert not coefs, 'transposed convs take materialised inputs'
         dwp = torch.empty(plan.Cgi * plan.T * plan.Cgo, dtype=torch.float32, device=dev)
         C.conv_wgrad(xs, gys, dwp, dims, dy, dx, False)
         dst = b.sink if b.sink is not None else torch.zeros_like(b.weight, dtype=torch.float32)
@@ -298,7 +304,7 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
     KT = plan.T * plan.Cip
     nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # atomic-spreading dW replicas, summed on unpack
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
-    C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False)
+    C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask)
     cin_tot = plan.Gi * plan.ci_l
     for b, nd in zip(plan.branches, need):
         if not nd:
@@ -315,14 +321,20 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev):
 
 
 def conv(plan: ConvPlan, xs, want_stats=False, bn_handle=None):
-    """Run ``plan`` on input group tensors ``xs``; returns (list of Go output tensors, stat partials).
-    ``bn_handle``: the input is a BN output read by this conv only (see ``ops.bn.BwdStatsHandle``)."""
-    if isinstance(xs, torch.Tensor):
+    """Run ``plan`` on input groups ``xs`` (tensors or ``ops.bn.Deferred`` BN outputs, whose
+    normalise+ReLU runs as this conv's load prologue); returns (list of Go output tensors, stat
+    partials).  ``bn_handle``: the input is a BN output read by this conv only
+    (see ``ops.bn.BwdStatsHandle``)."""
+    from .bn import materialize, split_inputs
+    if not isinstance(xs, (list, tuple)):
         xs = [xs]
     assert len(xs) == plan.Gi
+    if plan.transposed:
+        xs = [materialize(x) for x in xs]
+    ts, coefs, mask = split_inputs(xs)
     weights = [b.weight for b in plan.branches]
     extra = [plan.bias] if plan.bias is not None else []
-    out = _ConvFn.apply(plan, want_stats, len(xs), bn_handle, *xs, *weights, *extra)
+    out = _ConvFn.apply(plan, want_stats, len(ts), bn_handle, (coefs, mask), *ts, *weights, *extra)
     return list(out[:plan.Go]), (out[plan.Go] if want_stats else None)
 
 

@@ -53,16 +53,16 @@ class _FromFM(torch.autograd.Function):
 
 
 class _Up2Add(torch.autograd.Function):
-    """nearest-2x(low) + skip  (reference models/ducknet.py:82-84)."""
+    """nearest-2x(low) + skip  (reference models/ducknet.py:82-84); pro = deferred-BN prologues."""
 
     @staticmethod
-    def forward(ctx, low, skip):
+    def forward(ctx, pro, low, skip):
         C = require()
         low, skip = low.contiguous(), skip.contiguous()
         n, h, w, cp = low.shape
         assert skip.shape == (n, 2 * h, 2 * w, cp), (low.shape, skip.shape)
         out = torch.empty_like(skip)
-        C.up2_add(low, skip, out, n, h, w, cp)
+        C.up2_add(low, skip, out, n, h, w, cp, pro[0], pro[1])
         ctx.shape = (n, h, w, cp)
         return out
 
@@ -73,22 +73,22 @@ class _Up2Add(torch.autograd.Function):
         g = g.contiguous()
         dlow = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=g.device)
         C.pool2_sum(g, dlow, n, h, w, cp)
-        return dlow, g
+        return None, dlow, g
 
 
 class _AddN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, *xs):
+    def forward(ctx, pro, *xs):
         C = require()
         xs = [x.contiguous() for x in xs]
         out = torch.empty_like(xs[0])
-        C.add_n(xs, out)
+        C.add_n(xs, out, pro[0], pro[1])
         ctx.k = len(xs)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        return (g,) * ctx.k
+        return (None,) + (g,) * ctx.k
 
 
 def to_fm(x):
@@ -100,8 +100,16 @@ def from_fm(fm, c):
 
 
 def up2_add(low, skip):
-    return _Up2Add.apply(low, skip)
+    """``low``/``skip``: tensors or ``ops.bn.Deferred`` (normalise+ReLU applied while loading)."""
+    from .bn import split_inputs
+    (lt, st), coefs, mask = split_inputs([low, skip])
+    return _Up2Add.apply((coefs, mask), lt, st)
 
 
 def add_n(*xs):
-    return xs[0] if len(xs) == 1 else _AddN.apply(*xs)
+    """Elementwise sum of tensors / ``ops.bn.Deferred`` BN outputs (always a plain tensor)."""
+    from .bn import materialize, split_inputs
+    if len(xs) == 1:
+        return materialize(xs[0])
+    ts, coefs, mask = split_inputs(xs)
+    return _AddN.apply((coefs, mask), *ts)

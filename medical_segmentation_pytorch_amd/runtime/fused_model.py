@@ -3,8 +3,11 @@ drives the HIP kernels with the modules' own parameters (so ``state_dict`` / che
 reference's), keeping every activation NHWC bf16 on the device.
 
 What is fused relative to the module graph (reference ``models/ducknet.py``, ``models/unet.py``):
-  * every ConvBNAct = 1 implicit-GEMM conv launch whose epilogue emits the BN channel partials,
-    + finalize + one normalize/ReLU pass (no separate statistics read);
+  * every ConvBNAct = 1 implicit-GEMM conv launch whose epilogue emits the BN channel partials
+    + one reduce/finalize launch; the normalize+ReLU never runs as a pass of its own: the BN output
+    stays *deferred* (``ops.bn.Deferred``) and every consumer -- the next conv's halo/igemm staging,
+    its weight-gradient staging, the branch sums feeding the next BN, the decoder up2+add -- applies
+    scale/shift/ReLU while loading the pre-BN tensor (SURVEY §7.2 "BN-apply+ReLU prologue");
   * DUCK (``ducknet.py:113-154``): the five 3x3 first convs and the three 1x1 residual shortcuts
     that all read ``in_bn(x)`` are ONE GEMM with 8 output groups (Cout = 8*C), so the input is read
     once and the data-gradient of all eight is a single launch that sums them for free;
@@ -21,7 +24,7 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BNState, BwdStatsHandle, bn_act
+from ..ops.bn import BNState, BwdStatsHandle, Deferred, bn_act, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
@@ -132,21 +135,22 @@ class FusedExecutor:
 
     # -- single-consumer BN outputs ------------------------------------------------------------------
     def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
-        """bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
+        """Deferred bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
         h = BwdStatsHandle() if (single and training and _BN_EPILOGUE) else None
-        z = bn_act(xs, st, relu, training, part_info, handle=h)
+        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=True)
         if h is not None:
-            self._handles[id(z)] = (z, h)
+            self._handles[id(z.t)] = (z.t, h)
         return z
 
     def _conv(self, plan, xs, training):
-        h = self._handles.pop(id(xs[0]), (None, None))[1] if len(xs) == 1 else None
+        key = xs[0].t if isinstance(xs[0], Deferred) else xs[0]
+        h = self._handles.pop(id(key), (None, None))[1] if len(xs) == 1 else None
         return conv(plan, xs, want_stats=training, bn_handle=h)
 
     # -- blocks -------------------------------------------------------------------------------------
     def cba(self, m, xs, training, single=False):
         """ConvBNAct: Sequential(conv, BN, act)."""
-        if isinstance(xs, torch.Tensor):
+        if not isinstance(xs, (list, tuple)):
             xs = [xs]
         plan = self.plan_conv(m[0], gi=len(xs))
         (y,), part = self._conv(plan, xs, training)
@@ -169,8 +173,10 @@ class FusedExecutor:
         low = self.cba(m.lower_branch[1], low_z, training)
         return self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training, single=single_out)
 
-    def duck(self, m, x, training):
-        xb = bn_act([x], self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training)
+    def duck(self, m, xs, training):
+        """DUCK block over in_bn(sum(xs)): the encoder's ``x_i + x`` merge rides in in_bn's statistics
+        pass (both summands are deferred BN outputs)."""
+        xb = bn_act(xs, self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training, deferred=True)
         b1, b2, b3, b4, b5, b6 = m.branches()
         r4, r5 = b4[0], b5[0]
         convs3 = [b1[0][0], b2[0][0], b3.lower_branch[0][0], r4.lower_branch[0][0], r5.lower_branch[0][0]]
@@ -198,7 +204,7 @@ class FusedExecutor:
         # separated 1x7 -> 7x1
         o6 = self.cba(b6[0], xb, training, single=True)
         o6 = self.cba(b6[1], o6, training)
-        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training)
+        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training, deferred=True)
 
     def head(self, conv_mod, x, num_class):
         plan = self.plan_conv(conv_mod)
@@ -211,13 +217,13 @@ class FusedExecutor:
         stages = model.down_stages()
         s1 = stages[0]
         shortcut = self.cba(s1.conv2, x, training)
-        skip = self.duck(s1.duck, x, training)
+        skip = self.duck(s1.duck, [x], training)
         down = self.cba(s1.conv1, skip, training)
         skips = [skip]
         for st in stages[1:]:
-            x1 = add_n(down, shortcut)
-            shortcut = self.cba(st.conv2, shortcut, training)
-            skip = self.duck(st.duck, x1, training)
+            nxt = self.cba(st.conv2, shortcut, training)
+            skip = self.duck(st.duck, [down, shortcut], training)   # x_i + x inside in_bn's stats pass
+            shortcut = nxt
             down = self.cba(st.conv1, skip, training)
             skips.append(skip)
         x = add_n(down, shortcut)
@@ -226,7 +232,7 @@ class FusedExecutor:
             x = self.residual(blk, x, training, single_out=k + 1 < len(mids))
         for st, skip in zip(model.up_stages(), reversed(skips)):
             x = up2_add(x, skip)
-            x = self.duck(st.duck, x, training)
+            x = self.duck(st.duck, [x], training)
         return self.head(model.seg_head, x, model.num_class)
 
     def unet(self, model, images, training):
@@ -235,7 +241,7 @@ class FusedExecutor:
         for i in range(1, 5):
             st = getattr(model, f'down_stage{i}')
             f = self.cba(st.conv[0], x, training, single=True)
-            f = self.cba(st.conv[1], f, training)
+            f = materialize(self.cba(st.conv[1], f, training))   # maxpool has no BN prologue
             skips.append(f)
             p = st.pool
             x = maxpool(f, p.kernel_size, p.stride, p.padding)
@@ -246,7 +252,7 @@ class FusedExecutor:
             dc = st.up.up_conv
             plan = self.plan_deconv(dc[0])
             (u,), part = conv(plan, [x], want_stats=training)
-            u = bn_act([u], self.bn(dc[1]), _is_relu(dc[2]), training, (part, plan.rows, 0) if training else None)
+            u = self._bn_out([u], self.bn(dc[1]), _is_relu(dc[2]), training, (part, plan.rows, 0) if training else None)
             x = self.cba(st.conv[0], [u, skips[i - 1]], training, single=True)
             x = self.cba(st.conv[1], x, training)
         return self.head(model.seg_head, x, model.num_class)
@@ -270,12 +276,12 @@ class FusedExecutor:
             o = self.conv_bn(blk.conv3, blk.bn3, o, training, relu=False)
         else:
             o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=False)
-        return add_act(o, idt, relu=True)
+        return add_act(materialize(o), materialize(idt), relu=True)
 
     def resnet_unet(self, model, images, training):
         enc, dec = model.encoder, model.decoder
         x = to_fm(images)
-        f1 = self.conv_bn(enc.conv1, enc.bn1, x, training, relu=True)
+        f1 = materialize(self.conv_bn(enc.conv1, enc.bn1, x, training, relu=True))
         mp = enc.maxpool
         x = maxpool(f1, _pair(mp.kernel_size)[0], _pair(mp.stride)[0], _pair(mp.padding)[0])
         feats = [f1]
@@ -289,7 +295,7 @@ class FusedExecutor:
         for i, blk in enumerate(dec.blocks):
             skip = skips[i] if i < len(skips) else None
             cs = skip_ch[i] if skip is not None else 0
-            x = up2_cat(x, skip, cx, cs)
+            x = up2_cat(materialize(x), skip, cx, cs)
             x = self.cba(blk.conv1, x, training, single=True)
             x = self.cba(blk.conv2, x, training)
             cx = blk.conv2[0].out_channels

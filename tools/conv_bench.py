@@ -53,6 +53,8 @@ def main():
     ap.add_argument('--miopen', action='store_true')
     ap.add_argument('--halo', type=int, default=1, help='1: halo-tiled stride-1 kernel where eligible, 0: gather only')
     ap.add_argument('--only', default='', help='substring filter on layer names')
+    ap.add_argument('--prologue', action='store_true',
+                    help='input is a deferred BN(+ReLU) output: fwd / wgrad apply the BN prologue while staging')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     from medical_segmentation_pytorch_amd.ops import _ext
@@ -77,7 +79,13 @@ def main():
         ys = [torch.empty(n, oh, ow, plan.Cgo, device=dev, dtype=torch.bfloat16) for _ in range(groups)]
         nblk = C.conv_stat_blocks(dims, dy, dx)
         part = torch.empty(nblk, 2, plan.rows, device=dev)
-        t_f = timeit(lambda: C.conv_fwd([x], wp, ys, None, part, dims, dy, dx, False), a.iters)
+        xc, xr = [], 0
+        if a.prologue:   # BN stats rows (scale, shift, mean, invstd) of the input channels
+            st = torch.zeros(4, plan.Cgi, device=dev)
+            st[0, :ci] = torch.rand(ci, device=dev) + 0.5
+            st[1, :ci] = torch.randn(ci, device=dev) * 0.1
+            xc, xr = [st], 1
+        t_f = timeit(lambda: C.conv_fwd([x], wp, ys, None, part, dims, dy, dx, False, xc, xr), a.iters)
         wd, Kp_d = plan.pack_dgrad(dev)
         gys = [torch.randn_like(y, dtype=torch.float32).to(torch.bfloat16) for y in ys]
         dxs = [torch.empty_like(x)]
@@ -85,7 +93,7 @@ def main():
         bdy, bdx = [t[0] for t in plan.taps_bwd], [t[1] for t in plan.taps_bwd]
         t_d = timeit(lambda: C.conv_fwd(gys, wd, dxs, None, None, dims_d, bdy, bdx, s > 1), a.iters)
         dwp = torch.empty(C.conv_wgrad_replicas(dims, dy, dx, False) * plan.rows * plan.T * plan.Cip, device=dev)
-        t_w = timeit(lambda: C.conv_wgrad(gys, [x], dwp, dims, dy, dx, False), a.iters)
+        t_w = timeit(lambda: C.conv_wgrad(gys, [x], dwp, dims, dy, dx, False, xc, xr), a.iters)
         flops = 2.0 * n * oh * ow * co * ci * k[0] * k[1] * groups
         row = {'layer': name, 'fwd_ms': round(t_f, 4), 'dgrad_ms': round(t_d, 4), 'wgrad_ms': round(t_w, 4),
                'fwd_tflops': round(flops / t_f / 1e9, 1), 'dgrad_tflops': round(flops / t_d / 1e9, 1),
