@@ -47,7 +47,63 @@ def parse_args(argv=None):
     p.add_argument('--graph-ddp', action='store_true', help='also capture the multi-GPU step in a hipGraph')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
+    p.add_argument('--data', choices=['augment', 'fixed'], default='augment',
+                   help='augment (default): every step draws a fresh MyConfig-augmented batch from an HBM-resident '
+                        'synthetic polyp split (GPU augmentation kernels, inside the timed loop); fixed: replay one '
+                        'resident batch (isolates the model step)')
+    p.add_argument('--train-images', type=int, default=128, help='synthetic train split size (per rank)')
+    p.add_argument('--val-images', type=int, default=32, help='held-out synthetic val split for the Dice (0 = skip)')
+    p.add_argument('--lr', type=float, default=1e-3, help='Adam lr per GPU (reference: 0.1 * base_lr * gpu_num)')
     return p.parse_args(argv)
+
+
+def synthetic_split(n, size, seed):
+    """n synthetic polyp frames (HWC uint8) + masks (HW {0,1} uint8), reference-like content."""
+    import numpy as np
+    from medical_segmentation_pytorch_amd.datasets.synthetic import make_sample
+    rng = np.random.default_rng(seed)
+    pairs = [make_sample(size, rng) for _ in range(n)]
+    return [p[0] for p in pairs], [p[1] for p in pairs]
+
+
+def make_feed(args, device, seed):
+    """The timed loop's data pipeline: HBM-resident split + the reference train augmentation
+    (MyConfig: randscale [-0.5, 1.0], colour jitter 0.5 (+ hue 0.2), flips 0.5; crop = bench size) on the
+    GPU kernels, one fresh batch per step written into the step's static input buffers."""
+    from medical_segmentation_pytorch_amd.datasets.device_loader import DeviceAugLoader, DeviceDataset
+    from medical_segmentation_pytorch_amd.utils.transforms import SegAugment
+    imgs, msks = synthetic_split(args.train_images, args.size, seed)
+    data = DeviceDataset.from_arrays(imgs, msks, device)
+    aug = SegAugment(args.size, args.size, randscale=[-0.5, 1.0], brightness=0.5, contrast=0.5, saturation=0.5,
+                     h_flip=0.5, v_flip=0.5)
+    loader = DeviceAugLoader(None, args.batch, device, seed=seed, data=data, aug=aug)
+    order = loader.stream()
+
+    def feed(images, masks):
+        loader.batch(next(order), out=(images, masks))
+    return feed
+
+
+def val_dice(model, args, device, seed):
+    """Reference validation metric (torchmetrics Dice, average='macro' over both classes, from one
+    confusion matrix -- reference utils/metrics.py:4-13) + foreground Dice, on a held-out synthetic split,
+    evaluated by the fused executor in eval mode (running BN statistics)."""
+    from medical_segmentation_pytorch_amd.runtime.fused_model import FusedExecutor
+    from medical_segmentation_pytorch_amd.utils.transforms import normalize_to_tensor
+    imgs, msks = synthetic_split(args.val_images, args.size, seed)
+    ex = FusedExecutor(model)
+    model.eval()
+    cm = torch.zeros(2, 2, dtype=torch.float64)
+    with torch.no_grad():
+        for i in range(0, len(imgs), 16):
+            x = torch.stack([normalize_to_tensor(im) for im in imgs[i:i + 16]]).to(device)
+            t = torch.stack([torch.from_numpy(m.astype('int64')) for m in msks[i:i + 16]]).to(device)
+            p = ex(x, training=False).argmax(1)
+            cm += torch.bincount((t * 2 + p).flatten(), minlength=4).view(2, 2).double().cpu()
+    model.train()
+    tp = cm.diag()
+    dice = 2 * tp / (cm.sum(0) + cm.sum(1)).clamp(min=1)
+    return float(dice.mean()), float(dice[1])
 
 
 def model_label(args):
@@ -78,10 +134,12 @@ def main(argv=None):
 
     impl = args.impl
     use_graph = not args.no_graph and (world == 1 or args.graph_ddp)
+    feed = make_feed(args, device, seed=1000 + rank) if args.data == 'augment' else None
     step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
                             base_channel=args.base_channel, device=device,
                             channels_last=args.channels_last, use_graph=use_graph,
-                            distributed=world > 1, model_name=args.model, teacher_name=args.teacher)
+                            distributed=world > 1, model_name=args.model, teacher_name=args.teacher,
+                            feed=feed, total_steps=args.warmup + args.steps, lr=args.lr * world)
 
     t_w = time.perf_counter()
     if rank == 0:   # heartbeat: MIOpen's first-call kernel search (eager impl) can be silent for minutes
@@ -118,6 +176,10 @@ def main(argv=None):
     ms = elapsed / args.steps * 1e3
     global_batch = args.batch * world
     value = global_batch * args.steps / elapsed
+    dice = fg_dice = None
+    if args.val_images > 0 and rank == 0 and args.model in ('ducknet', 'unet') and hasattr(step, 'ema_model'):
+        # the EMA model (= live weights with use_ema=False, MyConfig) after this run's W+K steps
+        dice, fg_dice = val_dice(step.ema_model, args, device, seed=99)
     baseline = None
     try:
         with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')) as f:
@@ -133,7 +195,15 @@ def main(argv=None):
             'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': (value / baseline) if baseline else None,
-            'dtype': 'bf16', 'data': 'synthetic 352x352 polyp images/masks, random-init weights',
+            'dtype': 'bf16',
+            'data': ('synthetic 352x352 polyp images/masks, random-init weights; ' +
+                     ('fresh GPU-augmented batch per step (MyConfig aug) inside the timed loop'
+                      if args.data == 'augment' else 'one resident batch replayed')),
+            'val_dice': None if dice is None else round(dice, 4),
+            'val_dice_fg': None if fg_dice is None else round(fg_dice, 4),
+            'val_dice_note': (f'macro Dice (reference metric) on {args.val_images} held-out synthetic images after '
+                              f'this run\'s {args.warmup + args.steps} training steps (OneCycle over those steps); '
+                              'converged accuracy: tools/train_synthetic.py') if dice is not None else None,
             'config': {'model': model_label(args), 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,

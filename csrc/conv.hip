@@ -669,6 +669,14 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   }
 }
 
+// Zero-fill as a kernel node: inside captured hipGraphs a hipMemsetAsync on the capturing stream was
+// measured NOT to re-zero the buffer on replays >= 2 (replicas then held stale graph-pool bytes), so
+// every accumulation buffer of the step is cleared by this kernel instead.
+__global__ void zero_f32_kernel(float4* __restrict__ p, long n4) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
+    p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, int nrow, int nch,
                                    int T, int Cpk, int Kp, int t_base, int c_base, long s_row, long s_ch) {
   const long total = (long)nrow * nch * T;
@@ -876,6 +884,47 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
   }
 
   const int n_rg = CHUNKED ? 1 : (rows + 16 * MI - 1) / (16 * MI);
+  if (!CHUNKED) {
+    // Whole-input staging, before the row-group loop so that none of its temporaries stay live into
+    // the MFMA loop.  The deferred-BN prologue runs at LDS-store time from the coefficient table
+    // (code[u] = tile offset | (input channel + 1) << 16 for in-image vectors).
+    for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
+      uint4 v[kHaloLd];
+      int dst[kHaloLd];
+      load_batch(0, base, v, dst);
+      if (!BNE && hg.xtab) {
+#pragma unroll
+        for (int u = 0; u < kHaloLd; ++u) {
+          if (dst[u] < 0) continue;
+          uint4 val = v[u];
+          const int idx = base + u * 64 * kHaloWaves;
+          const int hp = fdiv(idx, C8c, hg.inv_c8), c8 = idx - __mul24(hp, C8c);
+          const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
+          const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
+          if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
+            const float* cp = s_coef + c8 * 8;
+            const float4 s0 = *reinterpret_cast<const float4*>(cp), s1 = *reinterpret_cast<const float4*>(cp + 4);
+            const float4 h0 = *reinterpret_cast<const float4*>(cp + Cip);
+            const float4 h1 = *reinterpret_cast<const float4*>(cp + Cip + 4);
+            const float4 l0 = *reinterpret_cast<const float4*>(cp + 2 * Cip);
+            const float4 l1 = *reinterpret_cast<const float4*>(cp + 2 * Cip + 4);
+            float f[8];
+            unpack8(val, f);
+            f[0] = fmaxf(fmaf(f[0], s0.x, h0.x), l0.x); f[1] = fmaxf(fmaf(f[1], s0.y, h0.y), l0.y);
+            f[2] = fmaxf(fmaf(f[2], s0.z, h0.z), l0.z); f[3] = fmaxf(fmaf(f[3], s0.w, h0.w), l0.w);
+            f[4] = fmaxf(fmaf(f[4], s1.x, h1.x), l1.x); f[5] = fmaxf(fmaf(f[5], s1.y, h1.y), l1.y);
+            f[6] = fmaxf(fmaf(f[6], s1.z, h1.z), l1.z); f[7] = fmaxf(fmaf(f[7], s1.w, h1.w), l1.w);
+            val = pack8(f);
+          }
+          *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+        }
+      } else {
+        store_batch(v, dst);
+      }
+    }
+    __syncthreads();
+  }
+
   for (int rg = 0; rg < n_rg; ++rg) {
     const int co0 = rg * 16 * MI;
     const uint16_t* wrow[MI];
@@ -896,18 +945,6 @@ __global__ __launch_bounds__(64 * kHaloWaves, CHUNKED ? 2 : 3) void conv_halo_ke
         if (ch + 1 < hg.nch) load_batch(c0 + hg.CC, tid, pv, pd);   // in flight during the MFMAs
         if (!BNE && hg.xtab) {   // prologues are forward-only, BNE data-gradient-only
           xform_pass(c0);
-          __syncthreads();
-        }
-      } else if (rg == 0) {
-        for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
-          uint4 v[kHaloLd];
-          int dst[kHaloLd];
-          load_batch(0, base, v, dst);
-          store_batch(v, dst);
-        }
-        __syncthreads();
-        if (!BNE && hg.xtab) {
-          xform_pass(0);
           __syncthreads();
         }
       }
@@ -1336,7 +1373,11 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
   for (int i = 0; i < g.Gi; ++i) P.xc[i] = xc != nullptr ? xc[i] : nullptr;
   P.xrelu = xrelu;
   const int nrep = conv_wgrad_replicas(g, trans);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)rows * KT * nrep, s);
+  {
+    const long n = (long)rows * KT * nrep;   // multiple of 4 (rows % 8 == 0), 16-B aligned (torch alloc)
+    const long blocks = std::min<long>(std::max<long>((n / 4 + 255) / 256, 1), 2048);
+    hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<float4*>(dw), n / 4);
+  }
   DwTile tl{};
   if (!trans && wgrad_halo_ok(g, tl)) {
     const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;

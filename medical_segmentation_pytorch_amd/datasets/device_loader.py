@@ -40,13 +40,15 @@ def pack_params(prms, indices, n_iparams=14):
 class DeviceDataset:
     """Every (image, mask) of a :class:`PolypDataset` split decoded once into device memory."""
 
-    def __init__(self, dataset, device):
+    def __init__(self, dataset, device, arrays=None):
+        if arrays is None:
+            arrays = ((np.asarray(Image.open(ip).convert('RGB'), dtype=np.uint8),
+                       np.asarray(Image.open(mp).convert('1'), dtype=np.uint8))
+                      for ip, mp in zip(dataset.images, dataset.masks))
         imgs, msks, meta = [], [], []
         off = moff = 0
-        for ip, mp in zip(dataset.images, dataset.masks):
-            im = np.asarray(Image.open(ip).convert('RGB'), dtype=np.uint8)
-            mk = np.asarray(Image.open(mp).convert('1'), dtype=np.uint8)
-            assert im.shape[:2] == mk.shape, (ip, im.shape, mk.shape)
+        for im, mk in arrays:
+            assert im.dtype == np.uint8 and mk.dtype == np.uint8 and im.shape[:2] == mk.shape, (im.shape, mk.shape)
             h, w = mk.shape
             meta.append((off, h, w, moff))
             imgs.append(im.reshape(-1))
@@ -58,6 +60,11 @@ class DeviceDataset:
         self.masks = torch.from_numpy(np.concatenate(msks)).to(device)
         self.meta = torch.tensor(meta, dtype=torch.int64, device=device)
         self.device = device
+
+    @classmethod
+    def from_arrays(cls, images, masks, device):
+        """From in-memory HWC uint8 images and HW {0,1} uint8 masks (synthetic data, tests)."""
+        return cls(None, device, arrays=zip(images, masks))
 
     def __len__(self):
         return len(self.shapes)
@@ -72,10 +79,10 @@ class DeviceAugLoader:
     ``set_epoch`` (DistributedSampler) exactly like the host loader."""
 
     def __init__(self, dataset, batch_size, device, sampler=None, shuffle=True, drop_last=True, seed=0,
-                 binary_float=False):
+                 binary_float=False, data=None, aug=None):
         require()
         self.dataset = dataset
-        self.data = DeviceDataset(dataset, device)
+        self.data = data if data is not None else DeviceDataset(dataset, device)
         self.batch_size = batch_size
         self.sampler = sampler
         self.shuffle = shuffle
@@ -83,9 +90,14 @@ class DeviceAugLoader:
         self.binary_float = binary_float
         self.epoch = 0
         self.seed = seed
-        aug = dataset.transform
+        aug = aug if aug is not None else dataset.transform
         assert isinstance(aug, SegAugment), 'DeviceAugLoader needs the train SegAugment pipeline'
         self.aug = aug
+        # pinned parameter staging ring: the per-batch H2D copies stay asynchronous (a pageable copy
+        # would make the host wait for the GPU before it can draw the next batch)
+        self._ring = [None] * 4
+        self._ring_ev = [None] * 4
+        self._ri = 0
         self.aug.seed(seed)
         ch, cw = aug.crop
         B = batch_size
@@ -108,9 +120,32 @@ class DeviceAugLoader:
             return torch.randperm(len(self.data), generator=g).tolist()
         return list(range(len(self.data)))
 
-    def batch(self, indices, prms=None):
+    def _stage(self, ip, fp):
+        """Device copies of the parameter tables through the pinned ring (async H2D)."""
+        if self.device.type != 'cuda':
+            return torch.from_numpy(ip).to(self.device), torch.from_numpy(fp).to(self.device)
+        i = self._ri
+        self._ri = (i + 1) % len(self._ring)
+        ev = self._ring_ev[i]
+        if ev is not None:
+            ev.synchronize()   # that slot's previous copy has been consumed
+        slot = self._ring[i]
+        if slot is None or slot[0].shape != ip.shape:
+            slot = self._ring[i] = (torch.empty(ip.shape, dtype=torch.int32).pin_memory(),
+                                    torch.empty(fp.shape, dtype=torch.float32).pin_memory())
+        slot[0].numpy()[...] = ip
+        slot[1].numpy()[...] = fp
+        ip_d = slot[0].to(self.device, non_blocking=True)
+        fp_d = slot[1].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ring_ev[i] = ev
+        return ip_d, fp_d
+
+    def batch(self, indices, prms=None, out=None):
         """Augment the samples ``indices`` -> (images [B,3,ch,cw] fp32, masks [B,ch,cw]) on the device.
-        ``prms``: pre-drawn parameter records (tests); default = draw from the pipeline's RNG."""
+        ``prms``: pre-drawn parameter records (tests); default = draw from the pipeline's RNG.
+        ``out``: optional (images, int64 masks) buffers to write into (static graph inputs)."""
         C = require()
         ch, cw = self.aug.crop
         B = len(indices)
@@ -118,12 +153,15 @@ class DeviceAugLoader:
         if prms is None:
             prms = [self.aug.sample_params(*self.data.shapes[i]) for i in indices]
         ip, fp = pack_params(prms, indices, C.aug_iparams())
-        ip_d = torch.from_numpy(ip).to(self.device, non_blocking=True)
-        fp_d = torch.from_numpy(fp).to(self.device, non_blocking=True)
+        ip_d, fp_d = self._stage(ip, fp)
         stages = [k for k in range(4) if ip[:, 10 + k].any()]
         contrast = [k for k in stages if (ip[:, 10 + k] == _OPS['c']).any()]
-        out = torch.empty(B, 3, ch, cw, dtype=torch.float32, device=self.device)
-        masks = torch.empty(B, ch, cw, dtype=torch.int64, device=self.device)
+        if out is not None:
+            out, masks = out
+            assert out.shape == (B, 3, ch, cw) and masks.shape == (B, ch, cw) and masks.dtype == torch.int64
+        else:
+            out = torch.empty(B, 3, ch, cw, dtype=torch.float32, device=self.device)
+            masks = torch.empty(B, ch, cw, dtype=torch.int64, device=self.device)
         work = self.work[:B * ch * cw * 3]
         C.aug_batch(self.data.images, self.data.masks, self.data.meta, ip_d, fp_d, work, self.mean, out, masks,
                     stages, contrast, self.norm_mean, self.norm_std)
@@ -135,6 +173,14 @@ class DeviceAugLoader:
         stop = len(order) - (len(order) % B if self.drop_last else 0)
         for i in range(0, stop, B):
             yield self.batch(order[i:i + B])
+
+    def stream(self):
+        """Endless epoch-after-epoch index batches (bench / step-based training)."""
+        while True:
+            order = self._order()
+            B = self.batch_size
+            for i in range(0, len(order) - B + 1, B):
+                yield order[i:i + B]
 
 
 def reference_batch(aug: SegAugment, dataset, indices, prms):

@@ -40,7 +40,8 @@ class _OneCycle:
 
 
 def build_eager_step(batch, size, base_channel, device, channels_last=False, distributed=False,
-                     lr=1e-3, total_steps=100000, model_name='ducknet', teacher_name=None, kd_temperature=4.0):
+                     lr=1e-3, total_steps=100000, model_name='ducknet', teacher_name=None, kd_temperature=4.0,
+                     feed=None):
     from .trainer_engine import make_model
     torch.manual_seed(1)
     model = make_model(model_name, base_channel).to(device)
@@ -60,7 +61,12 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
     images = images.contiguous(memory_format=fmt)
     ema_vals = list(ema.state_dict().values())
 
+    nchw = torch.empty(images.shape, dtype=images.dtype, device=device)
+
     def step():
+        if feed is not None:   # same data pipeline as the fused step (GPU augmentation per batch)
+            feed(nchw, masks)
+            images.copy_(nchw)
         opt.zero_grad()
         with torch.autocast('cuda', dtype=torch.bfloat16):
             preds = model(images)
@@ -80,15 +86,18 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
                 e.copy_(m)
         return loss
 
+    step.model_ref = model.module if distributed else model
+    step.ema_model = ema
     return step
 
 
 def build_bench_step(impl, batch, size, base_channel, device, channels_last=False,
-                     use_graph=True, distributed=False, model_name='ducknet', teacher_name=None):
+                     use_graph=True, distributed=False, model_name='ducknet', teacher_name=None, feed=None,
+                     total_steps=100000, lr=1e-3):
     if impl == 'eager':
-        return build_eager_step(batch, size, base_channel, device, channels_last, distributed,
-                                model_name=model_name, teacher_name=teacher_name)
+        return build_eager_step(batch, size, base_channel, device, channels_last, distributed, lr=lr,
+                                total_steps=total_steps, model_name=model_name, teacher_name=teacher_name, feed=feed)
     from .trainer_engine import build_fused_step
     return build_fused_step(batch=batch, size=size, base_channel=base_channel, device=device,
                             use_graph=use_graph, distributed=distributed, model_name=model_name,
-                            teacher_name=teacher_name)
+                            teacher_name=teacher_name, feed=feed, total_steps=total_steps, lr=lr)

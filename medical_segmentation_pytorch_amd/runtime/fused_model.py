@@ -32,6 +32,8 @@ from ..ops.pool import add_act, maxpool, up2_cat
 
 # env MSP_BN_EPILOGUE=0 disables the dgrad-epilogue BN partials (A/B switch)
 _BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
+# env MSP_DEFER_BN=0 materialises every BN output (bn_act_apply pass) instead of deferring it (A/B switch)
+_DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
 
 
 def _is_relu(act_mod):
@@ -137,9 +139,10 @@ class FusedExecutor:
     def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
         """Deferred bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
         h = BwdStatsHandle() if (single and training and _BN_EPILOGUE) else None
-        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=True)
+        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=_DEFER_BN)
+        key = z.t if isinstance(z, Deferred) else z
         if h is not None:
-            self._handles[id(z.t)] = (z.t, h)
+            self._handles[id(key)] = (key, h)
         return z
 
     def _conv(self, plan, xs, training):
@@ -176,7 +179,7 @@ class FusedExecutor:
     def duck(self, m, xs, training):
         """DUCK block over in_bn(sum(xs)): the encoder's ``x_i + x`` merge rides in in_bn's statistics
         pass (both summands are deferred BN outputs)."""
-        xb = bn_act(xs, self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training, deferred=True)
+        xb = bn_act(xs, self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training, deferred=_DEFER_BN)
         b1, b2, b3, b4, b5, b6 = m.branches()
         r4, r5 = b4[0], b5[0]
         convs3 = [b1[0][0], b2[0][0], b3.lower_branch[0][0], r4.lower_branch[0][0], r5.lower_branch[0][0]]
@@ -204,7 +207,8 @@ class FusedExecutor:
         # separated 1x7 -> 7x1
         o6 = self.cba(b6[0], xb, training, single=True)
         o6 = self.cba(b6[1], o6, training)
-        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training, deferred=True)
+        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training,
+                      deferred=_DEFER_BN)
 
     def head(self, conv_mod, x, num_class):
         plan = self.plan_conv(conv_mod)

@@ -23,7 +23,7 @@ class FusedStep:
     def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
                  total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
                  syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
-                 kd_coef=1.0):
+                 kd_coef=1.0, feed=None):
         require()
         dev = images.device
         self.model = model
@@ -54,6 +54,9 @@ class FusedStep:
         # KD (reference core/seg_trainer.py:69-79): frozen eval-mode teacher on the same fused kernels
         self.teacher = FusedExecutor(teacher) if teacher is not None else None
         self.kd_temperature, self.kd_coef = kd_temperature, kd_coef
+        # feed(images, masks): writes the next (augmented) batch into the static input buffers on the
+        # current stream before each step -- the data pipeline runs inside the timed loop, outside the graph
+        self.feed = feed
 
     def _body(self):
         C = require()
@@ -89,22 +92,26 @@ class FusedStep:
         self.sched.step()
 
     def __call__(self):
+        """One training step (exactly one optimizer update per call).  Graph mode: call 1 runs eagerly
+        on a side stream (allocator / autograd warm-up, every plan created), call 2 builds the pack
+        program, captures the body and replays it; every later call is one replay."""
+        if self.feed is not None:
+            self.feed(self.images, self.masks)
         self._prepare()
         if self.ex.pack_program is None and self.itrs > 1:
             self.ex.build_pack_program(self.images.device)
         if not self.use_graph:
             self.loss = self._body()
             return self.loss
-        if self.graph is None:
-            # warm up on a side stream (allocator + autograd state), then capture
+        if self.itrs == 1:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._body()
-                if self.ex.pack_program is None:
-                    self.ex.build_pack_program(self.images.device)
-                self._body()
+                self.loss = self._body()
             torch.cuda.current_stream().wait_stream(s)
+            return self.loss
+        if self.graph is None:
+            torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self.loss = self._body()
@@ -128,7 +135,7 @@ def make_model(model_name, base_channel=17, num_class=2):
 
 
 def build_fused_step(batch, size, base_channel, device, use_graph=True, distributed=False, optimizer='adam',
-                     lr=1e-3, model_name='ducknet', syncbn=True, teacher_name=None):
+                     lr=1e-3, model_name='ducknet', syncbn=True, teacher_name=None, feed=None, total_steps=100000):
     from .bench_step import synthetic_batch
     torch.manual_seed(1)
     model = make_model(model_name, base_channel).to(device).train()
@@ -144,4 +151,4 @@ def build_fused_step(batch, size, base_channel, device, use_graph=True, distribu
             p.requires_grad_(False)
     images, masks = synthetic_batch(batch, size, device, seed=dist.get_rank() if distributed else 0)
     return FusedStep(model, images, masks, optimizer=optimizer, lr=lr, use_graph=use_graph, distributed=distributed,
-                     syncbn=syncbn, teacher=teacher)
+                     syncbn=syncbn, teacher=teacher, feed=feed, total_steps=total_steps)
