@@ -449,10 +449,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
     }
     __syncthreads();
   }
+  // deterministic split-K: this block's partial tile goes to ITS slab (blockIdx.z) with plain stores;
+  // unpack_wgrad sums the gridDim.z slabs in fixed order (no atomics, no zero-fill)
+  float* slab = dw + (long)blockIdx.z * rows * KT;
   for (int e = tid; e < CO_T * K_T; e += 256) {
     const int ci = e / K_T, kj = e - (e / K_T) * K_T;
     const int co = co0 + ci, k = k0 + kj;
-    if (co < rows && (co % g.Cgo) < g.Cgo_l && k < KT) atomicAdd(&dw[(long)co * KT + k], red[e]);
+    if (co < rows && k < KT) slab[(long)co * KT + k] = red[e];
   }
 }
 
@@ -491,7 +494,7 @@ DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 1
 // them: one input pass per NCB sub-tiles instead of per sub-tile, and fewer LDS reads/writes per MFMA.
 template <int NPW, int NCB>
 __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
-                                                              DwTile tl, int KT, long ntiles, int nrep) {
+                                                              DwTile tl, int KT, long ntiles) {
   constexpr int NST = dw_stage(NCB);
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
   constexpr int NPX = 256, NSL = 8, SUB = NPX * DW_CH;
@@ -647,9 +650,9 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
       }
     }
   }
-  // every block adds into one of nrep dW replicas (summed by unpack_wgrad): spreads the adds of
-  // ~nsplit blocks over nrep x more addresses instead of hot-spotting a few L2 lines
-  float* dwr = dw + (long)(blockIdx.x % nrep) * rows * KT;
+  // deterministic split-K: block x writes its partial dW tile into slab x (plain stores, every needed
+  // element exactly once per slab); unpack_wgrad sums the nsplit slabs in fixed order
+  float* dwr = dw + (long)blockIdx.x * rows * KT;
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
     const int pr = wave + kDwWaves * j;
@@ -664,17 +667,9 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + DW_CH * cb + 16 * i + 4 * lg + r;
-          if (co < rows && (co % g.Cgo) < g.Cgo_l) atomicAdd(&dwr[(long)co * KT + t * Cip + ci], acc[cb][i][j][r]);
+          if (co < rows) dwr[(long)co * KT + t * Cip + ci] = acc[cb][i][j][r];
         }
   }
-}
-
-// Zero-fill as a kernel node: inside captured hipGraphs a hipMemsetAsync on the capturing stream was
-// measured NOT to re-zero the buffer on replays >= 2 (replicas then held stale graph-pool bytes), so
-// every accumulation buffer of the step is cleared by this kernel instead.
-__global__ void zero_f32_kernel(float4* __restrict__ p, long n4) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
-    p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, int nrow, int nch,
@@ -700,7 +695,7 @@ __global__ void unpack_wgrad_kernel(const float* __restrict__ src, float* __rest
     const int row = (int)(rc / nch);
     const long si = (long)row * Ktot + (t_base + t) * Cpk + c_base + c;
     float v = 0.f;
-    for (int r = 0; r < nrep; ++r) v += src[r * rep_stride + si];   // sum of the atomic replicas
+    for (int r = 0; r < nrep; ++r) v += src[r * rep_stride + si];   // split-K slabs, fixed order
     float* d = dst + row * s_row + c * s_ch + t;
     *d = accumulate ? *d + v : v;
   }
@@ -1354,33 +1349,25 @@ static bool wgrad_halo_ok(const ConvGeom& g, DwTile& tl) {
   return wgrad_halo_lds(tl, 1) <= 64 * 1024;
 }
 
-// dW replicas for the halo path: as many as fit in ~4 MB (at most 16)
-int conv_wgrad_replicas(const ConvGeom& g, bool trans) {
-  DwTile tl{};
-  if (trans || !wgrad_halo_ok(g, tl)) return 1;
-  const long bytes = 4L * g.Go * g.Cgo * g.T * g.Gi * g.Cgi;
-  long r = (4L << 20) / std::max(bytes, 1L);
-  return (int)std::max(1L, std::min(16L, r));
-}
+// Weight-gradient launch plan.  Both kernels split the pixel reduction over blocks (split-K) and
+// write one fp32 dW slab per split; unpack_wgrad sums the slabs in a fixed order -> bitwise
+// deterministic weight gradients (SURVEY §5 race detection / §7.4), no atomics and no zero-fill.
+// (No hipMemsetAsync anywhere in the step: inside a captured hipGraph it was measured NOT to re-run
+// on replays >= 2, which left stale graph-pool bytes in the old atomic replicas.)
+struct WgradPlan {
+  bool halo;
+  DwTile tl;
+  int ncb, gx, gy, gz, k_t, co_t;
+  long nsplit, ntiles;
+};
 
-void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-                const float* const* xc, unsigned xrelu, hipStream_t s) {
+static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
+  WgradPlan P{};
   const int KT = g.T * g.Gi * g.Cgi;
   const int rows = g.Go * g.Cgo;
-  WgradPtrs P{};
-  for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
-  for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
-  for (int i = 0; i < g.Gi; ++i) P.xc[i] = xc != nullptr ? xc[i] : nullptr;
-  P.xrelu = xrelu;
-  const int nrep = conv_wgrad_replicas(g, trans);
-  {
-    const long n = (long)rows * KT * nrep;   // multiple of 4 (rows % 8 == 0), 16-B aligned (torch alloc)
-    const long blocks = std::min<long>(std::max<long>((n / 4 + 255) / 256, 1), 2048);
-    hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<float4*>(dw), n / 4);
-  }
-  DwTile tl{};
-  if (!trans && wgrad_halo_ok(g, tl)) {
-    const long ntiles = (long)g.N * tl.tiles_y * tl.tiles_x;
+  if (!trans && wgrad_halo_ok(g, P.tl)) {
+    P.halo = true;
+    P.ntiles = (long)g.N * P.tl.tiles_y * P.tl.tiles_x;
     // co sub-tiles per block: as many as the LDS budget allows (<= kDwMaxNcb; env MSP_DW_NCB caps it)
     static int max_ncb = -1;
     if (max_ncb < 0) {
@@ -1388,22 +1375,47 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
       max_ncb = (e != nullptr && atoi(e) > 0) ? std::min(atoi(e), kDwMaxNcb) : kDwMaxNcb;
     }
     int ncb = std::min(max_ncb, cdiv(rows, DW_CH));
-    while (ncb > 1 && wgrad_halo_lds(tl, ncb) > (size_t)kDwMaxLds) --ncb;
-    const int gy = cdiv(rows, DW_CH * ncb), gz = cdiv(g.Gi * g.Cgi, DW_CH);
-    // Blocks split the tiles and add their dW slab with fp32 atomics (into nrep replicas): atomic bytes
-    // = nsplit * rows * KT * 4, so one 8-wave block per CU that software-pipelines its ~8 tiles beats
-    // more, shorter-lived blocks.
+    while (ncb > 1 && wgrad_halo_lds(P.tl, ncb) > (size_t)kDwMaxLds) --ncb;
+    P.ncb = ncb;
+    P.gy = cdiv(rows, DW_CH * ncb);
+    P.gz = cdiv(g.Gi * g.Cgi, DW_CH);
+    // one 8-wave block per CU that software-pipelines its ~8 tiles beats more, shorter-lived blocks
     static long split_target = -1;   // blocks in the grid; env MSP_DW_SPLIT overrides (tuning)
     if (split_target < 0) {
       const char* e = getenv("MSP_DW_SPLIT");
       split_target = (e != nullptr && atol(e) > 0) ? atol(e) : kDwSplitTarget;
     }
-    long nsplit = split_target / ((long)gy * gz);
-    if (nsplit < 1) nsplit = 1;
-    if (nsplit > ntiles) nsplit = ntiles;
-    const size_t lds = wgrad_halo_lds(tl, ncb);
-    dim3 grid((unsigned)nsplit, gy, gz);
+    P.nsplit = std::max(1L, std::min(split_target / ((long)P.gy * P.gz), P.ntiles));
+    return P;
+  }
+  P.halo = false;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long nchunks = (M + WG_M - 1) / WG_M;
+  P.co_t = rows <= 32 ? 32 : 64;
+  P.k_t = KT <= 64 ? 64 : 128;
+  P.gx = cdiv(KT, P.k_t);
+  P.gy = cdiv(rows, P.co_t);
+  P.nsplit = std::max(1L, std::min(2048L / ((long)P.gx * P.gy), nchunks));
+  return P;
+}
+
+// number of dW slabs the caller allocates ([nsplit][rows][KT] fp32) and unpack_wgrad sums
+int conv_wgrad_replicas(const ConvGeom& g, bool trans) { return (int)wgrad_plan(g, trans).nsplit; }
+
+void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
+                const float* const* xc, unsigned xrelu, hipStream_t s) {
+  const int KT = g.T * g.Gi * g.Cgi;
+  WgradPtrs P{};
+  for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
+  for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
+  for (int i = 0; i < g.Gi; ++i) P.xc[i] = xc != nullptr ? xc[i] : nullptr;
+  P.xrelu = xrelu;
+  const WgradPlan W = wgrad_plan(g, trans);
+  if (W.halo) {
+    const size_t lds = wgrad_halo_lds(W.tl, W.ncb);
+    dim3 grid((unsigned)W.nsplit, W.gy, W.gz);
     const int npw = cdiv(2 * g.T, kDwWaves);
+    const int ncb = W.ncb;
     // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU) is opted into once per instantiation, before any
     // graph capture (the first call of every shape runs eagerly)
 #define HW_(N_, C_)                                                                                      \
@@ -1414,24 +1426,17 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kDwMaxLds);               \
         lds_attr = true;                                                                                \
       }                                                                                                 \
-      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, tl, KT, \
-                         ntiles, nrep);                                                                 \
+      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, W.tl, KT, \
+                         W.ntiles);                                                                     \
       return;                                                                                           \
     }
     HW_(1, 1) HW_(2, 1) HW_(3, 1) HW_(1, 2) HW_(2, 2) HW_(3, 2) HW_(1, 3) HW_(2, 3) HW_(3, 3)
 #undef HW_
+    return;
   }
-  const long M = (long)g.N * g.OH * g.OW;
-  const long nchunks = (M + WG_M - 1) / WG_M;
-  const int co_t = rows <= 32 ? 32 : 64;
-  const int k_t = KT <= 64 ? 64 : 128;
-  const int gx = cdiv(KT, k_t), gy = cdiv(rows, co_t);
-  long target = 2048 / ((long)gx * gy);
-  if (target < 1) target = 1;
-  if (target > nchunks) target = nchunks;
-  dim3 grid(gx, gy, (unsigned)target);
+  dim3 grid(W.gx, W.gy, (unsigned)W.nsplit);
 #define WG(CO_, K_)                                                                                  \
-  if (co_t == CO_ && k_t == K_) {                                                                    \
+  if (W.co_t == CO_ && W.k_t == K_) {                                                                \
     if (trans) hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, true>), grid, dim3(256), 0, s, P, dw, g, KT); \
     else hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, false>), grid, dim3(256), 0, s, P, dw, g, KT);      \
     return;                                                                                          \

@@ -293,16 +293,18 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0)):
         dims = [n, oh, ow, 1, plan.Cgo, ih, iw, 1, plan.Cgi, plan.ci_l, plan.T, Kp_w, plan.stride]
         dy, dx = _taps(plan.taps_fwd)
         assert not coefs, 'transposed convs take materialised inputs'
-        dwp = torch.empty(plan.Cgi * plan.T * plan.Cgo, dtype=torch.float32, device=dev)
+        nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # split-K slabs, summed in order by unpack
+        one = plan.Cgi * plan.T * plan.Cgo
+        dwp = torch.empty(nrep * one, dtype=torch.float32, device=dev)
         C.conv_wgrad(xs, gys, dwp, dims, dy, dx, False)
         dst = b.sink if b.sink is not None else torch.zeros_like(b.weight, dtype=torch.float32)
         C.unpack_wgrad(dwp, dst.view(-1), plan.ci_l, plan.co_l, plan.T, plan.Cgo, plan.T * plan.Cgo, 0, 0,
-                       plan.co_l * plan.T, plan.T, True)
+                       plan.co_l * plan.T, plan.T, True, nrep, one)
         return [None if b.sink is not None else dst]
     dims = plan.fwd_dims(n, ih, iw, oh, ow)
     dy, dx = _taps(plan.taps_fwd)
     KT = plan.T * plan.Cip
-    nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # atomic-spreading dW replicas, summed on unpack
+    nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # split-K dW slabs, summed in fixed order on unpack
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
     C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask)
     cin_tot = plan.Gi * plan.ci_l

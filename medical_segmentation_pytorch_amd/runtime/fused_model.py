@@ -65,11 +65,17 @@ class FusedExecutor:
         # pops its input's handle (see ops.bn.BwdStatsHandle).  Reset every forward.
         self._handles = {}
 
+    # Caches are keyed by id(module); the entry keeps the module itself and a hit must be the SAME
+    # object (an id can be reused by a new module once the old one is freed).
+    def _cached(self, cache, key, owner):
+        e = cache.get(key)
+        return e[1] if e is not None and e[0] is owner else None
+
     def build_pack_program(self, device):
         """After one forward created every plan: pack all weights in one launch per step.  The
         persistent packed buffers start zeroed, so the program runs once right away: every later
         forward -- eager or captured -- sees the current weights even before its own repack()."""
-        self.pack_program = PackProgram(list(self._plans.values()), device)
+        self.pack_program = PackProgram([e[1] for e in self._plans.values()], device)
         self.pack_program.run()
         return self.pack_program
 
@@ -79,12 +85,12 @@ class FusedExecutor:
 
     # -- caches -------------------------------------------------------------------------------------
     def bn(self, m):
-        st = self._bns.get(id(m))
+        st = self._cached(self._bns, id(m), m)
         if st is None:
             st = BNState.from_module(m, self.group, self.sinks)
             st.count_nbt = self.count_nbt
             st.ready_hook = self.ready_hook
-            self._bns[id(m)] = st
+            self._bns[id(m)] = (m, st)
         return st
 
     def _branch(self, conv_mod, out_group=0, t_base=0):
@@ -93,7 +99,7 @@ class FusedExecutor:
 
     def plan_conv(self, c: nn.Conv2d, gi=1):
         key = ('c', id(c), gi)
-        p = self._plans.get(key)
+        p = self._cached(self._plans, key, c)
         if p is None:
             kh, kw = _pair(c.kernel_size)
             assert c.groups == 1, 'grouped/depthwise conv not in the fused engine yet'
@@ -101,12 +107,12 @@ class FusedExecutor:
                          padding=_pair(c.padding), dilation=_pair(c.dilation), Gi=gi, bias=c.bias,
                          bias_sink=self.sinks.get(id(c.bias)) if c.bias is not None else None,
                          ready_hook=self.ready_hook)
-            self._plans[key] = p
+            self._plans[key] = (c, p)
         return p
 
     def plan_deconv(self, c: nn.ConvTranspose2d):
         key = ('t', id(c))
-        p = self._plans.get(key)
+        p = self._cached(self._plans, key, c)
         if p is None:
             kh, kw = _pair(c.kernel_size)
             p = ConvPlan(kh, kw, c.in_channels, c.out_channels,
@@ -115,13 +121,13 @@ class FusedExecutor:
                          transposed=True, output_padding=_pair(c.output_padding)[0], bias=c.bias,
                          bias_sink=self.sinks.get(id(c.bias)) if c.bias is not None else None,
                          ready_hook=self.ready_hook)
-            self._plans[key] = p
+            self._plans[key] = (c, p)
         return p
 
     def plan_fused3x3(self, key, convs3, convs1):
         """One 3x3/d1/p1 GEMM over sibling convs reading the same input: 3x3 convs first, then 1x1
         convs at the centre tap.  Output group order = convs3 + convs1."""
-        p = self._plans.get(key)
+        p = self._cached(self._plans, key, convs3[0])
         if p is None:
             c0 = convs3[0]
             branches = [self._branch(c, g, 0) for g, c in enumerate(convs3)]
@@ -132,7 +138,7 @@ class FusedExecutor:
                 assert _pair(c.kernel_size) == (1, 1) and c.bias is None
             p = ConvPlan(3, 3, c0.in_channels, c0.out_channels, branches, stride=1, padding=(1, 1),
                          dilation=(1, 1), Go=len(branches), ready_hook=self.ready_hook)
-            self._plans[key] = p
+            self._plans[key] = (convs3[0], p)
         return p
 
     # -- single-consumer BN outputs ------------------------------------------------------------------
