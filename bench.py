@@ -126,11 +126,16 @@ def main(argv=None):
 
     from medical_segmentation_pytorch_amd.runtime.bench_step import build_bench_step
     dist = None
+    # test hooks: BENCH_DIST_BACKEND=gloo + BENCH_SAME_DEVICE=1 rehearse the N-rank path on one GPU
+    # (RCCL refuses two ranks per device); the driver's runs use RCCL, one rank per GPU
+    dev_index = 0 if os.environ.get('BENCH_SAME_DEVICE') == '1' else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    device = torch.device('cuda', local_rank)
+        torch.cuda.set_device(dev_index)
+        backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
+        kw = {'device_id': torch.device('cuda', dev_index)} if backend == 'nccl' else {}
+        dist.init_process_group(backend, **kw)
+    device = torch.device('cuda', dev_index)
 
     impl = args.impl
     use_graph = not args.no_graph and (world == 1 or args.graph_ddp)

@@ -256,6 +256,9 @@ class _BNAct(torch.autograd.Function):
                 b_t[:st.C] += tot[0][:st.C]
         dy = torch.empty_like(y)
         C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+        if h is not None:   # break the output -> node -> ctx -> handle -> output cycle now
+            h.y = h.stats = h.part = None
+            ctx.handle = None
         if st.ready_hook is not None:
             st.ready_hook([t for t in (st.weight, st.bias) if t is not None])
         return (None, None, None, None, None, None, None,

@@ -261,6 +261,7 @@ class _ConvFn(torch.autograd.Function):
                 h.part = part
             else:
                 C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
+            ctx.bn_handle = None
         wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev, ctx.pro)
         bgrad = None
         if plan.bias is not None:

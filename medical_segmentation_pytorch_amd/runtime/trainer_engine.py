@@ -75,7 +75,7 @@ class FusedStep:
         self.arena.nbt.add_(1)
         C.ema_update(self.ema_arena.data, self.arena.data, self.ema_hyper)
         C.ema_update(self.ema_arena.bufdata, self.arena.bufdata, self.ema_hyper)
-        return loss
+        return loss.detach()   # the autograd graph (and every ctx it holds) dies with this step
 
     def _prepare(self):
         lr, mom = self.sched.values()

@@ -101,3 +101,22 @@ def test_syncbn_ddp_matches_single_process(gpu, tmp_path):
     print('update rel diff: split', split, 'noise floor', floor, 'loss', one['loss'], two['loss'], pert['loss'])
     assert split < 2.0 * floor + 0.05, (split, floor)
     assert abs(one['loss'] - two['loss']) < 1e-2 * abs(one['loss']), (one['loss'], two['loss'])
+
+
+def test_bench_ddp_path_two_ranks(gpu, tmp_path):
+    """The driver's multi-GPU bench invocation (torch.distributed.run, one rank per device) rehearsed
+    with 2 ranks on this one GPU over gloo: DDP bucketing + SyncBN + GPU augmentation feed + the JSON
+    contract (whole-job images/sec, n_gpus, dp2)."""
+    import json
+    s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
+    env = dict(os.environ, BENCH_DIST_BACKEND='gloo', BENCH_SAME_DEVICE='1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--steps', '3',
+           '--warmup', '2', '--batch', '2', '--size', '64', '--train-images', '8', '--val-images', '4']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(line) == 1, r.stdout   # rank 0 prints exactly one JSON line
+    d = json.loads(line[0])
+    assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'dp2' and d['config']['global_batch'] == 4
+    assert d['value'] > 0 and d['steps'] == 3 and d['warmup'] == 2 and d['config']['syncbn']
