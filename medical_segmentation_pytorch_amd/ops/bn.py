@@ -56,10 +56,11 @@ class Deferred:
     consumer kernel applies the affine+ReLU while it loads ``t`` (the "BN prologue": conv halo/igemm
     staging, weight-gradient staging, branch sums), so no ``bn_act_apply`` pass ever writes ``z``.
     :func:`materialize` turns it into a plain tensor for consumers without a prologue."""
-    __slots__ = ('t', 'stats', 'relu')
+    __slots__ = ('t', 'stats', 'relu', 'z')
 
     def __init__(self, t, stats, relu):
         self.t, self.stats, self.relu = t, stats, relu
+        self.z = None   # materialised copy, made at most once (shared by every consumer that needs it)
 
     @property
     def shape(self):
@@ -104,7 +105,9 @@ class _Materialize(torch.autograd.Function):
 def materialize(x):
     """Plain NHWC tensor of ``x`` (Deferred -> one bn_act_apply pass; tensors pass through)."""
     if isinstance(x, Deferred):
-        return _Materialize.apply(x.t, x.stats, x.relu)
+        if x.z is None:
+            x.z = _Materialize.apply(x.t, x.stats, x.relu)
+        return x.z
     return x
 
 

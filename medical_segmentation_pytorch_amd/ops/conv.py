@@ -87,6 +87,17 @@ class ConvPlan:
     def fwd_dims(self, n, ih, iw, oh, ow):
         return [n, ih, iw, self.Gi, self.Cgi, oh, ow, self.Go, self.Cgo, self.co_l, self.T, self.Kp, self.stride]
 
+    def uses_halo(self, n, ih, iw):
+        """Whether the forward of this plan on an [n, ih, iw] input runs the halo-tiled kernel."""
+        cache = self.__dict__.setdefault('_halo_cache', {})
+        key = (n, ih, iw)
+        if key not in cache:
+            oh, ow = self.out_hw(ih, iw)
+            taps = self.taps_bwd if self.transposed else self.taps_fwd
+            cache[key] = bool(require().conv_uses_halo(self.fwd_dims(n, ih, iw, oh, ow), [t[0] for t in taps],
+                                                       [t[1] for t in taps], self.transposed and self.stride > 1))
+        return cache[key]
+
     def stat_blocks(self, n, ih, iw):
         oh, ow = self.out_hw(ih, iw)
         taps = self.taps_bwd if self.transposed else self.taps_fwd
@@ -328,12 +339,21 @@ def conv(plan: ConvPlan, xs, want_stats=False, bn_handle=None):
     normalise+ReLU runs as this conv's load prologue); returns (list of Go output tensors, stat
     partials).  ``bn_handle``: the input is a BN output read by this conv only
     (see ``ops.bn.BwdStatsHandle``)."""
-    from .bn import materialize, split_inputs
+    from .bn import Deferred, materialize, split_inputs
     if not isinstance(xs, (list, tuple)):
         xs = [xs]
     assert len(xs) == plan.Gi
     if plan.transposed:
         xs = [materialize(x) for x in xs]
+    elif any(isinstance(x, Deferred) for x in xs):
+        # The implicit-GEMM (non-halo) kernel re-reads every input pixel once per tap from L2, so its
+        # prologue costs T times the affine work per pixel; from 64 channels up one normalise pass
+        # (shared by all consumers through Deferred.z) is cheaper -- measured: L3-L5 fused-8 forward
+        # +0.6 ms each with the per-k-step prologue vs ~0.05 ms for the pass.
+        n, ih, iw, _ = xs[0].shape
+        if not plan.uses_halo(n, ih, iw) and plan.Cgi >= 64:
+            xs = [materialize(x) for x in xs]
+    xs = [x.z if isinstance(x, Deferred) and x.z is not None else x for x in xs]
     ts, coefs, mask = split_inputs(xs)
     weights = [b.weight for b in plan.branches]
     extra = [plan.bias] if plan.bias is not None else []
