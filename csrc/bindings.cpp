@@ -473,6 +473,25 @@ void ce_fwd_bwd_t(const at::Tensor& logits, const at::Tensor& target, const c10:
              (int)ignore_index, cur_stream());
 }
 
+void ohem_select_t(const at::Tensor& pix, const at::Tensor& target, double thr, int64_t ignore_index,
+                   const at::Tensor& bpart, const at::Tensor& state, const at::Tensor& hist, const at::Tensor& loss) {
+  CHECK_F32(pix); CHECK_I64(target); CHECK_F32(bpart); CHECK_F32(loss); CHECK_DEV(state); CHECK_DEV(hist);
+  const long P = pix.numel();
+  TORCH_CHECK(target.numel() == P && bpart.numel() == 3 * ce_blocks(P) && loss.numel() == 1);
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() == ohem_state_words(), "state: int32 [ohem_state_words]");
+  TORCH_CHECK(hist.scalar_type() == at::kInt && hist.numel() == 256, "hist: int32 [256]");
+  ohem_select(f32(pix), target.data_ptr<int64_t>(), P, (float)thr, (int)ignore_index, f32(bpart),
+              reinterpret_cast<unsigned*>(state.data_ptr<int>()), reinterpret_cast<unsigned*>(hist.data_ptr<int>()),
+              f32(loss), cur_stream());
+}
+
+void ohem_backward_t(const at::Tensor& grad, const at::Tensor& pix, const at::Tensor& state, const at::Tensor& gup) {
+  CHECK_F32(grad); CHECK_F32(pix); CHECK_F32(gup); CHECK_DEV(state);
+  TORCH_CHECK(grad.dim() == 4 && pix.numel() == grad.size(0) * grad.size(2) * grad.size(3) && gup.numel() == 1);
+  ohem_backward(f32(grad), f32(pix), reinterpret_cast<const unsigned*>(state.data_ptr<int>()), f32(gup), grad.size(0),
+                grad.size(1), grad.size(2) * grad.size(3), cur_stream());
+}
+
 void kd_kl_fwd_bwd_t(const at::Tensor& s, const at::Tensor& t, const at::Tensor& grad, const at::Tensor& part,
                      double T) {
   CHECK_F32(s); CHECK_F32(t); CHECK_F32(grad); CHECK_F32(part);
@@ -598,6 +617,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("ce_blocks", &ce_blocks_t);
   m.def("ce_fwd_bwd", &ce_fwd_bwd_t);
   m.def("kd_kl_fwd_bwd", &kd_kl_fwd_bwd_t);
+  m.def("ohem_select", &ohem_select_t);
+  m.def("ohem_backward", &ohem_backward_t);
+  m.def("ohem_state_words", []() { return ohem_state_words(); });
   m.def("mse_fwd_bwd", &mse_fwd_bwd_t);
   m.def("bce_dice_stats", &bce_dice_stats_t);
   m.def("bce_dice_grad", &bce_dice_grad_t);

@@ -143,6 +143,13 @@ void ce_fwd_bwd(const float* logits, const int64_t* target, const float* weight,
                 float* pix_loss, float* part, int N, int C, long HW, int ignore_index, hipStream_t s);
 void kd_kl_fwd_bwd(const float* s_logits, const float* t_logits, float* grad, float* part, int N, int C,
                    long HW, float T, hipStream_t s);
+// OHEM on the device (no host sync): bpart fp32 [ce_blocks(P)][3], state uint32 [ohem_state_words()],
+// hist uint32 [256], loss fp32 [1]; backward scales the CE gradient in place by g * w(pixel)
+int ohem_state_words();
+void ohem_select(const float* pix_loss, const int64_t* target, long P, float thr, int ignore_index, float* bpart,
+                 unsigned* state, unsigned* hist, float* loss, hipStream_t s);
+void ohem_backward(float* grad, const float* pix_loss, const unsigned* state, const float* gup, int N, int C, long HW,
+                   hipStream_t s);
 // part[ce_blocks(n)] = partial sums of (s - t)^2; grad = 2 (s - t) / n
 void mse_fwd_bwd(const float* s_, const float* t, float* grad, float* part, long n, hipStream_t s);
 // binary logits / targets fp32 [N, HW]: part [N][bce_dice_splits(HW)][4]; coef [N][2]; gup device scalar

@@ -45,19 +45,28 @@ class GraphedStep:
     def __init__(self, trainer, config):
         self.t, self.config = trainer, config
         self.graph = None
-        self.images = self.masks = self.loss = None
+        self.images = self.masks = self.loss = self.kd = None
         self.calls = 0
 
     def _body(self):
-        t = self.t
+        """zero_grad -> repack -> forward -> loss (CE / device-side OHEM / BCE+Dice) [+ KD term with the
+        frozen fused teacher, reference core/seg_trainer.py:69-79] -> backward -> fused optimizer."""
+        t, config = self.t, self.config
         t.optimizer.zero_grad()
         ex = t.model.executor
         ex.repack()
         preds = t.model(self.images)
         loss = t.loss_fn(preds, self.masks)
+        kd = None
+        if config.kd_training:
+            with torch.no_grad():
+                teacher_preds = t.teacher_model(self.images)
+            kd = kd_loss_fn(config, preds.float(), teacher_preds.detach().float())
+            loss = loss + config.kd_loss_coefficient * kd
+            kd = kd.detach()
         loss.backward()
         t.optimizer.launch()
-        return loss.detach()
+        return loss.detach(), kd
 
     def __call__(self, images, masks):
         t = self.t
@@ -80,8 +89,9 @@ class GraphedStep:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
-                self.loss = self._body()
+                self.loss, self.kd = self._body()
         self.graph.replay()
+        t._last_kd = self.kd.clone() if self.kd is not None else None   # static graph output
         return self.loss
 
 
@@ -128,8 +138,11 @@ class SegTrainer(BaseTrainer):
         return loss.detach()
 
     def _use_graph(self, config):
-        return (self.fused and config.use_graph and not config.kd_training and not config.use_aux
-                and config.loss_type == 'ce' and not self.scaler.is_enabled()
+        # every loss (CE, device-side OHEM, BCE+Dice) and the KD term are capture-safe; fp16 GradScaler
+        # steps and the eager teacher fallback are not
+        kd_ok = not config.kd_training or isinstance(self.teacher_model, FusedModel)
+        return (self.fused and config.use_graph and kd_ok and not config.use_aux
+                and not self.scaler.is_enabled()
                 and (not config.DDP or config.gpu_num == 1 or config.graph_ddp))
 
     def _flush_logs(self, config, pbar=None):

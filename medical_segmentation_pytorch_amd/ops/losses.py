@@ -4,7 +4,8 @@
   (reference ``core/loss.py:30-31``): one kernel computes the loss partials and d(loss)/d(logits);
   backward is a scalar rescale, no second pass over the logits.
 * :func:`ohem_cross_entropy` == reference ``OhemCELoss`` (``core/loss.py:6-20``): the per-pixel
-  losses come from the same fused kernel; selection (threshold, top-k fallback) uses torch.
+  losses come from the same fused kernel; the selection (threshold, exact top-k fallback by radix
+  select) runs in device kernels with no host sync, so OHEM steps are graph-captured too.
 * :func:`kd_kl_div` == ``F.kl_div(log_softmax(s/T), softmax(t/T)) * T**2`` with the default
   elementwise-mean reduction (reference ``core/loss.py:42-46``).
 * :func:`kd_mse` == ``F.mse_loss(s, t)`` (reference ``core/loss.py:47-48``), one fused pass.
@@ -48,34 +49,36 @@ def cross_entropy(logits, target, weight=None, ignore_index=255):
 
 
 class _OHEM(torch.autograd.Function):
+    """Per-pixel CE from the fused kernel; hard-pixel selection (threshold, else exact top-k) entirely on
+    the device (``loss.hip`` ohem_*): no host synchronisation, so the step stays graph-capturable."""
+
     @staticmethod
     def forward(ctx, logits, target, thresh, ignore_index):
         C = require()
         logits = logits.contiguous().float()
         target = target.contiguous().long()
         n, c, h, w = logits.shape
+        dev = logits.device
         grad = torch.empty_like(logits)
-        pix = torch.empty(n * h * w, dtype=torch.float32, device=logits.device)
-        part = torch.empty(C.ce_blocks(n * h * w), 2, dtype=torch.float32, device=logits.device)
+        P = n * h * w
+        pix = torch.empty(P, dtype=torch.float32, device=dev)
+        nb = C.ce_blocks(P)
+        part = torch.empty(nb, 2, dtype=torch.float32, device=dev)
         C.ce_fwd_bwd(logits, target, None, grad, pix, part, ignore_index)
-        n_min = int((target != ignore_index).sum().item()) // 16
-        sel = pix > thresh
-        if int(sel.sum().item()) < n_min:
-            _, idx = pix.topk(n_min)
-            sel = torch.zeros_like(sel)
-            sel[idx] = True
-        cnt = sel.sum().clamp_min(1).float()
-        loss = (pix * sel).sum() / cnt
-        ctx.save_for_backward(grad, sel, cnt)
-        ctx.hw = (n, h * w)
-        return loss
+        bpart = torch.empty(nb, 3, dtype=torch.float32, device=dev)
+        state = torch.empty(C.ohem_state_words(), dtype=torch.int32, device=dev)
+        hist = torch.empty(256, dtype=torch.int32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        C.ohem_select(pix, target, thresh, ignore_index, bpart, state, hist, loss)
+        ctx.save_for_backward(grad, pix, state)
+        return loss[0]
 
     @staticmethod
     def backward(ctx, g):
-        grad, sel, cnt = ctx.saved_tensors
-        n, hw = ctx.hw
-        mask = sel.view(n, 1, hw).float() * (g / cnt)
-        return grad * mask.view(n, 1, *grad.shape[2:]), None, None, None
+        grad, pix, state = ctx.saved_tensors
+        out = grad.clone()
+        require().ohem_backward(out, pix, state, g.reshape(1).float().contiguous())
+        return out, None, None, None
 
 
 def ohem_cross_entropy(logits, target, thresh=0.7, ignore_index=255):

@@ -479,3 +479,74 @@ def test_bn_partials_from_dgrad_epilogue(gpu, relu, halo):
         C.conv_set_halo(True)
     for a, b in zip(res[0], res[1]):
         assert _rel(b, a) < 1e-3, _rel(b, a)
+
+
+def _ohem_ref(logits, tgt, thresh, ignore=255):
+    px = F.cross_entropy(logits, tgt, ignore_index=ignore, reduction='none').view(-1)
+    hard = px[px > -math.log(thresh)]
+    n_min = int((tgt != ignore).sum()) // 16
+    if hard.numel() < n_min:
+        hard, _ = px.topk(n_min)
+    return hard.mean()
+
+
+@pytest.mark.parametrize('case', ['threshold', 'topk', 'ignore', 'ties'])
+def test_ohem_device_selection(gpu, case):
+    """Device-side OHEM (threshold count + exact radix top-k, no host sync) vs the reference formula
+    (core/loss.py:13-20) in both branches, with ignored pixels and with ties at the k-th loss."""
+    from medical_segmentation_pytorch_amd.ops.losses import ohem_cross_entropy
+    torch.manual_seed(17)
+    n, h, w = 3, 40, 48
+    tgt = torch.randint(0, 2, (n, h, w), device=gpu)
+    if case == 'threshold':
+        logits = torch.randn(n, 2, h, w, device=gpu)                  # many hard pixels
+    elif case == 'topk':
+        logits = (tgt * 2 - 1).float()[:, None] * torch.tensor([-2.5, 2.5], device=gpu)[None, :, None, None]
+        logits = logits + 0.5 * torch.randn_like(logits)             # confident: few above thr
+    elif case == 'ignore':
+        logits = torch.randn(n, 2, h, w, device=gpu) * 3
+        tgt[:, :10] = 255
+    else:                                                            # every loss identical: all tied
+        tgt = torch.zeros_like(tgt)
+        logits = torch.tensor([5.0, -5.0], device=gpu)[None, :, None, None].expand(n, 2, h, w).contiguous()
+    lf = logits.clone().requires_grad_(True)
+    lr = logits.clone().requires_grad_(True)
+    loss = ohem_cross_entropy(lf, tgt, 0.7, 255)
+    ref = _ohem_ref(lr, tgt, 0.7)
+    assert abs(loss.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item())), (loss.item(), ref.item())
+    (2.0 * loss).backward()
+    (2.0 * ref).backward()
+    if case == 'ties':   # torch picks an arbitrary subset of the ties; the gradient's total agrees
+        assert _rel(lf.grad.sum((0, 2, 3)), lr.grad.sum((0, 2, 3))) < 1e-4
+    else:
+        assert _rel(lf.grad, lr.grad) < 1e-4
+
+
+def test_ohem_in_captured_graph(gpu):
+    """OHEM inside a hipGraph: replays with new data match the reference every time."""
+    from medical_segmentation_pytorch_amd.ops.losses import ohem_cross_entropy
+    torch.manual_seed(3)
+    x = torch.randn(2, 2, 32, 32, device=gpu, requires_grad=True)
+    tgt = torch.randint(0, 2, (2, 32, 32), device=gpu)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # warm-up outside the capture
+        ohem_cross_entropy(x, tgt).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    x.grad = None
+    with torch.cuda.graph(g):
+        out = ohem_cross_entropy(x, tgt)
+        out.backward()
+    for scale in (1.0, 0.05, 4.0):   # 0.05: confident logits -> the top-k branch
+        with torch.no_grad():
+            x.copy_(torch.randn_like(x) * scale)
+            tgt.copy_(torch.randint(0, 2, tgt.shape, device=gpu))
+            x.grad.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        xr = x.detach().clone().requires_grad_(True)
+        ref = _ohem_ref(xr, tgt, 0.7)
+        ref.backward()
+        assert abs(out.item() - ref.item()) < 1e-5, (scale, out.item(), ref.item())
+        assert _rel(x.grad, xr.grad) < 1e-4

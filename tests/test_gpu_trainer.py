@@ -58,3 +58,22 @@ def test_fused_optimizer_matches_torch_adam(gpu):
             s.step()
     for p, q in zip(m1.parameters(), m2.parameters()):
         assert torch.allclose(p, q, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize('mode', ['ohem', 'kd'])
+def test_trainer_graph_with_ohem_and_kd(gpu, tmp_path, mode):
+    """OHEM (device-side selection) and KD (frozen fused teacher) steps run inside the hipGraph."""
+    from medical_segmentation_pytorch_amd.core import SegTrainer
+    kw = {'loss_type': 'ohem'} if mode == 'ohem' else {}
+    if mode == 'kd':
+        from medical_segmentation_pytorch_amd.models.smp import Unet
+        teacher = Unet(encoder_name='resnet18', encoder_weights=None, in_channels=3, classes=2)
+        ck = tmp_path / 'teacher.pth'
+        torch.save({'state_dict': teacher.state_dict()}, ck)
+        kw = dict(kd_training=True, teacher_ckpt=str(ck), teacher_model='smp', teacher_encoder='resnet18',
+                  teacher_decoder='unet')
+    c = _cfg(tmp_path, engine='fused', **kw)
+    t = SegTrainer(c)
+    t.run(c)
+    assert t.graph_step is not None and t.graph_step.graph is not None
+    assert torch.isfinite(torch.tensor(t.last_loss))
