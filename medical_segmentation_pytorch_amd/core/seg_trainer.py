@@ -21,6 +21,7 @@ import torch
 from PIL import Image
 
 from ..models import get_teacher_model
+from ..ops.bn import flush_pending
 from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
 from .base_trainer import BaseTrainer
 from ..ops.resample import colorize, resize_bilinear
@@ -65,6 +66,7 @@ class GraphedStep:
             loss = loss + config.kd_loss_coefficient * kd
             kd = kd.detach()
         loss.backward()
+        flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
         t.optimizer.launch()
         return loss.detach(), kd
 
@@ -133,6 +135,7 @@ class SegTrainer(BaseTrainer):
             loss = loss + config.kd_loss_coefficient * loss_kd
             self._last_kd = loss_kd.detach()
         self.scaler.scale(loss).backward()
+        flush_pending()
         self.scaler.step(self.optimizer)
         self.scaler.update()
         return loss.detach()

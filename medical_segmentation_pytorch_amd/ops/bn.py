@@ -74,6 +74,7 @@ class Deferred:
 def split_inputs(xs):
     """(tensors, prologue coefficient list or [], relu bitmask) of a list of Tensor | Deferred."""
     ts, cs, mask = [], [], 0
+    need_stats(xs)
     for i, x in enumerate(xs):
         if isinstance(x, Deferred):
             ts.append(x.t.contiguous())
@@ -106,6 +107,7 @@ def materialize(x):
     """Plain NHWC tensor of ``x`` (Deferred -> one bn_act_apply pass; tensors pass through)."""
     if isinstance(x, Deferred):
         if x.z is None:
+            need_stats([x])
             x.z = _Materialize.apply(x.t, x.stats, x.relu)
         return x.z
     return x
@@ -121,6 +123,66 @@ class BwdStatsHandle:
     def __init__(self):
         self.y = self.stats = self.part = None
         self.relu = False
+
+
+class _Pending:
+    """SyncBN statistic exchanges waiting to leave as ONE collective.
+
+    Forward: a training BN under SyncBN reduces its local (sum, sum^2) to one fp64 row and parks
+    it here with its finalize; backward: the same for (sum dy, sum dy*xmu) with finalize + apply.
+    The queue is flushed -- ONE all-reduce over the concatenated rows, then every parked job -- by the
+    first consumer that needs a parked result (``need_stats`` / ``need_grads``: the consumer's
+    kernels read the BN coefficients or the data-gradient).  The fused executor launches sibling
+    branches level by level (``runtime.fused_model._lockstep``), so every BN of a level is parked
+    before any consumer runs, in both directions: per-BN collectives become per-level ones
+    (reference SyncBatchNorm: one all-gather per BN forward and one all-reduce per BN backward,
+    ``/root/reference/utils/parallel.py:37-38``)."""
+
+    def __init__(self):
+        self.rows, self.jobs, self.keys, self.group = [], [], set(), None
+
+    def add(self, row, group, job, key):
+        if self.rows and group is not self.group:
+            self.flush()
+        self.group = group
+        self.rows.append(row)
+        self.jobs.append(job)
+        self.keys.add(key)
+
+    def flush(self):
+        if not self.rows:
+            return
+        rows, jobs, group = self.rows, self.jobs, self.group
+        self.rows, self.jobs, self.keys, self.group = [], [], set(), None
+        buf = torch.cat([r.reshape(-1) for r in rows]) if len(rows) > 1 else rows[0].reshape(-1)
+        dist.all_reduce(buf, group=group)
+        EXCHANGES[0] += 1
+        o = 0
+        for r, job in zip(rows, jobs):
+            job(buf[o:o + r.numel()].view(1, -1))
+            o += r.numel()
+
+
+_FWD, _BWD = _Pending(), _Pending()
+EXCHANGES = [0]   # SyncBN collectives issued by this process (tests count them)
+
+
+def need_stats(xs):
+    """Flush the forward queue if any Deferred in ``xs`` has coefficients still parked in it."""
+    if _FWD.keys and any(isinstance(x, Deferred) and x.stats.data_ptr() in _FWD.keys for x in xs):
+        _FWD.flush()
+
+
+def need_grads(gs):
+    """Flush the backward queue if any incoming gradient in ``gs`` is a parked BN data-gradient."""
+    if _BWD.keys and any(g is not None and g.data_ptr() in _BWD.keys for g in gs):
+        _BWD.flush()
+
+
+def flush_pending():
+    """Issue every parked exchange (step boundaries; idempotent)."""
+    _FWD.flush()
+    _BWD.flush()
 
 
 def _world(group):
@@ -141,16 +203,19 @@ def _counters(dev):
     return t
 
 
-def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev):
+def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev, reduce=True):
     """fp64 [S, 2*Cp] split sums (finalize kernels sum the S rows); SyncBN: collapsed to one row and
-    all-reduced across the group (one RCCL call of 2*Cp doubles)."""
+    all-reduced across the group (one RCCL call of 2*Cp doubles; ``reduce=False``: the local row,
+    for the caller to park in a :class:`_Pending` queue)."""
     S = C.bn_reduce_splits(nblk)
     tmp = torch.empty(S, 2 * Cp, dtype=torch.float64, device=dev)
     C.bn_reduce_partials(part, nblk, width, col_off, Cp, tmp)
     if _world(group) > 1:
         out = torch.empty(1, 2 * Cp, dtype=torch.float64, device=dev)
         C.bn_collapse(tmp, Cp, out)
-        dist.all_reduce(out, group=group)
+        if reduce:
+            dist.all_reduce(out, group=group)
+            EXCHANGES[0] += 1
         return out
     return tmp
 
@@ -159,10 +224,14 @@ class _BNAct(torch.autograd.Function):
     # inputs: st, relu, training, part_info, handle, deferred, pro, gamma, beta, *xs  (gamma/beta are
     # inputs so that their grads reach autograd when the engine gives no grad sink).  pro = (coefs,
     # relu mask): inputs that are themselves Deferred BN outputs (their prologue runs in sum_stats).
-    # deferred: return the alias of y (the caller wraps it in a Deferred) instead of materialising z.
+    # mode = (deferred, defer_bwd).  deferred: return the alias of y (the caller wraps it in a Deferred)
+    # instead of materialising z.  defer_bwd: under SyncBN, park the backward exchange (the caller
+    # guarantees every input is read only by this BN, so the returned data-gradient reaches one of
+    # our backward functions -- which flush -- and never an autograd accumulation).
     @staticmethod
-    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, deferred, pro, gamma, beta, *xs):
+    def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, mode, pro, gamma, beta, *xs):
         C = require()
+        deferred, defer_bwd = mode
         xs = [x.contiguous() for x in xs]
         coefs, rmask = pro
         y0 = xs[0]
@@ -189,10 +258,15 @@ class _BNAct(torch.autograd.Function):
                 tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
                 C.bn_reduce_finalize(part, nblk, width, col_off, st.C, Cp, tmp, _counters(dev), count, g_, b_,
                                      st.running_mean, st.running_var, st.momentum, st.eps, stats)
-            else:            # SyncBN: collapse, RCCL all-reduce, finalize
-                sums = _channel_sums(C, part, nblk, width, col_off, Cp, st.group, dev)
-                C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
-                              st.eps, True, stats)
+            else:            # SyncBN: collapse, park (one all-reduce per level), finalize on flush
+                row = _channel_sums(C, part, nblk, width, col_off, Cp, st.group, dev, reduce=False)
+
+                def job(sums, st=st, Cp=Cp, count=count, g_=g_, b_=b_, stats=stats):
+                    C.bn_finalize(sums, st.C, Cp, count, g_, b_, st.running_mean, st.running_var, st.momentum,
+                                  st.eps, True, stats)
+                _FWD.add(row, st.group, job, stats.data_ptr())
+                if not deferred:   # z is normalised right here
+                    _FWD.flush()
             if st.count_nbt and st.num_batches_tracked is not None:
                 st.num_batches_tracked.add_(1)
         else:
@@ -203,6 +277,7 @@ class _BNAct(torch.autograd.Function):
                           st.eps, False, stats)
             count = float(P)
         ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
+        ctx.defer_bwd = defer_bwd
         ctx.handle = handle if training else None
         if ctx.handle is not None:
             handle.y, handle.stats, handle.relu, handle.part = y, stats, relu, None
@@ -217,6 +292,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, _dstats=None):
         C = require()
+        need_grads([dz])
         y, stats = ctx.saved_tensors
         st: BNState = ctx.st
         dz = dz.contiguous()
@@ -233,7 +309,12 @@ class _BNAct(torch.autograd.Function):
             C.bn_act_bwd_partial(dz, y, stats, part, P, Cp, ctx.relu)
         world = _world(st.group) if ctx.training else 1
         fused = ctx.training and world == 1
-        sums = None if fused else _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev)
+        # park the exchange only when nothing reads this backward's outputs before the flush: dy goes to
+        # our own backward functions (defer_bwd) and dgamma/dbeta to arena sinks, not to autograd
+        park = (ctx.training and world > 1 and ctx.defer_bwd and (st.weight is None or st.weight_sink is not None)
+                and (st.bias is None or st.bias_sink is not None))
+        sums = None if fused else _channel_sums(C, part, nblk, Cp, 0, Cp, st.group if ctx.training else None, dev,
+                                                reduce=not park)
         need_g = ctx.needs_input_grad[7] and st.weight_sink is None
         need_b = ctx.needs_input_grad[8] and st.bias_sink is None
         dgamma = torch.zeros(Cp, dtype=torch.float32, device=dev) if need_g else None
@@ -241,6 +322,20 @@ class _BNAct(torch.autograd.Function):
         g_t = st.weight_sink if st.weight_sink is not None else dgamma
         b_t = st.bias_sink if st.bias_sink is not None else dbeta
         coef = torch.empty(3, Cp, dtype=torch.float32, device=dev)
+        if park:
+            dy = torch.empty_like(y)
+            relu, count, hook = ctx.relu, ctx.count, st.ready_hook
+
+            def job(sums, st=st, Cp=Cp, P=P):
+                C.bn_bwd_finalize(sums, st.C, Cp, count, stats, g_t, b_t, coef, 1.0 / world)
+                C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, relu)
+                if hook is not None:
+                    hook([t for t in (st.weight, st.bias) if t is not None])
+            _BWD.add(sums, st.group, job, dy.data_ptr())
+            if h is not None:
+                h.y = h.stats = h.part = None
+                ctx.handle = None
+            return (None,) * 9 + (dy,) * ctx.k
         if fused:            # one launch: column reduction + backward finalize (last-arriving block)
             tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
             C.bn_reduce_bwd_finalize(part, nblk, st.C, Cp, tmp, _counters(dev), ctx.count, stats, g_t, b_t, coef, 1.0)
@@ -269,15 +364,19 @@ class _BNAct(torch.autograd.Function):
                 dbeta[:st.C] if dbeta is not None else None) + (dy,) * ctx.k
 
 
-def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None, deferred=False):
+def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None, deferred=False,
+           defer_bwd=False):
     """act(BN(sum(xs))) for NHWC bf16 feature maps (``xs``: tensors and/or :class:`Deferred` BN
     outputs).  ``part_info = (part, width, col_off)`` reuses conv-epilogue channel partials (single
     plain input only); ``handle``: see :class:`BwdStatsHandle`.  ``deferred=True`` returns a
-    :class:`Deferred` (no normalise pass) -- only for callers whose consumers all take prologues."""
+    :class:`Deferred` (no normalise pass) -- only for callers whose consumers all take prologues.
+    ``defer_bwd=True``: every input is read by this BN only (SyncBN backward exchange may be parked,
+    see :class:`_Pending`)."""
     if isinstance(xs, (torch.Tensor, Deferred)):
         xs = [xs]
     ts, coefs, mask = split_inputs(xs)
-    out, stats = _BNAct.apply(st, relu, training, part_info, handle, deferred, (coefs, mask), st.weight, st.bias, *ts)
+    out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd), (coefs, mask),
+                              st.weight, st.bias, *ts)
     return Deferred(out, stats, relu) if deferred else out
 
 

@@ -243,7 +243,9 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        from .bn import need_grads
         C = require()
+        need_grads(grads)
         plan: ConvPlan = ctx.plan
         xs = list(ctx.saved_tensors)
         n, ih, iw, oh, ow = ctx.shape

@@ -68,7 +68,9 @@ class _Up2Add(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        from .bn import need_grads
         C = require()
+        need_grads([g])
         n, h, w, cp = ctx.shape
         g = g.contiguous()
         dlow = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=g.device)

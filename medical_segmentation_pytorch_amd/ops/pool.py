@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import require
+from .bn import need_grads
 from .fm import cpad
 
 
@@ -32,6 +33,7 @@ class _MaxPool(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         C = require()
+        need_grads([g])
         (idx,) = ctx.saved_tensors
         k, s, p, shape = ctx.cfg
         dx = torch.empty(shape, dtype=torch.bfloat16, device=g.device)
@@ -53,6 +55,7 @@ class _Up2Cat(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         C = require()
+        need_grads([g])
         lshape, sshape, cl, cs = ctx.cfg
         g = g.contiguous()
         dlow = torch.empty(lshape, dtype=torch.bfloat16, device=g.device)
@@ -75,6 +78,7 @@ class _AddAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dz):
+        need_grads([dz])
         if not ctx.relu:
             return dz, dz, None
         C = require()

@@ -164,6 +164,8 @@ class GradBucketer:
         self.works.append((b, dist.all_reduce(buf, group=self.group, async_op=True)))
 
     def finish(self):
+        from ..ops.bn import flush_pending
+        flush_pending()   # parked SyncBN backward jobs report their gamma/beta grads ready
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)

@@ -24,7 +24,7 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BNState, BwdStatsHandle, Deferred, bn_act, materialize
+from ..ops.bn import BNState, BwdStatsHandle, Deferred, bn_act, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
@@ -34,6 +34,8 @@ from ..ops.pool import add_act, maxpool, up2_cat
 _BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
 # env MSP_DEFER_BN=0 materialises every BN output (bn_act_apply pass) instead of deferring it (A/B switch)
 _DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
+# env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
+_LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 
 
 def _is_relu(act_mod):
@@ -145,7 +147,8 @@ class FusedExecutor:
     def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
         """Deferred bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
         h = BwdStatsHandle() if (single and training and _BN_EPILOGUE) else None
-        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=_DEFER_BN)
+        # every caller's inputs are conv outputs / BN outputs read by this BN only -> defer_bwd
+        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=_DEFER_BN, defer_bwd=True)
         key = z.t if isinstance(z, Deferred) else z
         if h is not None:
             self._handles[id(key)] = (key, h)
@@ -171,21 +174,100 @@ class FusedExecutor:
                             (part, plan.rows, g * plan.Cgo) if training else None, single)
 
     def residual(self, m, x, training, single_out=False):
+        return self._lockstep([self._g_residual(m, x, training, single_out)])[0]
+
+    # -- level-synchronous branch scheduling ----------------------------------------------------------
+    # A branch is a generator that yields at the end of each PHASE, alternating "conv" (launch this
+    # level's conv, possibly none) and "bn" (this level's BN).  _lockstep advances sibling branches one
+    # phase at a time, so all convs of a level launch before all of its BNs.  Under SyncBN that parks
+    # the level's statistic exchanges together (ops.bn._Pending: ONE collective per level instead of one
+    # per BN); and since autograd runs ready nodes in reverse creation order, the backward reaches every
+    # BN of a level before any conv of it, which batches the backward exchanges the same way.
+    def _g_cba(self, m, x, training, single=False):
+        xs = x if isinstance(x, (list, tuple)) else [x]
+        plan = self.plan_conv(m[0], gi=len(xs))
+        (y,), part = self._conv(plan, xs, training)
+        yield
+        z = self._bn_out([y], self.bn(m[1]), _is_relu(m[2]), training, (part, plan.rows, 0) if training else None,
+                         single)
+        yield
+        return z
+
+    @staticmethod
+    def _g_bn(fn):
+        yield                # no conv at this level
+        z = fn()
+        yield
+        return z
+
+    def _g_residual_tail(self, m, upper_y, low_fn, training, single_out=False):
+        """ResidualBlock whose fused 3x3+1x1 launch already ran: (low BN) -> cba -> bn(upper + lower)."""
+        low = yield from self._g_bn(low_fn)
+        low = yield from self._g_cba(m.lower_branch[1], low, training)
+        return (yield from self._g_bn(lambda: self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]),
+                                                            training, single=single_out)))
+
+    def _g_residual(self, m, x, training, single_out=False):
         plan = self.plan_fused3x3(('res', id(m)), [m.lower_branch[0][0]], [m.upper_branch])
         ys, part = self._conv(plan, [x], training)
-        low = self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0, training,
-                                 single=True)
-        low = self.cba(m.lower_branch[1], low, training)
-        return self._bn_out([ys[1], low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training, single=single_out)
+        low_fn = lambda: self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0,  # noqa: E731
+                                            training, single=True)
+        return (yield from self._g_residual_tail(m, ys[1], low_fn, training, single_out))
 
-    def _residual_tail(self, m, upper_y, low_z, training, single_out=False):
-        low = self.cba(m.lower_branch[1], low_z, training)
-        return self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]), training, single=single_out)
+    def _g_chain(self, first, blocks, training):
+        """``first`` (a branch generator) followed by residual ``blocks``, each feeding the next only."""
+        o = yield from first
+        for k, blk in enumerate(blocks):
+            o = yield from self._g_residual(blk, o, training, single_out=k + 1 < len(blocks))
+        return o
 
-    def duck(self, m, xs, training):
+    def _g_parallel(self, gens):
+        res = [None] * len(gens)
+        if not self._level_sync():   # nothing to batch: plain depth-first order
+            for i, g in enumerate(gens):
+                while True:
+                    try:
+                        next(g)
+                    except StopIteration as e:
+                        res[i] = e.value
+                        break
+            return res
+        live = list(range(len(gens)))
+        while live:
+            nxt = []
+            for i in live:
+                try:
+                    next(gens[i])
+                    nxt.append(i)
+                except StopIteration as e:
+                    res[i] = e.value
+            live = nxt
+            if live:
+                yield
+        return res
+
+    def _level_sync(self):
+        """Level-synchronous order only where it batches something: SyncBN over > 1 rank (env
+        MSP_LOCKSTEP=1 forces it, =0 disables it)."""
+        if _LOCKSTEP is not None:
+            return _LOCKSTEP
+        g = self.group
+        return g is not None and torch.distributed.is_initialized() and torch.distributed.get_world_size(g) > 1
+
+    def _lockstep(self, gens):
+        g = self._g_parallel(gens)
+        while True:
+            try:
+                next(g)
+            except StopIteration as e:
+                return e.value
+
+    def _g_duck(self, m, xs, training):
         """DUCK block over in_bn(sum(xs)): the encoder's ``x_i + x`` merge rides in in_bn's statistics
-        pass (both summands are deferred BN outputs)."""
-        xb = bn_act(xs, self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training, deferred=_DEFER_BN)
+        pass (both summands are deferred BN outputs).  in_bn's inputs may have other readers, so its
+        backward exchange is never parked."""
+        xb = yield from self._g_bn(lambda: bn_act(xs, self.bn(m.in_bn[0]), _is_relu(m.in_bn[1]), training,
+                                                  deferred=_DEFER_BN))
         b1, b2, b3, b4, b5, b6 = m.branches()
         r4, r5 = b4[0], b5[0]
         convs3 = [b1[0][0], b2[0][0], b3.lower_branch[0][0], r4.lower_branch[0][0], r5.lower_branch[0][0]]
@@ -193,28 +275,41 @@ class FusedExecutor:
         plan = self.plan_fused3x3(('duck', id(m)), convs3, convs1)
         ys, part = conv(plan, [xb], want_stats=training)
         # every first-conv BN output feeds one conv only (single=True); branch outputs feed the 6-way sum
-        bnz = lambda seq, g: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training, single=True)  # noqa: E731
-        # widescope: d1 -> d2 -> d3 ; midscope: d1 -> d2
-        o1 = bnz(b1[0], 0)
-        o1 = self.cba(b1[1], o1, training, single=True)
-        o1 = self.cba(b1[2], o1, training)
-        o2 = bnz(b2[0], 1)
-        o2 = self.cba(b2[1], o2, training)
-        # residual x1 / x2 / x3 (first block's two convs come from the fused launch); inside a chain
-        # a block's output feeds only the next block's fused conv
-        o3 = self._residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training)
+        def bnz(seq, g):
+            return lambda: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training, single=True)
+
+        def wide():      # d1 -> d2 -> d3
+            o = yield from self._g_bn(bnz(b1[0], 0))
+            o = yield from self._g_cba(b1[1], o, training, single=True)
+            return (yield from self._g_cba(b1[2], o, training))
+
+        def mid():       # d1 -> d2
+            o = yield from self._g_bn(bnz(b2[0], 1))
+            return (yield from self._g_cba(b2[1], o, training))
+
+        def sep():       # 1x7 -> 7x1
+            o = yield from self._g_cba(b6[0], xb, training, single=True)
+            return (yield from self._g_cba(b6[1], o, training))
+
         rest4, rest5 = list(b4)[1:], list(b5)[1:]
-        o4 = self._residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training, single_out=bool(rest4))
-        for k, blk in enumerate(rest4):
-            o4 = self.residual(blk, o4, training, single_out=k + 1 < len(rest4))
-        o5 = self._residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training, single_out=bool(rest5))
-        for k, blk in enumerate(rest5):
-            o5 = self.residual(blk, o5, training, single_out=k + 1 < len(rest5))
-        # separated 1x7 -> 7x1
-        o6 = self.cba(b6[0], xb, training, single=True)
-        o6 = self.cba(b6[1], o6, training)
-        return bn_act([o1, o2, o3, o4, o5, o6], self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training,
-                      deferred=_DEFER_BN)
+        # residual x1 / x2 / x3: the first block's two convs come from the fused launch; inside a chain a
+        # block's output feeds only the next block's fused conv
+        branches = [wide(), mid(),
+                    self._g_residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training),
+                    self._g_chain(self._g_residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training,
+                                                        single_out=bool(rest4)), rest4, training),
+                    self._g_chain(self._g_residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training,
+                                                        single_out=bool(rest5)), rest5, training),
+                    sep()]
+        outs = yield from self._g_parallel(branches)
+        return (yield from self._g_bn(lambda: bn_act(outs, self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training,
+                                                     deferred=_DEFER_BN, defer_bwd=True)))
+
+    def duck(self, m, xs, training, extra=()):
+        """DUCK block; ``extra``: independent branch generators scheduled level-synchronously with it
+        (their results follow the block's output in the returned list when given)."""
+        res = self._lockstep([self._g_duck(m, xs, training)] + list(extra))
+        return res if extra else res[0]
 
     def head(self, conv_mod, x, num_class):
         plan = self.plan_conv(conv_mod)
@@ -226,14 +321,13 @@ class FusedExecutor:
         x = to_fm(images)
         stages = model.down_stages()
         s1 = stages[0]
-        shortcut = self.cba(s1.conv2, x, training)
-        skip = self.duck(s1.duck, [x], training)
+        skip, shortcut = self.duck(s1.duck, [x], training, extra=[self._g_cba(s1.conv2, x, training)])
         down = self.cba(s1.conv1, skip, training)
         skips = [skip]
         for st in stages[1:]:
-            nxt = self.cba(st.conv2, shortcut, training)
-            skip = self.duck(st.duck, [down, shortcut], training)   # x_i + x inside in_bn's stats pass
-            shortcut = nxt
+            # x_i + x inside in_bn's stats pass; the next shortcut conv runs level-synchronously with it
+            skip, shortcut = self.duck(st.duck, [down, shortcut], training,
+                                       extra=[self._g_cba(st.conv2, shortcut, training)])
             down = self.cba(st.conv1, skip, training)
             skips.append(skip)
         x = add_n(down, shortcut)
@@ -317,6 +411,7 @@ class FusedExecutor:
             return self._forward(images, training)
         finally:
             self._handles.clear()
+            flush_pending()
 
     def _forward(self, images, training=None):
         model = self.model

@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops._ext import require
+from ..ops.bn import flush_pending
 from ..ops.losses import cross_entropy, kd_kl_div
 from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, StagedScalars, stat_group
 from .fused_model import FusedExecutor
@@ -69,6 +70,7 @@ class FusedStep:
                 t_out = self.teacher(self.images, training=False)
             loss = loss + self.kd_coef * kd_kl_div(out, t_out, self.kd_temperature)
         loss.backward()
+        flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
         if self.bucketer is not None:
             self.bucketer.finish()
         self.opt.step()

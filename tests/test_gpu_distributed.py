@@ -38,8 +38,12 @@ names = [n for n, _ in model.named_parameters()]
 step = FusedStep(model, xs, ys, optimizer='sgd', lr=0.05, momentum=0.0, use_graph=False,
                  distributed=world > 1, syncbn=True, bucket_cap_mb=0.5)
 step.sched.max_lr = 0.05
+from medical_segmentation_pytorch_amd.ops import bn as bnmod
+ex0 = bnmod.EXCHANGES[0]
 loss = step()
 torch.cuda.synchronize()
+exchanges = bnmod.EXCHANGES[0] - ex0
+n_bn = sum(isinstance(m, torch.nn.BatchNorm2d) for m in model.modules())
 loss = torch.tensor([float(loss)])
 dist.all_reduce(loss)                     # mean of the per-rank half-batch losses == full-batch loss
 loss = loss / world
@@ -47,8 +51,8 @@ if rank == 0:
     upd = [p.detach().float().cpu() - a for p, a in zip(model.parameters(), w0)]   # the SGD update
     w = torch.cat([u.flatten() for u in upd])
     rms = [b.detach().float().cpu() for n, b in model.named_buffers() if 'running_mean' in n]
-    torch.save({'w': w, 'upd': upd, 'names': names, 'rm': torch.cat(rms), 'rms': rms, 'loss': float(loss)},
-               os.environ['OUT'])
+    torch.save({'w': w, 'upd': upd, 'names': names, 'rm': torch.cat(rms), 'rms': rms, 'loss': float(loss),
+                'exchanges': exchanges, 'n_bn': n_bn}, os.environ['OUT'])
 dist.destroy_process_group()
 '''
 
@@ -101,6 +105,11 @@ def test_syncbn_ddp_matches_single_process(gpu, tmp_path):
     print('update rel diff: split', split, 'noise floor', floor, 'loss', one['loss'], two['loss'], pert['loss'])
     assert split < 2.0 * floor + 0.05, (split, floor)
     assert abs(one['loss'] - two['loss']) < 1e-2 * abs(one['loss']), (one['loss'], two['loss'])
+    # level-synchronous SyncBN exchanges: one collective per dependency level and direction instead of
+    # one per BN and direction (reference SyncBatchNorm: 2 per BN)
+    print('SyncBN collectives per step:', two['exchanges'], 'for', two['n_bn'], 'BNs')
+    assert one['exchanges'] == 0
+    assert 0 < two['exchanges'] <= 0.5 * 2 * two['n_bn'], (two['exchanges'], two['n_bn'])
 
 
 def test_bench_ddp_path_two_ranks(gpu, tmp_path):
