@@ -208,7 +208,21 @@ class MobileNetV2Encoder(nn.Module):
         return out
 
     def make_dilated(self, output_stride):
-        raise ValueError('MobileNetV2 encoder does not support dilated mode in this framework')
+        """smp ``replace_strides_with_dilation`` over the last stage(s) (DeepLabV3/V3+, PAN)."""
+        stages = self.get_stages()
+        if output_stride == 16:
+            plan = [(stages[5], 2)]
+        elif output_stride == 8:
+            plan = [(stages[4], 2), (stages[5], 4)]
+        else:
+            raise ValueError(f'output stride should be 16 or 8, got {output_stride}')
+        for stage, rate in plan:
+            for m in stage.modules():
+                if isinstance(m, nn.Conv2d):
+                    m.stride = (1, 1)
+                    m.dilation = (rate, rate)
+                    kh, kw = m.kernel_size
+                    m.padding = ((kh // 2) * rate, (kw // 2) * rate)
 
 
 ENCODERS = {

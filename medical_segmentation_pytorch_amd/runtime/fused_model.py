@@ -382,20 +382,39 @@ class FusedExecutor:
             o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=False)
         return add_act(materialize(o), materialize(idt), relu=True)
 
-    def resnet_unet(self, model, images, training):
-        enc, dec = model.encoder, model.decoder
+    def resnet_encoder(self, enc, images, training):
+        """smp ResNet encoder stages 1..depth as NHWC bf16 feature maps (dilated output-stride-8/16
+        variants included: their stride-1 dilated convs are ordinary fused convs)."""
         x = to_fm(images)
         f1 = materialize(self.conv_bn(enc.conv1, enc.bn1, x, training, relu=True))
-        mp = enc.maxpool
-        x = maxpool(f1, _pair(mp.kernel_size)[0], _pair(mp.stride)[0], _pair(mp.padding)[0])
         feats = [f1]
-        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+        if enc._depth >= 2:
+            mp = enc.maxpool
+            x = maxpool(f1, _pair(mp.kernel_size)[0], _pair(mp.stride)[0], _pair(mp.padding)[0])
+        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4)[:max(enc._depth - 1, 0)]:
             for blk in layer:
                 x = self.resnet_block(blk, x, training)
             feats.append(x)
+        return feats
+
+    def smp_hybrid(self, model, images, training):
+        """Any smp decoder (FPN, DeepLabV3/V3+, Linknet, MAnet, PAN, PSPNet, Unet++) over a ResNet
+        encoder: the encoder -- the bulk of the FLOPs -- runs on the fused kernels, the decoder and head
+        eagerly under bf16 autocast on the NCHW features (reference ``models/__init__.py:8-10,23-25``)."""
+        enc = model.encoder
+        feats = self.resnet_encoder(enc, images, training)
+        chans = list(enc.out_channels[1:])
+        nchw = [images] + [from_fm(f, c) for f, c in zip(feats, chans)]
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=images.is_cuda):
+            out = model.segmentation_head(model.decoder(*nchw))
+        return out.float()
+
+    def resnet_unet(self, model, images, training):
+        enc, dec = model.encoder, model.decoder
+        feats = self.resnet_encoder(enc, images, training)
         chans = list(enc.out_channels[1:])
         skips, skip_ch = feats[:-1][::-1], chans[:-1][::-1]
-        cx = chans[-1]
+        x, cx = feats[-1], chans[-1]
         for i, blk in enumerate(dec.blocks):
             skip = skips[i] if i < len(skips) else None
             cs = skip_ch[i] if skip is not None else 0
@@ -423,20 +442,31 @@ class FusedExecutor:
             return self.unet(model, images, training)
         if _is_resnet_unet(model):
             return self.resnet_unet(model, images, training)
+        if _is_resnet_smp(model):
+            return self.smp_hybrid(model, images, training)
         raise NotImplementedError(f'no fused executor for {name}')
 
     __call__ = forward
 
 
-def _is_resnet_unet(model) -> bool:
-    """smp ``Unet`` over a (non-grouped, stride-32) ResNet encoder with BatchNorm decoder blocks."""
-    from ..models.smp import ResNetEncoder, SegmentationModel, UnetDecoder
+def _is_resnet_smp(model) -> bool:
+    """smp model over a non-grouped ResNet encoder (any decoder; dilated encoders included)."""
+    from ..models.smp import ResNetEncoder, SegmentationModel
     if not isinstance(model, SegmentationModel):
         return False
-    enc, dec = getattr(model, 'encoder', None), getattr(model, 'decoder', None)
-    if not isinstance(enc, ResNetEncoder) or not isinstance(dec, UnetDecoder) or enc._depth != 5:
+    enc = getattr(model, 'encoder', None)
+    if not isinstance(enc, ResNetEncoder) or enc._depth < 1:
         return False
-    if any(isinstance(m, nn.Conv2d) and m.groups != 1 for m in enc.modules()):
+    return not any(isinstance(m, nn.Conv2d) and m.groups != 1 for m in enc.modules())
+
+
+def _is_resnet_unet(model) -> bool:
+    """smp ``Unet`` over a (non-grouped, stride-32) ResNet encoder with BatchNorm decoder blocks."""
+    from ..models.smp import UnetDecoder
+    if not _is_resnet_smp(model):
+        return False
+    enc, dec = model.encoder, model.decoder
+    if not isinstance(dec, UnetDecoder) or enc._depth != 5:
         return False
     if any(_pair(m.dilation) != (1, 1) for m in enc.modules() if isinstance(m, nn.Conv2d)):
         return False
@@ -446,5 +476,12 @@ def _is_resnet_unet(model) -> bool:
     return all(isinstance(b.conv1[1], nn.BatchNorm2d) for b in dec.blocks)
 
 
+def eager_parts(model):
+    """Attribute names of the sub-modules the fused executor runs eagerly (hybrid smp models)."""
+    if type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_unet(model) or not _is_resnet_smp(model):
+        return []
+    return ['decoder', 'segmentation_head']
+
+
 def supports(model) -> bool:
-    return type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_unet(model)
+    return type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_smp(model)

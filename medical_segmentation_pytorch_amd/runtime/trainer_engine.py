@@ -123,7 +123,8 @@ class FusedStep:
 
 def make_model(model_name, base_channel=17, num_class=2):
     """Bench/test model zoo: 'ducknet' (DUCKNet-<base_channel>), 'unet' (UNet-<base_channel>),
-    'smp-<encoder>' (smp Unet over a ResNet encoder, e.g. 'smp-resnet18', 'smp-resnet101')."""
+    'smp-<encoder>' (smp Unet over a ResNet encoder, e.g. 'smp-resnet18', 'smp-resnet101'),
+    'smp-<decoder>-<encoder>' (any smp decoder, e.g. 'smp-fpn-resnet18', 'smp-deeplabv3plus-resnet50')."""
     from ..models.ducknet import DuckNet
     from ..models.smp import Unet
     from ..models.unet import UNet
@@ -132,6 +133,12 @@ def make_model(model_name, base_channel=17, num_class=2):
     if model_name == 'unet':
         return UNet(num_class=num_class, n_channel=3, base_channel=base_channel)
     if model_name.startswith('smp-'):
+        parts = model_name.split('-')
+        if len(parts) == 3:   # smp-<decoder>-<encoder>, e.g. smp-fpn-resnet18 (fused encoder, eager decoder)
+            from ..models import smp
+            arch = {n.lower(): n for n in ('Unet', 'UnetPlusPlus', 'FPN', 'Linknet', 'MAnet', 'PAN', 'PSPNet',
+                                           'DeepLabV3', 'DeepLabV3Plus')}[parts[1]]
+            return getattr(smp, arch)(encoder_name=parts[2], encoder_weights=None, in_channels=3, classes=num_class)
         return Unet(encoder_name=model_name[4:], encoder_weights=None, in_channels=3, classes=num_class)
     raise ValueError(f'unknown model {model_name!r}')
 

@@ -107,6 +107,12 @@ def parallel_model(config, model, rank, device, optimizer=None):
                                     compress=getattr(config, 'grad_compress', None))
             optimizer.attach_bucketer(bucketer)
         from ..runtime.engine import stat_group
+        from ..runtime.fused_model import eager_parts
+        if group is not None and config.synBN:
+            # modules that run eagerly inside the fused model (smp decoders over a fused encoder): torch
+            # SyncBatchNorm on the same group (parameters / buffers are kept, so arena views survive)
+            for name in eager_parts(model):
+                setattr(model, name, nn.SyncBatchNorm.convert_sync_batchnorm(getattr(model, name), group))
         return FusedModel(model, group=stat_group(group) if config.synBN else None,
                           sinks=arena.sinks() if arena is not None else None,
                           ready_hook=bucketer.ready if bucketer is not None else None)
