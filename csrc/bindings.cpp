@@ -528,17 +528,35 @@ void bce_dice_grad_t(const at::Tensor& x, const at::Tensor& t, const at::Tensor&
 
 int64_t bce_dice_splits_t(int64_t HW) { return bce_dice_splits(HW); }
 
-void adam_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
-                 const at::Tensor& hyper, bool adamw) {
-  CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(hyper);
-  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel() && hyper.numel() >= 8);
-  adam_step(f32(p), f32(g), f32(m), f32(v), f32(hyper), p.numel(), adamw ? 1 : 0, cur_stream());
+static const float* amp_ptr(const c10::optional<at::Tensor>& amp) {
+  if (amp.has_value()) { CHECK_F32(*amp); TORCH_CHECK(amp->numel() >= 4); }
+  return f32_opt(amp);
 }
 
-void sgd_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, const at::Tensor& hyper) {
+void adam_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+                 const at::Tensor& hyper, bool adamw, const c10::optional<at::Tensor>& amp) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(hyper);
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel() && hyper.numel() >= 8);
+  adam_step(f32(p), f32(g), f32(m), f32(v), f32(hyper), p.numel(), adamw ? 1 : 0, amp_ptr(amp), cur_stream());
+}
+
+void sgd_step_t(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, const at::Tensor& hyper,
+                const c10::optional<at::Tensor>& amp) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(buf); CHECK_F32(hyper);
   TORCH_CHECK(g.numel() == p.numel() && buf.numel() == p.numel() && hyper.numel() >= 4);
-  sgd_step(f32(p), f32(g), f32(buf), f32(hyper), p.numel(), cur_stream());
+  sgd_step(f32(p), f32(g), f32(buf), f32(hyper), p.numel(), amp_ptr(amp), cur_stream());
+}
+
+void amp_check_t(const at::Tensor& g, const at::Tensor& amp) {
+  CHECK_F32(g); CHECK_F32(amp);
+  TORCH_CHECK(amp.numel() >= 4);
+  amp_check(f32(g), g.numel(), f32(amp), cur_stream());
+}
+
+void amp_update_t(const at::Tensor& amp, double growth, double backoff, int64_t interval) {
+  CHECK_F32(amp);
+  TORCH_CHECK(amp.numel() >= 4 && interval >= 1);
+  amp_update(f32(amp), (float)growth, (float)backoff, (int)interval, cur_stream());
 }
 
 void ema_update_t(const at::Tensor& ema, const at::Tensor& model, const at::Tensor& hyper) {
@@ -624,8 +642,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bce_dice_stats", &bce_dice_stats_t);
   m.def("bce_dice_grad", &bce_dice_grad_t);
   m.def("bce_dice_splits", &bce_dice_splits_t);
-  m.def("adam_step", &adam_step_t);
-  m.def("sgd_step", &sgd_step_t);
+  m.def("adam_step", &adam_step_t, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("hyper"),
+        py::arg("adamw"), py::arg("amp") = py::none());
+  m.def("sgd_step", &sgd_step_t, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("hyper"),
+        py::arg("amp") = py::none());
+  m.def("amp_check", &amp_check_t);
+  m.def("amp_update", &amp_update_t);
   m.def("ema_update", &ema_update_t);
   m.def("confmat_update", &confmat_update_t);
 }

@@ -160,8 +160,10 @@ void bce_dice_grad(const float* x, const float* t, const float* coef, const floa
 
 // optim.hip  (flat fp32 buffers; hyper = device fp32 array, see optim.hip for the layout)
 void adam_step(float* p, const float* g, float* m, float* v, const float* hyper, long n, int adamw,
-               hipStream_t s);
-void sgd_step(float* p, const float* g, float* buf, const float* hyper, long n, hipStream_t s);
+               const float* amp, hipStream_t s);
+void sgd_step(float* p, const float* g, float* buf, const float* hyper, long n, const float* amp, hipStream_t s);
+void amp_check(const float* g, long n, float* amp, hipStream_t s);
+void amp_update(float* amp, float growth, float backoff, int interval, hipStream_t s);
 void ema_update(float* ema, const float* model, const float* hyper, long n, hipStream_t s);
 
 // metrics.hip

@@ -25,6 +25,7 @@ from ..models import get_model
 from ..utils import (de_parallel, destroy_ddp_process, get_ema_model, get_logger, get_optimizer, get_scheduler,
                      get_writer, log_config, mkdir, parallel_model, save_config, set_device, set_seed, use_fused)
 from ..utils.model_ema import ModelEmaV2
+from ..utils.optimizer import FusedGradScaler
 from .loss import get_loss_fn
 
 
@@ -45,13 +46,17 @@ class BaseTrainer:
         self.main_rank = (group_rank(config) == 0) if config.DDP else True
         self.logger = get_logger(config, self.main_rank)
         amp_fp16 = config.amp_training and config.amp_dtype == 'fp16' and self.device.type == 'cuda'
-        self.scaler = torch.amp.GradScaler('cuda', enabled=amp_fp16)
         if self.main_rank:
             mkdir(config.save_dir)
         set_seed(config.random_seed)
         self.model = get_model(config).to(self.device)
         config._fused = use_fused(config, self.model, self.device)
         self.fused = config._fused
+        # fp16 loss scaling: torch GradScaler on the eager engine; on the fused engine the same semantics
+        # with device-side state inside the captured step (the fused kernels compute in bf16, so overflow
+        # skips are rare, but the reference's fp16 protocol -- scaled loss, skipped steps -- is kept)
+        self.scaler = FusedGradScaler(self.device, enabled=amp_fp16) if self.fused \
+            else torch.amp.GradScaler('cuda', enabled=amp_fp16)
         if self.fused and not config.DDP and config.gpu_num > 1:
             # The reference's single-process DP (`train_bs *= gpu_num`, lr * gpu_num;
             # reference utils/parallel.py:26-27,40-42) has no fused equivalent: the fused engine is one

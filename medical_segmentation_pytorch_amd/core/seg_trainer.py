@@ -65,9 +65,10 @@ class GraphedStep:
             kd = kd_loss_fn(config, preds.float(), teacher_preds.detach().float())
             loss = loss + config.kd_loss_coefficient * kd
             kd = kd.detach()
-        loss.backward()
+        t.scaler.scale(loss).backward()
         flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
-        t.optimizer.launch()
+        t.optimizer.launch(t.scaler)   # fp16 AMP: finite check + unscale / skip inside the graph
+        t.scaler.update()
         return loss.detach(), kd
 
     def __call__(self, images, masks):
@@ -141,11 +142,10 @@ class SegTrainer(BaseTrainer):
         return loss.detach()
 
     def _use_graph(self, config):
-        # every loss (CE, device-side OHEM, BCE+Dice) and the KD term are capture-safe; fp16 GradScaler
-        # steps and the eager teacher fallback are not
+        # every loss (CE, device-side OHEM, BCE+Dice), the KD term and the fused fp16 GradScaler are
+        # capture-safe; the eager teacher fallback is not
         kd_ok = not config.kd_training or isinstance(self.teacher_model, FusedModel)
         return (self.fused and config.use_graph and kd_ok and not config.use_aux
-                and not self.scaler.is_enabled()
                 and (not config.DDP or config.gpu_num == 1 or config.graph_ddp))
 
     def _flush_logs(self, config, pbar=None):

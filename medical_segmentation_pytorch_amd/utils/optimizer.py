@@ -70,29 +70,38 @@ class FusedOptimizer(torch.optim.Optimizer):
             h[7] = self.grad_scale
         self.staged.push()
 
-    def launch(self):
-        """Device work of a step (capturable): all-reduce wait + one optimizer kernel."""
+    def launch(self, scaler=None):
+        """Device work of a step (capturable): all-reduce wait + one optimizer kernel.  ``scaler``: a
+        :class:`FusedGradScaler` -- finite check of the reduced gradients, then an update that unscales
+        or is skipped entirely on inf/NaN (one more launch, no host sync)."""
         from ..ops._ext import require
         C = require()
         if self.bucketer is not None:
             self.bucketer.finish()
         a = self.arena
+        amp = None
+        if scaler is not None and scaler.is_enabled():
+            C.amp_check(a.grad, scaler.state)
+            amp = scaler.state
+            self._amp = scaler.state
         if self.kind == 'sgd':
-            C.sgd_step(a.data, a.grad, self.buf, self.hyper)
+            C.sgd_step(a.data, a.grad, self.buf, self.hyper, amp)
         else:
-            C.adam_step(a.data, a.grad, self.m, self.v, self.hyper, self.kind == 'adamw')
+            C.adam_step(a.data, a.grad, self.m, self.v, self.hyper, self.kind == 'adamw', amp)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, scaler=None):
         loss = closure() if closure is not None else None
         self.prepare()
-        self.launch()
+        self.launch(scaler)
         return loss
 
     def state_dict(self):
         if self.kind != 'sgd':
+            amp = getattr(self, '_amp', None)   # fp16 loss scaling: skipped steps do not count
+            n = float(amp[3]) if amp is not None else float(self.step_count)
             for p in self.arena.params:
-                self.state[p]['step'] = torch.tensor(float(self.step_count))
+                self.state[p]['step'] = torch.tensor(n)
         return super().state_dict()
 
     def load_state_dict(self, state_dict):
@@ -111,6 +120,55 @@ class FusedOptimizer(torch.optim.Optimizer):
                         self.state[p]['step'] = torch.tensor(float(v))
                 elif k in self.state[p] and v is not None:
                     self.state[p][k].copy_(v)
+
+
+class FusedGradScaler:
+    """``torch.amp.GradScaler`` for the fused engine (reference ``core/base_trainer.py:30``,
+    ``core/seg_trainer.py:82-84``) with its state on the DEVICE -- ``[scale, growth_tracker, found_inf,
+    applied_steps]`` -- so a captured hipGraph step scales the loss, checks the reduced gradients,
+    unscales inside the optimizer kernel, skips the update on overflow and adjusts the scale
+    (``csrc/optim.hip`` amp_check / amp_update) without a host round-trip."""
+
+    def __init__(self, device, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 enabled=True):
+        self._enabled = enabled
+        self.growth_factor, self.backoff_factor, self.growth_interval = growth_factor, backoff_factor, growth_interval
+        self.state = torch.tensor([init_scale, 0.0, 0.0, 0.0], dtype=torch.float32, device=device)
+
+    def is_enabled(self):
+        return self._enabled
+
+    def scale(self, loss):
+        return loss * self.state[0] if self._enabled else loss
+
+    def step(self, optimizer):
+        if isinstance(optimizer, FusedOptimizer):
+            return optimizer.step(scaler=self if self._enabled else None)
+        raise TypeError('FusedGradScaler drives FusedOptimizer only')
+
+    def update(self):
+        if self._enabled:
+            from ..ops._ext import require
+            require().amp_update(self.state, self.growth_factor, self.backoff_factor, self.growth_interval)
+
+    def get_scale(self):
+        return float(self.state[0]) if self._enabled else 1.0
+
+    def state_dict(self):
+        if not self._enabled:
+            return {}
+        st = self.state.tolist()
+        return {'scale': st[0], 'growth_factor': self.growth_factor, 'backoff_factor': self.backoff_factor,
+                'growth_interval': self.growth_interval, '_growth_tracker': int(st[1])}
+
+    def load_state_dict(self, sd):
+        if not sd:
+            return
+        self.growth_factor = sd.get('growth_factor', self.growth_factor)
+        self.backoff_factor = sd.get('backoff_factor', self.backoff_factor)
+        self.growth_interval = sd.get('growth_interval', self.growth_interval)
+        self.state[0] = float(sd['scale'])
+        self.state[1] = float(sd.get('_growth_tracker', 0))
 
 
 def get_optimizer(config, model):

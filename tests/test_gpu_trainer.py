@@ -77,3 +77,50 @@ def test_trainer_graph_with_ohem_and_kd(gpu, tmp_path, mode):
     t.run(c)
     assert t.graph_step is not None and t.graph_step.graph is not None
     assert torch.isfinite(torch.tensor(t.last_loss))
+
+
+def test_fused_grad_scaler_matches_torch(gpu):
+    """FusedGradScaler + FusedOptimizer == torch GradScaler + Adam: same unscaled updates, the step is
+    skipped on an inf gradient (params, moments and Adam's step count untouched) and the scale backs
+    off / grows exactly as torch's ``_amp_update_scale_``."""
+    import torch.nn as nn
+    from medical_segmentation_pytorch_amd.utils.optimizer import FusedGradScaler, FusedOptimizer
+    torch.manual_seed(0)
+    m1 = nn.Sequential(nn.Linear(64, 32), nn.Linear(32, 8)).to(gpu)
+    m2 = nn.Sequential(nn.Linear(64, 32), nn.Linear(32, 8)).to(gpu)
+    m2.load_state_dict(m1.state_dict())
+    o1 = FusedOptimizer(m1, 'adam', lr=1e-2)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-2)
+    sc1 = FusedGradScaler(gpu, init_scale=1024.0, growth_interval=3)
+    sc2 = torch.amp.GradScaler('cuda', init_scale=1024.0, growth_interval=3)
+    for it in range(8):
+        x = torch.randn(4, 64, device=gpu)
+        for m, o, sc in ((m1, o1, sc1), (m2, o2, sc2)):
+            o.zero_grad()
+            loss = m(x).pow(2).mean()
+            sc.scale(loss).backward()
+            if it == 4:   # poison one gradient: this step must be skipped
+                next(m.parameters()).grad.view(-1)[3] = float('inf')
+            sc.step(o)
+            sc.update()
+        assert sc1.get_scale() == sc2.get_scale(), (it, sc1.get_scale(), sc2.get_scale())
+        for p, q in zip(m1.parameters(), m2.parameters()):
+            assert torch.allclose(p, q, atol=1e-5, rtol=1e-4), it
+    st = o1.state_dict()['state']
+    assert float(next(iter(st.values()))['step']) == 7.0   # 8 steps, one skipped
+    assert sc1.state_dict()['_growth_tracker'] == sc2.state_dict()['_growth_tracker']
+
+
+def test_trainer_fp16_amp_graph(gpu, tmp_path):
+    """amp_dtype='fp16' on the fused engine keeps the hipGraph (loss scaling on device state)."""
+    from medical_segmentation_pytorch_amd.core import SegTrainer
+    from medical_segmentation_pytorch_amd.utils.optimizer import FusedGradScaler
+    c = _cfg(tmp_path, engine='fused', amp_training=True, amp_dtype='fp16')
+    t = SegTrainer(c)
+    assert isinstance(t.scaler, FusedGradScaler) and t.scaler.is_enabled()
+    t.run(c)
+    assert t.graph_step is not None and t.graph_step.graph is not None
+    assert torch.isfinite(torch.tensor(t.last_loss))
+    assert t.scaler.get_scale() == 2.0 ** 16   # no overflow in a few bf16-computed steps
+    ck = torch.load(os.path.join(c.save_dir, 'last.pth'), weights_only=True)
+    assert ck['scaler']['scale'] == 2.0 ** 16
