@@ -1701,3 +1701,84 @@ void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cp
   hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid1d(total)), dim3(256), 0, s, src, dst, nrow, nch, T, Cpk, Ktot,
                      t_base, c_base, s_row, s_ch, accumulate ? 1 : 0, nrep, rep_stride);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Host-side launch-planner self-check (SURVEY §5 race detection / sanitizers): enumerates DUCKNet /
+// UNet / ResNet layer geometries and verifies the invariants every kernel launch relies on -- LDS
+// budgets, staging-register capacities, tile coverage, cursor-step decompositions, weight-row
+// padding and grid sizes.  Pure host code (no launch, no device): built with AddressSanitizer +
+// UBSan on the host side by tools/sanitize/run.sh and run on the CPU by tests/test_sanitize_cpu.py.
+int conv_plan_selfcheck(int verbose) {
+  int bad = 0;
+  auto fail = [&](const char* what, const ConvGeom& g) {
+    ++bad;
+    if (verbose)
+      fprintf(stderr, "plan check FAILED: %s (N=%d %dx%d Gi=%d Cgi=%d Go=%d Cgo=%d T=%d s=%d)\n", what, g.N, g.IH,
+              g.IW, g.Gi, g.Cgi, g.Go, g.Cgo, g.T, g.stride);
+  };
+  struct K { int kh, kw, dil; };
+  const K ks[] = {{3, 3, 1}, {3, 3, 2}, {3, 3, 3}, {1, 7, 1}, {7, 1, 1}, {1, 1, 1}, {2, 2, 1}, {7, 7, 1}};
+  const int sizes[] = {352, 176, 88, 44, 22, 11, 7, 64, 33};
+  const int chans[] = {8, 24, 40, 72, 136, 272, 544, 64, 128, 256, 512};
+  long checked = 0;
+  for (int hw : sizes)
+    for (int cin : chans)
+      for (int go : {1, 2, 8})
+        for (int cout : {24, 40, 72, 136, 64})
+          for (const K& k : ks)
+            for (int stride : {1, 2}) {
+              if (stride == 2 && k.dil != 1) continue;
+              ConvGeom g{};
+              g.N = 4; g.IH = hw; g.IW = hw; g.Gi = 1; g.Cgi = cin;
+              const int ph = (k.kh / 2) * k.dil, pw = (k.kw / 2) * k.dil;
+              g.OH = (hw + 2 * ph - k.dil * (k.kh - 1) - 1) / stride + 1;
+              g.OW = (hw + 2 * pw - k.dil * (k.kw - 1) - 1) / stride + 1;
+              if (g.OH < 1 || g.OW < 1) continue;
+              g.Go = go; g.Cgo = cout; g.Cgo_l = cout;
+              g.T = k.kh * k.kw;
+              if (g.T > kMaxTaps) continue;
+              for (int r = 0, t = 0; r < k.kh; ++r)
+                for (int c = 0; c < k.kw; ++c, ++t) { g.dy[t] = r * k.dil - ph; g.dx[t] = c * k.dil - pw; }
+              g.Kp = cdiv(g.T * cin, 32) * 32;
+              g.stride = stride;
+              ++checked;
+              const int rows = g.Go * g.Cgo;
+              HaloGeom hg{};
+              if (conv_halo_ok(g, false, hg)) {
+                const int C8 = cin / 8, d = hg.CC / 8;
+                if (hg.nch * hg.CC != cin) fail("halo chunks do not tile the input channels", g);
+                if ((long)hg.tiles_y * hg.TH < g.OH || (long)hg.tiles_x * hg.TW < g.OW) fail("halo tiles miss pixels", g);
+                if (halo_lds(hg, rows) > 64 * 1024) fail("halo tile LDS > 64 KB", g);
+                if (hg.KS > kHaloMaxKS || hg.KS * 4 < g.T * d) fail("halo k-steps", g);
+                if (((hg.pitch / 8) & 1) == 0) fail("halo pitch not an odd number of 16-B slots", g);
+                if (hg.TW != (1 << hg.tw_shift)) fail("halo tw_shift", g);
+                if (hg.st_q * d + hg.st_r != 64 * kHaloWaves || hg.st_a * hg.HWD + hg.st_b != hg.st_q)
+                  fail("halo staging cursor step", g);
+                const long total = (long)hg.HH * hg.HWD * d;
+                if (hg.nch > 1 && total > 64L * kHaloWaves * kHaloLd) fail("chunk exceeds staging registers", g);
+                if (hg.pipe) {
+                  if (total > 64L * kHaloWaves * kPipeLd) fail("PIPE tile exceeds prefetch registers", g);
+                  if (halo_lds(hg, rows) + 12 * (size_t)cin + pipe_a_bytes(rows, hg.mi, hg.KS) > (size_t)kPipeMaxLds)
+                    fail("PIPE LDS budget", g);
+                  if (hg.nch != 1 || C8 != d) fail("PIPE with channel chunks", g);
+                }
+                if (cdiv(rows, 16 * hg.mi) * 16 * hg.mi > conv_rows_alloc(rows)) fail("weight rows under-allocated", g);
+                const long blocks = halo_blocks(g, hg);
+                if (blocks < 1 || blocks > (1L << 31) - 1) fail("halo grid size", g);
+                if (blocks != conv_stat_blocks(g)) fail("stat partial rows != launch grid", g);
+              }
+              if (cdiv(rows, 16 * conv_pick_mi(rows)) * 16 * conv_pick_mi(rows) > conv_rows_alloc(rows))
+                fail("igemm weight rows under-allocated", g);
+              const WgradPlan W = wgrad_plan(g, false);
+              if (W.nsplit < 1) fail("wgrad split", g);
+              if (W.halo) {
+                if (W.nsplit > W.ntiles) fail("wgrad more splits than tiles", g);
+                if (wgrad_halo_lds(W.tl, W.ncb) > (size_t)kDwMaxLds) fail("wgrad LDS budget", g);
+                if ((long)W.tl.tiles_y * W.tl.TH < g.OH || (long)W.tl.tiles_x * W.tl.TW < g.OW) fail("wgrad tiles", g);
+                if (W.tl.HH * W.tl.HWv > kDwMaxHalo) fail("wgrad halo exceeds staging registers", g);
+              }
+            }
+  if (verbose) fprintf(stderr, "conv plan self-check: %ld geometries, %d violations\n", checked, bad);
+  return bad;
+}
+

@@ -54,6 +54,7 @@ bool conv_uses_halo(const ConvGeom& g, bool trans);
 long conv_stat_blocks(const ConvGeom& g);
 void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
+int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
 int conv_wgrad_replicas(const ConvGeom& g, bool trans);
 // xc / xrelu: the deferred-BN prologue of the x groups (see ConvArgs; xc may be nullptr)
 void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
