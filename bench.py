@@ -47,6 +47,8 @@ def parse_args(argv=None):
     p.add_argument('--graph-ddp', action='store_true', help='also capture the multi-GPU step in a hipGraph')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
+    p.add_argument('--ddp', action='store_true',
+                   help='run the distributed code path (process group, RCCL gradient buckets) even at WORLD_SIZE=1')
     p.add_argument('--data', choices=['augment', 'fixed'], default='augment',
                    help='augment (default): every step draws a fresh MyConfig-augmented batch from an HBM-resident '
                         'synthetic polyp split (GPU augmentation kernels, inside the timed loop); fixed: replay one '
@@ -116,6 +118,12 @@ def model_label(args):
     return name + (f' + KD teacher {args.teacher}' if args.teacher else '')
 
 
+# In-house reference speed: the reference's training step in eager PyTorch-ROCm on one
+# MI355X at its best measured config, DUCKNet-17 352x352 (profiles/eager_reference_speed.json; kept here
+# too because the profiles directory does not travel to the GPU boxes).
+EAGER_REFERENCE_IMG_S_PER_GPU = 120.27
+
+
 def main(argv=None):
     args = parse_args(argv)
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -129,7 +137,8 @@ def main(argv=None):
     # test hooks: BENCH_DIST_BACKEND=gloo + BENCH_SAME_DEVICE=1 rehearse the N-rank path on one GPU
     # (RCCL refuses two ranks per device); the driver's runs use RCCL, one rank per GPU
     dev_index = 0 if os.environ.get('BENCH_SAME_DEVICE') == '1' else local_rank
-    if world > 1:
+    ddp = world > 1 or args.ddp
+    if ddp:
         import torch.distributed as dist
         torch.cuda.set_device(dev_index)
         backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
@@ -138,12 +147,12 @@ def main(argv=None):
     device = torch.device('cuda', dev_index)
 
     impl = args.impl
-    use_graph = not args.no_graph and (world == 1 or args.graph_ddp)
+    use_graph = not args.no_graph and (not ddp or args.graph_ddp)
     feed = make_feed(args, device, seed=1000 + rank) if args.data == 'augment' else None
     step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
                             base_channel=args.base_channel, device=device,
                             channels_last=args.channels_last, use_graph=use_graph,
-                            distributed=world > 1, model_name=args.model, teacher_name=args.teacher,
+                            distributed=ddp, model_name=args.model, teacher_name=args.teacher,
                             feed=feed, total_steps=args.warmup + args.steps, lr=args.lr * world)
 
     t_w = time.perf_counter()
@@ -194,12 +203,17 @@ def main(argv=None):
     try:
         with open(os.path.join(here, 'BASELINE.json')) as f:
             baseline = (json.load(f).get('published') or {}).get('images_per_sec')
-        if baseline is None and args.model == 'ducknet' and args.base_channel == 17 and args.size == 352 \
-                and not args.teacher:
-            with open(os.path.join(here, 'profiles', 'eager_reference_speed.json')) as f:
-                baseline = json.load(f)['images_per_sec_per_gpu'] * world
     except Exception:
         pass
+    if baseline is None and args.model == 'ducknet' and args.base_channel == 17 and args.size == 352 \
+            and not args.teacher:
+        per_gpu = EAGER_REFERENCE_IMG_S_PER_GPU
+        try:   # a re-measured value, where the profiles directory is present
+            with open(os.path.join(here, 'profiles', 'eager_reference_speed.json')) as f:
+                per_gpu = json.load(f)['images_per_sec_per_gpu']
+        except Exception:
+            pass
+        baseline = per_gpu * world
     if rank == 0:
         print(json.dumps({
             'metric': ('images/sec (whole node) + val Dice, DUCKNet-17 352x352 at 1/2/4/8 MI355X'

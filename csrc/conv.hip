@@ -684,18 +684,41 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, uint16_t* __re
   }
 }
 
-__global__ void unpack_wgrad_kernel(const float* __restrict__ src, float* __restrict__ dst, int nrow, int nch, int T,
-                                    int Cpk, int Ktot, int t_base, int c_base, long s_row, long s_ch, int accumulate,
-                                    int nrep, long rep_stride) {
+// dst[row][c][t] (+)= sum over the nrep split-K slabs of src[r][row][(t_base+t)*Cpk + c_base + c].
+// 64 elements x 8 slab groups per 512-thread block: group g sums slabs g, g+8, ... in order and the
+// 8 group sums are added in group order -- a fixed summation order, so bitwise deterministic, with 8x
+// the loads in flight of a one-thread-per-element loop (the slabs are read straight from L2/HBM).
+// Element order (row, t, c) keeps a wave's slab reads contiguous in c.
+constexpr int kUnpackGroups = 8;
+__global__ __launch_bounds__(64 * kUnpackGroups) void unpack_wgrad_kernel(
+    const float* __restrict__ src, float* __restrict__ dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base,
+    int c_base, long s_row, long s_ch, int accumulate, int nrep, long rep_stride) {
+  __shared__ float part[kUnpackGroups][64];
   const long total = (long)nrow * nch * T;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int t = (int)(i % T);
-    const long rc = i / T;
-    const int c = (int)(rc % nch);
-    const int row = (int)(rc / nch);
-    const long si = (long)row * Ktot + (t_base + t) * Cpk + c_base + c;
-    float v = 0.f;
-    for (int r = 0; r < nrep; ++r) v += src[r * rep_stride + si];   // split-K slabs, fixed order
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + lane;
+  long si = 0;
+  if (i < total) {
+    const int c = (int)(i % nch);
+    const long rt = i / nch;
+    const int t = (int)(rt % T);
+    const int row = (int)(rt / T);
+    si = (long)row * Ktot + (t_base + t) * Cpk + c_base + c;
+  }
+  float v = 0.f;
+  if (i < total) {
+#pragma unroll 4
+    for (int r = grp; r < nrep; r += kUnpackGroups) v += src[r * rep_stride + si];
+  }
+  part[grp][lane] = v;
+  __syncthreads();
+  if (grp == 0 && i < total) {
+#pragma unroll
+    for (int g2 = 1; g2 < kUnpackGroups; ++g2) v += part[g2][lane];
+    const int c = (int)(i % nch);
+    const long rt = i / nch;
+    const int t = (int)(rt % T);
+    const int row = (int)(rt / T);
     float* d = dst + row * s_row + c * s_ch + t;
     *d = accumulate ? *d + v : v;
   }
@@ -1698,8 +1721,8 @@ int pack_per_block() { return kPackPerBlock; }
 void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cpk, int Ktot, int t_base, int c_base,
                   long s_row, long s_ch, bool accumulate, int nrep, long rep_stride, hipStream_t s) {
   const long total = (long)nrow * nch * T;
-  hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid1d(total)), dim3(256), 0, s, src, dst, nrow, nch, T, Cpk, Ktot,
-                     t_base, c_base, s_row, s_ch, accumulate ? 1 : 0, nrep, rep_stride);
+  hipLaunchKernelGGL(unpack_wgrad_kernel, dim3((unsigned)((total + 63) / 64)), dim3(64 * kUnpackGroups), 0, s, src,
+                     dst, nrow, nch, T, Cpk, Ktot, t_base, c_base, s_row, s_ch, accumulate ? 1 : 0, nrep, rep_stride);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -231,6 +231,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, mode, pro, gamma, beta, *xs):
         C = require()
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the non-differentiable stats output
         deferred, defer_bwd = mode
         xs = [x.contiguous() for x in xs]
         coefs, rmask = pro
@@ -295,7 +296,7 @@ class _BNAct(torch.autograd.Function):
         need_grads([dz])
         y, stats = ctx.saved_tensors
         st: BNState = ctx.st
-        dz = dz.contiguous()
+        dz = torch.zeros_like(y) if dz is None else dz.contiguous()
         Cp = y.shape[-1]
         P = y.numel() // Cp
         dev = y.device

@@ -209,6 +209,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, plan: ConvPlan, want_stats: bool, nx: int, bn_handle, pro, *args):
         C = require()
+        ctx.set_materialize_grads(False)   # the stats output never gets a zero-filled gradient
         xs = [a.contiguous() for a in args[:nx]]
         coefs, rmask = pro
         n, ih, iw, _ = xs[0].shape

@@ -129,3 +129,23 @@ def test_bench_ddp_path_two_ranks(gpu, tmp_path):
     d = json.loads(line[0])
     assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'dp2' and d['config']['global_batch'] == 4
     assert d['value'] > 0 and d['steps'] == 3 and d['warmup'] == 2 and d['config']['syncbn']
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_bench_rccl_path_world1(gpu, tmp_path, graph):
+    """The RCCL code path on the real backend: one rank over `nccl` (RCCL) with --ddp, so the process
+    group, the bucketed gradient all-reduce of the arena and the step's RCCL calls all run on the GPU
+    (one device -> world size 1; more ranks are the driver's 8-GPU runs).  graph=True also captures
+    the RCCL all-reduces inside the hipGraph (the opt-in --graph-ddp mode)."""
+    import json
+    s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '1', '--ddp',
+           '--steps', '3', '--warmup', '2', '--batch', '4', '--size', '64', '--train-images', '8',
+           '--val-images', '4'] + (['--graph-ddp'] if graph else [])
+    r = subprocess.run(cmd, env=dict(os.environ), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d['n_gpus'] == 1 and d['value'] > 0 and d['config']['hipgraph'] == graph
