@@ -114,7 +114,8 @@ def model_label(args):
     elif args.model == 'unet':
         name = f'UNet-{args.base_channel}'
     else:
-        name = f'smp-Unet({args.model[4:]})'
+        parts = args.model.split('-')   # smp-<encoder> | smp-<decoder>-<encoder>
+        name = f'smp-{parts[1]}({parts[2]})' if len(parts) == 3 else f'smp-Unet({args.model[4:]})'
     return name + (f' + KD teacher {args.teacher}' if args.teacher else '')
 
 
