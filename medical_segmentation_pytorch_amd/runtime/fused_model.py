@@ -404,7 +404,10 @@ class FusedExecutor:
         enc = model.encoder
         feats = self.resnet_encoder(enc, images, training)
         chans = list(enc.out_channels[1:])
-        nchw = [images] + [from_fm(f, c) for f, c in zip(feats, chans)]
+        # ResNet feature widths are multiples of 8 (no channel padding): the NHWC bf16 map IS a
+        # channels-last NCHW tensor -- a zero-copy view, and MIOpen's NHWC kernels for the decoder
+        nchw = [images] + [f.permute(0, 3, 1, 2) if f.shape[-1] == c else from_fm(f, c)
+                           for f, c in zip(feats, chans)]
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=images.is_cuda):
             out = model.segmentation_head(model.decoder(*nchw))
         return out.float()
