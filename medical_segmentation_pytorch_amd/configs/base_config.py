@@ -119,6 +119,8 @@ class BaseConfig:
         self.engine = 'auto'           # 'auto' | 'fused' (HIP kernels) | 'eager' (stock torch ops)
         self.amp_dtype = 'bf16'        # CDNA4 autocast dtype when amp_training: 'bf16' | 'fp16'
         self.use_graph = True          # capture the static-shape train step in a hipGraph
+        self.eager_channels_last = True   # eager engine on a GPU: channels-last activations (MIOpen NHWC
+                                          # kernels; 1.8x the NCHW step on MI355X, profiles/r02/eager_sweep)
         self.bucket_cap_mb = 64        # gradient bucket size for the RCCL all-reduce
         self.grad_compress = None      # None | 'bf16' all-reduce compression
         self.gpu_augment = True        # run augmentation on the GPU over an HBM-resident dataset

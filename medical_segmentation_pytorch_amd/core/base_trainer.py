@@ -52,6 +52,11 @@ class BaseTrainer:
         self.model = get_model(config).to(self.device)
         config._fused = use_fused(config, self.model, self.device)
         self.fused = config._fused
+        # eager engine on a GPU: channels-last parameters/activations (before the optimizer holds them)
+        self.channels_last = (not self.fused and self.device.type == 'cuda'
+                              and getattr(config, 'eager_channels_last', False))
+        if self.channels_last:
+            self.model = self.model.to(memory_format=torch.channels_last)
         # fp16 loss scaling: torch GradScaler on the eager engine; on the fused engine the same semantics
         # with device-side state inside the captured step (the fused kernels compute in bf16, so overflow
         # skips are rare, but the reference's fp16 protocol -- scaled loss, skipped steps -- is kept)

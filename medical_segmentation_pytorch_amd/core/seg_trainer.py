@@ -119,6 +119,8 @@ class SegTrainer(BaseTrainer):
     # ------------------------------------------------------------------------------------------------
     def eager_step(self, images, masks):
         config = self.config_ref
+        if getattr(self, 'channels_last', False) and images.dim() == 4:
+            images = images.contiguous(memory_format=torch.channels_last)
         self.optimizer.zero_grad()
         ex = getattr(self.model, 'executor', None)
         if ex is not None:   # prepacked conv weights must follow the last optimizer step
