@@ -115,10 +115,18 @@ class FusedStep:
         if self.graph is None:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
                 self.loss = self._body()
         self.graph.replay()
         return self.loss
+
+
+def capture_mode():
+    """hipGraph capture error mode: 'thread_local' under torch.distributed -- the process group's
+    watchdog thread polls its work events while the step is being captured, which the default
+    'global' mode turns into a capture error and a SIGABRT (seen intermittently with --graph-ddp)."""
+    import torch.distributed as dist
+    return 'thread_local' if dist.is_available() and dist.is_initialized() else 'global'
 
 
 def make_model(model_name, base_channel=17, num_class=2):

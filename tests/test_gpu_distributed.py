@@ -144,7 +144,8 @@ def test_bench_rccl_path_world1(gpu, tmp_path, graph):
            '--steps', '3', '--warmup', '2', '--batch', '4', '--size', '64', '--train-images', '8',
            '--val-images', '4'] + (['--graph-ddp'] if graph else [])
     r = subprocess.run(cmd, env=dict(os.environ), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
-    assert r.returncode == 0, r.stderr[-3000:]
+    errs = [ln for ln in r.stderr.splitlines() if 'rror' in ln or 'what()' in ln or 'Exception' in ln][:20]
+    assert r.returncode == 0, '\n'.join(errs) + '\n...\n' + r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert len(line) == 1, r.stdout
     d = json.loads(line[0])

@@ -483,6 +483,68 @@ def test_bn_partials_from_dgrad_epilogue(gpu, relu, halo):
         assert _rel(b, a) < 1e-3, _rel(b, a)
 
 
+BNE_CASES = [
+    # c, co, (kh, kw), dilation, n_3x3 groups, n_1x1 groups, (n, h, w), halo
+    (64, 64, (3, 3), 1, 1, 0, (2, 20, 24), True),       # multi-row-group halo (MI >= 2 row tiles)
+    (160, 96, (3, 3), 1, 1, 0, (2, 12, 16), True),      # wide input, several row groups
+    (17, 17, (3, 3), 2, 1, 0, (2, 20, 24), True),       # dilated DUCK branches
+    (17, 17, (3, 3), 3, 1, 0, (2, 20, 24), True),
+    (17, 17, (1, 7), 1, 1, 0, (2, 20, 24), True),       # separated 1x7 / 7x1
+    (17, 17, (7, 1), 1, 1, 0, (2, 20, 24), True),
+    (17, 17, (3, 3), 1, 1, 1, (2, 20, 24), True),       # residual chain: fused 3x3 + 1x1 (Go = 2)
+    (64, 64, (3, 3), 1, 5, 3, (2, 24, 32), True),       # DUCK-style Go = 8: chunked halo data-gradient
+    (64, 64, (3, 3), 1, 1, 1, (2, 20, 24), False),      # implicit-GEMM data-gradient, Go = 2
+]
+
+
+@pytest.mark.parametrize('case', BNE_CASES)
+def test_bn_partials_from_dgrad_epilogue_geometries(gpu, case):
+    """The BN-epilogue data-gradient (conv_fwd_bn) over the geometries the executor marks single-consumer:
+    several row groups, dilation 2/3, 1x7/7x1, Go = 2 residual-chain and Go = 8 (chunked halo) fused
+    plans, and the implicit-GEMM path -- dx, dgamma, dbeta and dW must equal the separate-pass ones."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    from medical_segmentation_pytorch_amd.ops.bn import BwdStatsHandle
+    C = _ext.require()
+    c, co, (kh, kw), dil, n3, n1, (n, h, w), halo = case
+    torch.manual_seed(21)
+    bnm = nn.BatchNorm2d(c).to(gpu)
+    with torch.no_grad():
+        bnm.weight.uniform_(0.5, 1.5)
+        bnm.bias.uniform_(-0.5, 0.5)
+    convs = [nn.Conv2d(c, co, (kh, kw), 1, (dil * (kh // 2), dil * (kw // 2)), (dil, dil), bias=False).to(gpu)
+             for _ in range(n3)]
+    convs += [nn.Conv2d(c, co, 1, bias=False).to(gpu) for _ in range(n1)]
+    T = kh * kw
+    branches = [Branch(m.weight, g, 0, T) for g, m in enumerate(convs[:n3])]
+    branches += [Branch(m.weight, n3 + g, T // 2, 1) for g, m in enumerate(convs[n3:])]
+    y0 = to_fm_reference(_bf(torch.randn(n, c, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(3))))
+    gs = [to_fm_reference(_bf(torch.randn(n, co, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(4 + g))))
+          for g in range(n3 + n1)]
+    res = []
+    C.conv_set_halo(halo)
+    try:
+        for use in (False, True):
+            for m in [bnm] + convs:
+                for p in m.parameters():
+                    p.grad = None
+            st = BNState.from_module(bnm)
+            plan = ConvPlan(kh, kw, c, co, branches, padding=(dil * (kh // 2), dil * (kw // 2)), dilation=(dil, dil),
+                            Go=n3 + n1)
+            y = y0.clone().requires_grad_(True)
+            hdl = BwdStatsHandle() if use else None
+            z = bn_act([y], st, True, True, None, handle=hdl)
+            outs, _ = conv(plan, [z], want_stats=False, bn_handle=hdl)
+            torch.autograd.backward(outs, gs)
+            if use:
+                assert hdl.part is None, 'BN backward must have consumed the epilogue partials'
+            res.append([y.grad.float().clone(), bnm.weight.grad.clone(), bnm.bias.grad.clone()] +
+                       [m.weight.grad.clone() for m in convs])
+    finally:
+        C.conv_set_halo(True)
+    for a, b in zip(res[0], res[1]):
+        assert _rel(b, a) < 1e-3, _rel(b, a)
+
+
 def _ohem_ref(logits, tgt, thresh, ignore=255):
     px = F.cross_entropy(logits, tgt, ignore_index=ignore, reduction='none').view(-1)
     hard = px[px > -math.log(thresh)]

@@ -126,3 +126,24 @@ def test_block_cba(gpu):
     _block_check(gpu, ConvBNAct(17, 34, 3, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
     _block_check(gpu, ConvBNAct(17, 34, 2, 2), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
     _block_check(gpu, ConvBNAct(17, 17, (1, 7)), lambda ex, m, x: ex.cba(m, x, True), (4, 17, 32, 32))
+
+
+def test_bn_epilogue_on_off_full_model(gpu, monkeypatch):
+    """A whole DuckNet fused step with the dgrad-epilogue BN partials (MSP_BN_EPILOGUE=1) vs the separate
+    partial-sum pass (=0): same logits, same parameter gradients up to summation order."""
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    torch.manual_seed(0)
+    base = DuckNet(2, 3, 17).to(gpu).train()
+    x = torch.randn(2, 3, 96, 96, device=gpu)
+    tgt = torch.randint(0, 2, (2, 96, 96), device=gpu)
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(fused_model, '_BN_EPILOGUE', on)
+        model = copy.deepcopy(base)
+        out = FusedExecutor(model)(x, training=True)
+        F.cross_entropy(out, tgt).backward()
+        torch.cuda.synchronize()
+        res.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()]))
+    assert _cos(res[0][0], res[1][0]) > 0.9999
+    cs = [_cos(a, b) for a, b in zip(res[0][1], res[1][1]) if b.abs().sum() > 0]
+    assert min(cs) > 0.99 and sum(cs) / len(cs) > 0.999, (min(cs), sum(cs) / len(cs))
