@@ -482,6 +482,7 @@ constexpr int kDwMaxHalo = 640;  // halo pixels the staging registers cover (eve
 constexpr long kDwSplitTarget = 256;
 constexpr int kDwMaxNcb = 3;     // 32-row dY sub-tiles per block, all sharing ONE staged input halo
 constexpr int kDwMaxLds = 120 * 1024;
+constexpr double kDwHaloCost = 0.5;   // input-halo staging per tile, in units of one co sub-tile's work
 // staging elements per thread: NCB dY sub-tiles (2 slots of 128 pixels each) + the halo
 constexpr int dw_stage(int ncb) { return 2 * ncb + kDwMaxHalo / (16 * kDwWaves); }
 
@@ -1633,8 +1634,19 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
       const char* e = getenv("MSP_DW_NCB");
       max_ncb = (e != nullptr && atoi(e) > 0) ? std::min(atoi(e), kDwMaxNcb) : kDwMaxNcb;
     }
-    int ncb = std::min(max_ncb, cdiv(rows, DW_CH));
-    while (ncb > 1 && wgrad_halo_lds(P.tl, ncb) > (size_t)kDwMaxLds) --ncb;
+    // The kernel's time ~ (tiles per block) x (co sub-tiles per block) + the per-tile input-halo
+    // staging that NCB sub-tiles share: with the grid fixed at ~split_target blocks, cost ~ gy * ncb +
+    // kDwHaloCost * gy.  Balancing matters: 4 sub-tiles (a 5-group fused conv at 24 ch) run as 2 + 2,
+    // not 3 + 1 (the 3-sub-tile blocks would set the kernel time).
+    const int nst = cdiv(rows, DW_CH);
+    int ncb = 1;
+    double best = 1e30;
+    for (int c = 1; c <= std::min(max_ncb, nst); ++c) {
+      if (c > 1 && wgrad_halo_lds(P.tl, c) > (size_t)kDwMaxLds) break;
+      const int gy = cdiv(nst, c);
+      const double cost = (double)gy * c + kDwHaloCost * gy;
+      if (cost <= best) { best = cost; ncb = c; }   // ties -> the larger NCB (fewer input passes)
+    }
     P.ncb = ncb;
     P.gy = cdiv(rows, DW_CH * ncb);
     P.gz = cdiv(g.Gi * g.Cgi, DW_CH);

@@ -23,6 +23,7 @@ import os
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ..ops.bn import BNState, BwdStatsHandle, Deferred, bn_act, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
@@ -36,6 +37,30 @@ _BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
 _DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
+
+
+# How the DUCK block's 8 first convs (0-4: the 3x3 first convs of wide/mid/res1/res2/res3, 5-7: the
+# three 1x1 residual shortcuts, reference ducknet.py:144-149) split into launches, per block width.
+# One 8-group launch reads xb once and sums the 8 data-gradients in one kernel, but it carries the
+# 1x1 convs at the centre tap of a 3x3 GEMM (8/9 of their MFMA work is on zero weights) and, from
+# 576 output rows up, loses the halo kernel.  env MSP_DUCK_SPLIT ("8", "5+3", "3+2+3", ...) forces
+# one split for every width (A/B measurements).  Measured per level at bs128, fwd+dgrad+wgrad ms
+# (tools/conv_bench.py, profiles/r02/conv_bench_duck_splits_bs128.log): 17 ch @352: 8 = 10.1 vs 5+3 =
+# 10.6 (the input is the largest tensor: reading it once wins); 34 @176: 8.4 vs 7.0; 68 @88: 8.4 vs 5.5;
+# 136 @44: 7.0 vs 5.1 vs 3+2+3 = 4.9; 272 @22: 7.1 vs 5.8 vs 4.9.
+def _default_split(cout):
+    c = (cout + 7) // 8 * 8
+    return '8' if c <= 24 else ('5+3' if c <= 72 else '3+2+3')
+
+
+def duck_split(cout):
+    """Launches of a DUCK block's first convs (``cout`` output channels each): consecutive runs of the
+    order 0..7."""
+    spec = os.environ.get('MSP_DUCK_SPLIT') or _default_split(cout)
+    sizes = [int(n) for n in spec.split('+')]
+    assert sum(sizes) == 8 and min(sizes) > 0, f'bad DUCK split {spec}'
+    starts = [sum(sizes[:i]) for i in range(len(sizes))]
+    return [list(range(a, a + n)) for a, n in zip(starts, sizes)]
 
 
 def _is_relu(act_mod):
@@ -104,7 +129,7 @@ class FusedExecutor:
         p = self._cached(self._plans, key, c)
         if p is None:
             kh, kw = _pair(c.kernel_size)
-            assert c.groups == 1, 'grouped/depthwise conv not in the fused engine yet'
+            assert c.groups == 1, 'grouped convs take grouped_conv_bn'
             p = ConvPlan(kh, kw, c.in_channels // gi, c.out_channels, [self._branch(c)], stride=_pair(c.stride)[0],
                          padding=_pair(c.padding), dilation=_pair(c.dilation), Gi=gi, bias=c.bias,
                          bias_sink=self.sinks.get(id(c.bias)) if c.bias is not None else None,
@@ -141,6 +166,18 @@ class FusedExecutor:
             p = ConvPlan(3, 3, c0.in_channels, c0.out_channels, branches, stride=1, padding=(1, 1),
                          dilation=(1, 1), Go=len(branches), ready_hook=self.ready_hook)
             self._plans[key] = (convs3[0], p)
+        return p
+
+    def plan_fused1x1(self, key, convs1):
+        """One 1x1 GEMM over sibling 1x1 convs reading the same input (output group order = convs1)."""
+        p = self._cached(self._plans, key, convs1[0])
+        if p is None:
+            c0 = convs1[0]
+            for c in convs1:
+                assert _pair(c.kernel_size) == (1, 1) and _pair(c.stride) == (1, 1) and c.bias is None
+            p = ConvPlan(1, 1, c0.in_channels, c0.out_channels, [self._branch(c, g, 0) for g, c in enumerate(convs1)],
+                         stride=1, padding=(0, 0), dilation=(1, 1), Go=len(convs1), ready_hook=self.ready_hook)
+            self._plans[key] = (convs1[0], p)
         return p
 
     # -- single-consumer BN outputs ------------------------------------------------------------------
@@ -272,11 +309,23 @@ class FusedExecutor:
         r4, r5 = b4[0], b5[0]
         convs3 = [b1[0][0], b2[0][0], b3.lower_branch[0][0], r4.lower_branch[0][0], r5.lower_branch[0][0]]
         convs1 = [b3.upper_branch, r4.upper_branch, r5.upper_branch]
-        plan = self.plan_fused3x3(('duck', id(m)), convs3, convs1)
-        ys, part = conv(plan, [xb], want_stats=training)
+        allc = convs3 + convs1
+        # the 8 convs reading xb as one or more multi-output launches (duck_split); src[g] = (outputs,
+        # partials, plan, index) of conv g
+        src = [None] * 8
+        for li, idx in enumerate(duck_split(allc[0].out_channels)):
+            i3, i1 = [i for i in idx if i < 5], [i for i in idx if i >= 5]
+            plan = (self.plan_fused3x3(('duck', id(m), li), [allc[i] for i in i3], [allc[i] for i in i1]) if i3
+                    else self.plan_fused1x1(('duck', id(m), li), [allc[i] for i in i1]))
+            ys_l, part_l = conv(plan, [xb], want_stats=training)
+            for j, i in enumerate(i3 + i1):   # plan output groups: 3x3 convs first, then the 1x1s
+                src[i] = (ys_l, part_l, plan, j)
+        ys = [src[i][0][src[i][3]] for i in range(8)]
+
         # every first-conv BN output feeds one conv only (single=True); branch outputs feed the 6-way sum
         def bnz(seq, g):
-            return lambda: self.bn_from_group(seq[1], seq[2], ys, part, plan, g, training, single=True)
+            ys_l, part_l, plan_l, j = src[g]
+            return lambda: self.bn_from_group(seq[1], seq[2], ys_l, part_l, plan_l, j, training, single=True)
 
         def wide():      # d1 -> d2 -> d3
             o = yield from self._g_bn(bnz(b1[0], 0))
@@ -363,10 +412,26 @@ class FusedExecutor:
 
     # -- smp Unet with a ResNet encoder (reference models/__init__.py:23-25; KD teacher :42-62) ---------
     def conv_bn(self, conv_mod, bn_mod, x, training, relu, single=False):
+        if conv_mod.groups != 1:
+            return self.grouped_conv_bn(conv_mod, bn_mod, x, training, relu)
         plan = self.plan_conv(conv_mod)
         (y,), part = self._conv(plan, [x], training)
         return self._bn_out([y], self.bn(bn_mod), relu, training, (part, plan.rows, 0) if training else None,
                             single)
+
+    def grouped_conv_bn(self, conv_mod, bn_mod, x, training, relu):
+        """Grouped 3x3 conv (ResNeXt ``conv2``, ``groups=32``) inside the fused graph: the NHWC bf16
+        feature map IS a channels-last NCHW tensor (widths are multiples of 8), so the conv runs on
+        MIOpen's channels-last grouped kernels with no layout copy, between fused ops on both sides
+        (the 1x1 convs around it -- most of a ResNeXt block's FLOPs -- stay on the HIP kernels).  Its BN
+        takes the statistics pass (no conv epilogue) and never parks its backward exchange: the
+        data-gradient goes to an autograd op, not to one of ours."""
+        z = materialize(x)
+        assert z.shape[-1] == conv_mod.in_channels, 'grouped conv input must be unpadded (C % 8 == 0)'
+        y = F.conv2d(z.permute(0, 3, 1, 2), conv_mod.weight.to(torch.bfloat16), None, conv_mod.stride,
+                     conv_mod.padding, conv_mod.dilation, conv_mod.groups)
+        y = y.permute(0, 2, 3, 1).contiguous()   # a view when MIOpen returns channels-last
+        return bn_act([y], self.bn(bn_mod), relu, training, deferred=_DEFER_BN)
 
     def resnet_block(self, blk, x, training):
         """torchvision BasicBlock / Bottleneck: ``relu(bn_last(conv_last(...)) + identity)``."""
@@ -463,7 +528,9 @@ def _is_resnet_smp(model) -> bool:
     enc = getattr(model, 'encoder', None)
     if not isinstance(enc, ResNetEncoder) or enc._depth < 1:
         return False
-    return not any(isinstance(m, nn.Conv2d) and m.groups != 1 for m in enc.modules())
+    # grouped convs (ResNeXt) run on MIOpen inside the fused graph: channel widths must be unpadded
+    return all(m.in_channels % 8 == 0 and m.out_channels % 8 == 0
+               for m in enc.modules() if isinstance(m, nn.Conv2d) and m.groups != 1)
 
 
 def _is_resnet_unet(model) -> bool:

@@ -26,6 +26,10 @@ def layers(b=17):
         L.append((f'L{lvl + 1} 3x3d3 {c}->{c}', lvl, c, c, (3, 3), 1, (3, 3), (3, 3), 1))
         L.append((f'L{lvl + 1} 1x7 {c}->{c}', lvl, c, c, (1, 7), 1, (0, 3), (1, 1), 1))
         L.append((f'L{lvl + 1} fused8 {c}->8x{c}', lvl, c, c, (3, 3), 1, (1, 1), (1, 1), 8))
+        # DUCK first-conv decompositions: the 5 3x3 convs (in 1, 2 or 3 launches) + the 3 1x1 shortcuts
+        for gsz in (5, 3, 2):
+            L.append((f'L{lvl + 1} fused{gsz} {c}->{gsz}x{c}', lvl, c, c, (3, 3), 1, (1, 1), (1, 1), gsz))
+        L.append((f'L{lvl + 1} fused3-1x1 {c}->3x{c}', lvl, c, c, (1, 1), 1, (0, 0), (1, 1), 3))
         L.append((f'L{lvl + 1} 3x3s2 {c}->{2 * c}', lvl, c, 2 * c, (3, 3), 2, (1, 1), (1, 1), 1))
     L.append(('L6 3x3 544->544', 5, 32 * b, 32 * b, (3, 3), 1, (1, 1), (1, 1), 1))
     L.append(('L6 fused2 544->2x544', 5, 32 * b, 32 * b, (3, 3), 1, (1, 1), (1, 1), 2))
