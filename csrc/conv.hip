@@ -778,7 +778,8 @@ constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel
 constexpr int kHaloWaves = 4;
 constexpr int kHaloMaxRows = 512;
 constexpr int kHaloLd = 8;       // 16-B loads in flight per thread while staging
-constexpr int kHaloMaxLds = 96 * 1024;   // tile (<= 64 KB by geometry) + stats + prologue table
+constexpr int kHaloMaxLds = 96 * 1024;   // tile (<= halo_tile_cap() by geometry) + stats + prologue table
+constexpr int kHaloTileKB = 76;          // tile + stats + prologue table cap: 2 blocks/CU with the static tables
 constexpr int kPipeLd = 8;               // PIPE: 16-B vectors per thread prefetched for the next tile
 constexpr int kPipeGrid = 256 * 2;       // PIPE: persistent grid, 2 blocks on each of the 256 CUs
 constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table + weights, 2 blocks/CU
@@ -1382,6 +1383,29 @@ static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
   return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
 }
 
+// LDS cap of a halo tile + its stats rows + the prologue table.  Two blocks per CU hold up to ~76 KB of
+// dynamic LDS each (160 KB per CU minus the static tap tables); 64 KB measured 0.6 % slower per step
+// (L3 3x3 d3 leaves the gather kernel: fwd 0.49 -> 0.28 ms).  env MSP_HALO_TILE_KB overrides (A/B).
+static size_t halo_tile_cap() {
+  static long kb = -1;
+  if (kb < 0) {
+    const char* e = getenv("MSP_HALO_TILE_KB");
+    kb = (e != nullptr && atol(e) >= 16 && atol(e) <= 78) ? atol(e) : kHaloTileKB;
+  }
+  return (size_t)kb * 1024;
+}
+
+// Fallback row-group size of the halo kernel.  conv_pick_mi's MI <= 2 comes with the 512-pixel (NJ = 8)
+// tile; when that tile (+ halo) does not fit the LDS cap the 256-pixel MI 3/4 tile often does, instead of
+// falling back to the gather kernel (L3 5x3x3 + 3x1x1 DUCK split, 216 rows x 72 ch: 1.46 -> 0.57 ms fwd).
+// env MSP_HALO_MI_RULE=0 disables the fallback (A/B).
+static int halo_fallback_mi(int rows) {
+  static int rule = -1;
+  if (rule < 0) { const char* e = getenv("MSP_HALO_MI_RULE"); rule = (e != nullptr && e[0] == '0') ? 0 : 1; }
+  if (!rule || conv_pick_mi(rows) > 2) return 0;
+  return cdiv(rows, 48) * 48 <= cdiv(rows, 64) * 64 ? 3 : 4;
+}
+
 static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   if (trans || g.stride != 1 || g.OH != g.IH || g.OW != g.IW) return false;
   const int rows = g.Go * g.Cgo;
@@ -1397,10 +1421,12 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   // try 0: PIPE (whole input, halo tile within the prefetch registers); try 1: the standard kernels
   // PIPE pays where its 256-pixel tile is also the standard kernel's (MI 3) and the 3x3 halo is thin;
   // measured slower for the MI<=2 layers (which lose their 512-pixel tile) and the 1x7 / dilated halos
+  // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi)
   const bool pipe_ok = pipe_enabled() && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
-  for (int attempt = pipe_ok ? 0 : 1; attempt < 2; ++attempt) {
+  for (int attempt = pipe_ok ? 0 : 1; attempt < 3; ++attempt) {
   const bool pipe = attempt == 0;
-  const int mi = pipe ? pipe_pick_mi(rows) : conv_pick_mi(rows);
+  if (attempt == 2 && halo_fallback_mi(rows) == 0) break;
+  const int mi = pipe ? pipe_pick_mi(rows) : (attempt == 1 ? conv_pick_mi(rows) : halo_fallback_mi(rows));
   const int n_rg = cdiv(rows, 16 * mi);
   const int tp = kHaloWaves * halo_nj(mi, pipe) * 16;
   for (int pass = 0; pass < (pipe ? 1 : 2); ++pass) {          // pass 0: whole input; pass 1: channel chunks
@@ -1417,7 +1443,8 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
       for (int tw = 16; tw <= 64; tw *= 2) {
         const int th = tp / tw;
         const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
-        if (halo_lds_bytes(HH, HWD, pitch, rows) > 64 * 1024) continue;
+        // (+ the prologue table a deferred-BN input adds: two blocks per CU must still fit)
+        if (halo_lds_bytes(HH, HWD, pitch, rows) + 12 * (size_t)Cip > halo_tile_cap()) continue;
         if (pass == 1 && HH * HWD * d > 64 * kHaloWaves * kHaloLd) continue;
         if (pipe && HH * HWD * d > 64 * kHaloWaves * kPipeLd) continue;
         if (pipe && halo_lds_bytes(HH, HWD, pitch, rows) + 12 * (size_t)Cip + pipe_a_bytes(rows, mi, ks) >
@@ -1783,7 +1810,8 @@ int conv_plan_selfcheck(int verbose) {
                 const int C8 = cin / 8, d = hg.CC / 8;
                 if (hg.nch * hg.CC != cin) fail("halo chunks do not tile the input channels", g);
                 if ((long)hg.tiles_y * hg.TH < g.OH || (long)hg.tiles_x * hg.TW < g.OW) fail("halo tiles miss pixels", g);
-                if (halo_lds(hg, rows) > 64 * 1024) fail("halo tile LDS > 64 KB", g);
+                if (halo_lds(hg, rows) + 12 * (size_t)cin > halo_tile_cap()) fail("halo tile LDS over the cap", g);
+                if (halo_lds(hg, rows) + 12 * (size_t)cin > (size_t)kHaloMaxLds) fail("halo LDS > opted-in maximum", g);
                 if (hg.KS > kHaloMaxKS || hg.KS * 4 < g.T * d) fail("halo k-steps", g);
                 if (((hg.pitch / 8) & 1) == 0) fail("halo pitch not an odd number of 16-B slots", g);
                 if (hg.TW != (1 << hg.tw_shift)) fail("halo tw_shift", g);
