@@ -8,10 +8,12 @@ bucketed all-reduce + SyncBN), optimizer step (Adam, MyConfig default), OneCycle
 EMA update.  W untimed warmup steps, then K steps bracketed by barrier + synchronize; the MAX
 elapsed over ranks is reported.  Data: synthetic 352x352 polyp images/masks, random-init weights.
 
-Per-GPU micro-batch defaults to 128 images (the north star sizes micro-batches to fill the 288 GB of
-HBM3E; 128 x 352^2 DUCKNet-17 needs ~103 GiB): at the reference's 16 the step is dominated by ~2.7k
-fixed-cost launches and, under DDP, 584 SyncBN exchanges.  ``--batch 16`` reproduces MyConfig's
-per-process batch (measured 265 img/s vs 376 img/s at 128 on one MI355X, ``profiles/r01_fused_v8_*``).
+Per-GPU micro-batch defaults to 384 images on the fused engine: the north star sizes micro-batches to
+fill the 288 GB of HBM3E, and 384 x 352^2 DUCKNet-17 peaks at 200 GiB (measured on one MI355X: 434 img/s
+at 128 / 67 GiB, 445 at 256 / 134 GiB, 450 at 384 / 200 GiB -- the small deep layers fill the chip
+better).  The eager engine defaults to 128 (its NCHW step needs ~103 GiB there).  At the reference's
+16 the step is dominated by fixed-cost launches and, under DDP, SyncBN exchanges; ``--batch 16``
+reproduces MyConfig's per-process batch.
 
 ``--impl fused`` (default) runs the MI355X-native engine (HIP kernels + hipGraph); ``--impl eager``
 runs the same step with stock PyTorch-ROCm (MIOpen convs, torch DDP/SyncBN) = the in-house
@@ -35,8 +37,8 @@ def parse_args(argv=None):
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--batch', type=int, default=128,
-                   help='per-GPU micro-batch (images); 128 x 352^2 uses ~103 GiB of the 288 GiB HBM3E')
+    p.add_argument('--batch', type=int, default=None,
+                   help='per-GPU micro-batch (images); default 384 fused (200 GiB of the 288 GiB HBM3E), 128 eager')
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
     p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
@@ -53,10 +55,14 @@ def parse_args(argv=None):
                    help='augment (default): every step draws a fresh MyConfig-augmented batch from an HBM-resident '
                         'synthetic polyp split (GPU augmentation kernels, inside the timed loop); fixed: replay one '
                         'resident batch (isolates the model step)')
-    p.add_argument('--train-images', type=int, default=128, help='synthetic train split size (per rank)')
+    p.add_argument('--train-images', type=int, default=128,
+                   help='synthetic train split size (per rank; a larger --batch spans several epochs of it)')
     p.add_argument('--val-images', type=int, default=32, help='held-out synthetic val split for the Dice (0 = skip)')
     p.add_argument('--lr', type=float, default=1e-3, help='Adam lr per GPU (reference: 0.1 * base_lr * gpu_num)')
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    if a.batch is None:
+        a.batch = 384 if a.impl == 'fused' and a.model == 'ducknet' and a.base_channel == 17 else 128
+    return a
 
 
 def synthetic_split(n, size, seed):

@@ -175,10 +175,18 @@ class DeviceAugLoader:
             yield self.batch(order[i:i + B])
 
     def stream(self):
-        """Endless epoch-after-epoch index batches (bench / step-based training)."""
+        """Endless epoch-after-epoch index batches (bench / step-based training).  A batch larger than
+        the split spans consecutive epochs (each epoch a fresh permutation) instead of never filling."""
+        B = self.batch_size
+        if B > len(self.data):
+            buf = []
+            while True:
+                while len(buf) < B:
+                    buf.extend(self._order())
+                yield buf[:B]
+                buf = buf[B:]
         while True:
             order = self._order()
-            B = self.batch_size
             for i in range(0, len(order) - B + 1, B):
                 yield order[i:i + B]
 
