@@ -591,6 +591,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_stat_blocks", &conv_stat_blocks_t);
   m.def("conv_uses_halo", &conv_uses_halo_t);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
+  m.def("conv_set_small_halo", [](bool on) { conv_set_small_halo(on ? 1 : 0); });
   m.def("conv_set_phase", [](bool on) { conv_set_phase(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);
   m.def("unpack_wgrad", &unpack_wgrad_t, py::arg("src"), py::arg("dst"), py::arg("nrow"), py::arg("nch"),

@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restri
 struct HaloGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
   int xtab;                          // deferred-BN prologue present: LDS coefficient table (3 x Cip fp32)
-  int mi, pipe;                      // row-group size (16*mi rows) and PIPE mode chosen by conv_halo_ok
+  int mi, pipe, nj;                  // row-group size (16*mi rows), PIPE mode, pixel columns per wave
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
   int dbg;                           // perf knock-outs (env MSP_HALO_DBG; 0 in production): 1 no y stores,
@@ -1378,6 +1378,14 @@ static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
 // whole (one chunk, LDS <= 64 KB) or -- single row group only -- in chunks of CC channels (CC | Cip, a
 // chunk's staging fits the kHaloLd registers per thread), widest CC first.
 static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe) ? 8 : 4; }
+// env MSP_HALO_SMALL=1 enables the 128-pixel (NJ 2) halo tiles for inputs too wide for 256 pixels.  Off by
+// default: measured 1.3 % slower per step (L4 3x3 fwd -10 %, but dgrad +8 %, 1x7 fwd +26 %: at NJ 2 each
+// B fragment feeds only MI MFMAs and the halo ring is 40 % of the tile; profiles/r02/conv_bench_L4_small.log)
+static int g_small_tile = -1;
+static bool halo_small_tile_enabled() {
+  if (g_small_tile < 0) { const char* e = getenv("MSP_HALO_SMALL"); g_small_tile = (e != nullptr && e[0] == '1') ? 1 : 0; }
+  return g_small_tile == 1;
+}
 
 static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
   return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
@@ -1421,15 +1429,21 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   // try 0: PIPE (whole input, halo tile within the prefetch registers); try 1: the standard kernels
   // PIPE pays where its 256-pixel tile is also the standard kernel's (MI 3) and the 3x3 halo is thin;
   // measured slower for the MI<=2 layers (which lose their 512-pixel tile) and the 1x7 / dilated halos
-  // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi)
+  // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi); try 3: a
+  // 128-pixel tile (NJ = 2) for inputs too wide for a 256-pixel halo tile (136 channels at 44^2: the
+  // gather kernel re-reads every input pixel once per tap from L2)
   const bool pipe_ok = pipe_enabled() && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
-  for (int attempt = pipe_ok ? 0 : 1; attempt < 3; ++attempt) {
+  for (int attempt = pipe_ok ? 0 : 1; attempt < 4; ++attempt) {
   const bool pipe = attempt == 0;
-  if (attempt == 2 && halo_fallback_mi(rows) == 0) break;
-  const int mi = pipe ? pipe_pick_mi(rows) : (attempt == 1 ? conv_pick_mi(rows) : halo_fallback_mi(rows));
+  if (attempt == 2 && halo_fallback_mi(rows) == 0) continue;
+  if (attempt == 3 && !halo_small_tile_enabled()) break;
+  const int mi = pipe ? pipe_pick_mi(rows)
+                      : (attempt == 1 ? conv_pick_mi(rows) : (attempt == 2 ? halo_fallback_mi(rows)
+                                                                           : std::max(3, conv_pick_mi(rows))));
   const int n_rg = cdiv(rows, 16 * mi);
-  const int tp = kHaloWaves * halo_nj(mi, pipe) * 16;
-  for (int pass = 0; pass < (pipe ? 1 : 2); ++pass) {          // pass 0: whole input; pass 1: channel chunks
+  const int nj = attempt == 3 ? 2 : halo_nj(mi, pipe);
+  const int tp = kHaloWaves * nj * 16;
+  for (int pass = 0; pass < (pipe || attempt == 3 ? 1 : 2); ++pass) {   // pass 0: whole input; 1: chunks
     if (pass == 1 && n_rg != 1) break;
     for (int d = C8; d >= 1; --d) {
       if (C8 % d != 0) continue;
@@ -1465,6 +1479,7 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
       hg.nch = C8 / d;
       hg.KS = ks;
       hg.mi = mi;
+      hg.nj = nj;
       hg.pipe = pipe ? 1 : 0;
       hg.tw_shift = hg.TW == 16 ? 4 : (hg.TW == 32 ? 5 : 6);
       hg.inv_c8 = 1.0f / (float)d;
@@ -1492,6 +1507,7 @@ static bool halo_enabled() {
 }
 
 void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
+void conv_set_small_halo(int on) { g_small_tile = on ? 1 : 0; }
 bool conv_uses_halo(const ConvGeom& g, bool trans) {
   HaloGeom hg;
   return halo_enabled() && conv_halo_ok(g, trans, hg);
@@ -1583,6 +1599,11 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       }                                                                                                      \
       hipLaunchKernelGGL((K_), dim3(blocks), dim3(64 * kHaloWaves), lds, s, a, hg);                         \
     }
+#define HS_(MI_, BNE_)                                                                                       \
+    if (hmi == MI_ && bne == BNE_ && !pipe && hg.nj == 2) {                                                  \
+      HC_LAUNCH_((conv_halo_kernel<MI_, 2, false, BNE_>))                                                    \
+      return;                                                                                                \
+    }
 #define HC_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe) {                                                                \
       if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))                  \
@@ -1595,10 +1616,12 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       return;                                                                                                \
     }
     const bool bne = a.bn_y != nullptr;
+    HS_(3, false) HS_(4, false) HS_(3, true) HS_(4, true)
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
     HP_(2, false) HP_(3, false) HP_(2, true) HP_(3, true)
     abort();   // no instantiation for this row-group size
 #undef HP_
+#undef HS_
 #undef HC_
 #undef HC_LAUNCH_
   }

@@ -37,7 +37,21 @@ CONV_CASES = [
     (2, 17, 15, 17, 34, (3, 3), 2, (1, 1), (1, 1)),    # odd sizes: uneven output phases in the dgrad
     (2, 16, 16, 64, 128, (1, 1), 2, (0, 0), (1, 1)),   # ResNet downsample: 3 of 4 dgrad phases are empty
     (2, 32, 32, 3, 64, (7, 7), 2, (3, 3), (1, 1)),     # ResNet stem: 49 taps
+    (2, 20, 20, 136, 136, (3, 3), 1, (1, 1), (1, 1)),  # 136 ch: too wide for a 256-px halo tile
+    (2, 13, 19, 136, 72, (3, 3), 1, (2, 2), (2, 2)),   # the same, dilated, ragged tiles
 ]
+
+
+@pytest.mark.parametrize('case', CONV_CASES[-2:])
+def test_conv_small_halo_tile(gpu, case, monkeypatch):
+    """The opt-in 128-pixel (NJ 2) halo tile (MSP_HALO_SMALL=1) on the shapes that take it."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    C = _ext.require()
+    C.conv_set_small_halo(True)
+    try:
+        test_conv_fwd_bwd(gpu, case)
+    finally:
+        C.conv_set_small_halo(False)
 
 
 @pytest.mark.parametrize('case', CONV_CASES)
