@@ -292,6 +292,50 @@ void bn_act_bwd_apply_t(const at::Tensor& dz, const at::Tensor& y, const at::Ten
   bn_act_bwd_apply(bf(dz), bf(y), st, st + Cp, f32(coef), bf(dy), P, Cp, relu ? 1 : 0, cur_stream());
 }
 
+// DUCK tail backward passes (bn.hip): out_bn (dz, ys, stats, coef) + k branch-last BNs (y_i, stats_i
+// [, coef_i, dy_i]); part = fp32 [k, bn_tail_blocks(P, Cp), 2, Cp]
+static void tail_check(const at::Tensor& dz, const at::Tensor& ys, const at::Tensor& ostats, const at::Tensor& ocoef,
+                       const std::vector<at::Tensor>& y, const std::vector<at::Tensor>& st, int64_t P, int64_t Cp) {
+  CHECK_BF16(dz); CHECK_BF16(ys); CHECK_F32(ostats); CHECK_F32(ocoef);
+  TORCH_CHECK(Cp % 8 == 0 && Cp <= kTailMaxCp, "tail passes: Cp a multiple of 8, <= ", kTailMaxCp);
+  TORCH_CHECK(!y.empty() && (int)y.size() <= kTailMax && st.size() == y.size(), "1..6 branches");
+  TORCH_CHECK(dz.numel() == P * Cp && ys.numel() == P * Cp && ostats.numel() == 4 * Cp && ocoef.numel() == 3 * Cp);
+  for (size_t i = 0; i < y.size(); ++i) {
+    CHECK_BF16(y[i]); CHECK_F32(st[i]);
+    TORCH_CHECK(y[i].numel() == P * Cp && st[i].numel() == 4 * Cp, "branch tensor / stats size mismatch");
+  }
+}
+
+void bn_tail_partial_t(const at::Tensor& dz, const at::Tensor& ys, const at::Tensor& ostats, const at::Tensor& ocoef,
+                       bool orelu, std::vector<at::Tensor> y, std::vector<at::Tensor> st, int64_t relu_mask,
+                       const at::Tensor& part, int64_t P, int64_t Cp) {
+  tail_check(dz, ys, ostats, ocoef, y, st, P, Cp);
+  CHECK_F32(part);
+  TORCH_CHECK(part.numel() == (int64_t)y.size() * bn_tail_blocks(P, Cp) * 2 * Cp, "part: [k, bn_tail_blocks, 2, Cp]");
+  std::vector<const uint16_t*> yp;
+  std::vector<const float*> sp;
+  for (size_t i = 0; i < y.size(); ++i) { yp.push_back(bf(y[i])); sp.push_back(f32(st[i])); }
+  bn_tail_partial(bf(dz), bf(ys), f32(ostats), f32(ocoef), orelu ? 1 : 0, (int)y.size(), yp.data(), sp.data(),
+                  (unsigned)relu_mask, f32(part), P, Cp, cur_stream());
+}
+
+void bn_tail_apply_t(const at::Tensor& dz, const at::Tensor& ys, const at::Tensor& ostats, const at::Tensor& ocoef,
+                     bool orelu, std::vector<at::Tensor> y, std::vector<at::Tensor> st, std::vector<at::Tensor> coef,
+                     int64_t relu_mask, std::vector<at::Tensor> dy, int64_t P, int64_t Cp) {
+  tail_check(dz, ys, ostats, ocoef, y, st, P, Cp);
+  TORCH_CHECK(coef.size() == y.size() && dy.size() == y.size(), "coef / dy per branch");
+  std::vector<const uint16_t*> yp;
+  std::vector<const float*> sp, cp;
+  std::vector<uint16_t*> dp;
+  for (size_t i = 0; i < y.size(); ++i) {
+    CHECK_F32(coef[i]); CHECK_BF16(dy[i]);
+    TORCH_CHECK(coef[i].numel() == 3 * Cp && dy[i].numel() == P * Cp, "coef / dy size mismatch");
+    yp.push_back(bf(y[i])); sp.push_back(f32(st[i])); cp.push_back(f32(coef[i])); dp.push_back(bf(dy[i]));
+  }
+  bn_tail_apply(bf(dz), bf(ys), f32(ostats), f32(ocoef), orelu ? 1 : 0, (int)y.size(), yp.data(), sp.data(), cp.data(),
+                (unsigned)relu_mask, dp.data(), P, Cp, cur_stream());
+}
+
 void nchw_to_nhwc_t(const at::Tensor& x, const at::Tensor& y, int64_t Cp) {
   CHECK_F32(x); CHECK_BF16(y);
   TORCH_CHECK(x.dim() == 4, "x must be NCHW");
@@ -615,6 +659,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),
         py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("pscale") = 1.0);
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
+  m.def("bn_tail_partial", &bn_tail_partial_t);
+  m.def("bn_tail_apply", &bn_tail_apply_t);
+  m.def("bn_tail_blocks", [](int64_t P, int64_t Cp) { return bn_tail_blocks(P, (int)Cp); });
+  m.attr("kTailMax") = kTailMax;
+  m.attr("kTailMaxCp") = kTailMaxCp;
   m.def("nchw_to_nhwc", &nchw_to_nhwc_t);
   m.def("nhwc_to_nchw", &nhwc_to_nchw_t);
   m.def("up2_add", &up2_add_t, py::arg("low"), py::arg("skip"), py::arg("out"), py::arg("N"), py::arg("h"),

@@ -419,6 +419,162 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// DUCK tail backward (reference ducknet.py:151-154: out_bn(act(sum of the six branch-last BNs))):
+// the backward of out_bn and of the k branch-last BNs it sums, in two passes instead of 1 + 2k.
+//   dys = out_bn's data-gradient (its apply: relu'(ys) * (k1 dz + k2 ys + k3)) is never written: both
+//   passes recompute it from (dz, ys) in registers -- it IS every branch BN's dz;
+//   pass 1 (tail_partial): per branch i the (sum dzr_i, sum dzr_i * (y_i - mean_i)) channel partials;
+//   pass 2 (tail_apply):   dy_i = k1_i dzr_i + k2_i y_i + k3_i for every branch.
+// Traffic per tail: 8 + 14 tensor passes (dz, ys, k inputs; + k outputs) instead of out_bn's apply (3)
+// plus k separate partial (2 each) and apply (3 each) passes that each re-read dys.
+// The branch coefficients (scale, shift, mean | k1, k2, k3 per channel) sit in LDS; out_bn's in
+// registers (thread-owned 8-channel group, as in the single-BN passes).
+struct TailArgs {
+  const uint16_t* dz;          // out_bn output gradient
+  const uint16_t* ys;          // out_bn input (the branch sum)
+  const float* oscale; const float* oshift; const float* ocoef;   // out_bn stats rows 0/1, coef [3][Cp]
+  int orelu, k;
+  const uint16_t* y[kTailMax];            // branch-last BN inputs
+  const float* st[kTailMax];              // their stats [4][Cp] (scale, shift, mean, invstd)
+  const float* coef[kTailMax];            // their backward coef [3][Cp] (apply pass)
+  unsigned relu;                          // bit i: branch i has a ReLU
+  uint16_t* dy[kTailMax];                 // branch data-gradients (apply pass)
+};
+
+// 8 consecutive floats from LDS as two 16-B reads (the caller guarantees 32-B alignment)
+DEVI void lds8(const float* p, float* d) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// dzr of out_bn for one 8-channel vector: relu'(ys) * (k1 dz + k2 ys + k3) -- the branch BNs' dz
+DEVI void tail_dys(const uint4& gz, const uint4& yv, const float* a, const float* b, const float* k1,
+                   const float* k2, const float* k3, bool relu, float* d) {
+  float g[8], v[8];
+  unpack8(gz, g);
+  unpack8(yv, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
+    d[e] = bf2f(f2bf(k1[e] * gr + k2[e] * v[e] + k3[e]));   // rounded like the materialised dys
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, float* __restrict__ part, long P, int Cp) {
+  extern __shared__ float tsm[];          // [k][3][Cp] branch scale, shift, mean; then red[2][kBlock][8]
+  float* red = tsm + t.k * 3 * Cp;
+  const int CG = Cp >> 3, R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG, c0 = 8 * cg;
+  for (int i = tid; i < t.k * 3 * Cp; i += kBlock) {
+    const int b = i / (3 * Cp), rem = i - b * 3 * Cp;
+    tsm[i] = t.st[b][rem];                // rows 0..2 of the branch's stats = scale, shift, mean
+  }
+  float a[8], sh[8], k1[8], k2[8], k3[8];
+  load8f(t.oscale + c0, a); load8f(t.oshift + c0, sh);
+  load8f(t.ocoef + c0, k1); load8f(t.ocoef + Cp + c0, k2); load8f(t.ocoef + 2 * Cp + c0, k3);
+  float s[kTailMax][8], q[kTailMax][8];
+#pragma unroll
+  for (int i = 0; i < kTailMax; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[i][e] = 0.f; q[i][e] = 0.f; }
+  __syncthreads();
+  if (r < R) {
+    const long stride = (long)gridDim.x * R;
+    for (long p = (long)blockIdx.x * R + r; p < P; p += stride) {
+      const long off = p * Cp + c0;
+      const uint4 gz = *reinterpret_cast<const uint4*>(t.dz + off);
+      const uint4 yv = *reinterpret_cast<const uint4*>(t.ys + off);
+      uint4 yi[kTailMax];
+#pragma unroll
+      for (int i = 0; i < kTailMax; ++i)
+        yi[i] = i < t.k ? *reinterpret_cast<const uint4*>(t.y[i] + off) : make_uint4(0, 0, 0, 0);
+      float d[8];
+      tail_dys(gz, yv, a, sh, k1, k2, k3, t.orelu != 0, d);
+#pragma unroll
+      for (int i = 0; i < kTailMax; ++i) {
+        if (i >= t.k) break;
+        float sc[8], shf[8], mu[8], v[8];
+        lds8(tsm + i * 3 * Cp + c0, sc);           // 16-B LDS reads (rows are 32-B aligned: Cp % 8 == 0)
+        lds8(tsm + i * 3 * Cp + Cp + c0, shf);
+        lds8(tsm + i * 3 * Cp + 2 * Cp + c0, mu);
+        unpack8(yi[i], v);
+        const bool rl = (t.relu >> i) & 1u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gr = (!rl || fmaf(v[e], sc[e], shf[e]) > 0.f) ? d[e] : 0.f;
+          s[i][e] += gr;
+          q[i][e] += gr * (v[e] - mu[e]);
+        }
+      }
+    }
+  }
+  // per branch: block column reduction -> part[i][blk][2][Cp] (fixed order: deterministic)
+  const long nblk = gridDim.x;
+#pragma unroll
+  for (int i = 0; i < kTailMax; ++i) {
+    if (i >= t.k) break;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[(0 * kBlock + tid) * 8 + e] = s[i][e]; red[(1 * kBlock + tid) * 8 + e] = q[i][e]; }
+    __syncthreads();
+    for (int c = tid; c < Cp; c += kBlock) {
+      const int g = c >> 3, e = c & 7;
+      float ss = 0.f, qq = 0.f;
+      for (int rr = 0; rr < R; ++rr) { ss += red[(rr * CG + g) * 8 + e]; qq += red[(kBlock + rr * CG + g) * 8 + e]; }
+      part[(((long)i * nblk + blockIdx.x) * 2 + 0) * Cp + c] = ss;
+      part[(((long)i * nblk + blockIdx.x) * 2 + 1) * Cp + c] = qq;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bn_tail_apply_kernel(TailArgs t, long P, int Cp) {
+  extern __shared__ float tsm[];          // [k][5][Cp] branch scale, shift, k1, k2, k3
+  const int CG = Cp >> 3, R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG, c0 = 8 * cg;
+  for (int i = tid; i < t.k * 5 * Cp; i += kBlock) {
+    const int b = i / (5 * Cp), rem = i - b * 5 * Cp;
+    tsm[i] = rem < 2 * Cp ? t.st[b][rem] : t.coef[b][rem - 2 * Cp];
+  }
+  float a[8], sh[8], k1[8], k2[8], k3[8];
+  load8f(t.oscale + c0, a); load8f(t.oshift + c0, sh);
+  load8f(t.ocoef + c0, k1); load8f(t.ocoef + Cp + c0, k2); load8f(t.ocoef + 2 * Cp + c0, k3);
+  __syncthreads();
+  if (r >= R) return;
+  // two pixels per trip: each branch's 5 coefficient rows are read from LDS once for both
+  const long stride = (long)gridDim.x * R;
+  for (long p = (long)blockIdx.x * R + r; p < P; p += 2 * stride) {
+    const long p1 = p + stride;
+    const bool ok1 = p1 < P;
+    const long off0 = p * Cp + c0, off1 = p1 * Cp + c0;
+    float d0[8], d1[8];
+    tail_dys(*reinterpret_cast<const uint4*>(t.dz + off0), *reinterpret_cast<const uint4*>(t.ys + off0), a, sh, k1, k2,
+             k3, t.orelu != 0, d0);
+    tail_dys(ok1 ? *reinterpret_cast<const uint4*>(t.dz + off1) : make_uint4(0, 0, 0, 0),
+             ok1 ? *reinterpret_cast<const uint4*>(t.ys + off1) : make_uint4(0, 0, 0, 0), a, sh, k1, k2, k3,
+             t.orelu != 0, d1);
+#pragma unroll
+    for (int i = 0; i < kTailMax; ++i) {
+      if (i >= t.k) break;
+      const uint4 y0 = *reinterpret_cast<const uint4*>(t.y[i] + off0);
+      const uint4 y1 = ok1 ? *reinterpret_cast<const uint4*>(t.y[i] + off1) : make_uint4(0, 0, 0, 0);
+      const float* cf = tsm + i * 5 * Cp + c0;
+      float sc[8], shf[8], c1[8], c2[8], c3[8], v0[8], v1[8], o0[8], o1[8];
+      lds8(cf, sc); lds8(cf + Cp, shf); lds8(cf + 2 * Cp, c1); lds8(cf + 3 * Cp, c2); lds8(cf + 4 * Cp, c3);
+      unpack8(y0, v0);
+      unpack8(y1, v1);
+      const bool rl = (t.relu >> i) & 1u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g0 = (!rl || fmaf(v0[e], sc[e], shf[e]) > 0.f) ? d0[e] : 0.f;
+        const float g1 = (!rl || fmaf(v1[e], sc[e], shf[e]) > 0.f) ? d1[e] : 0.f;
+        o0[e] = c1[e] * g0 + c2[e] * v0[e] + c3[e];
+        o1[e] = c1[e] * g1 + c2[e] * v1[e] + c3[e];
+      }
+      *reinterpret_cast<uint4*>(t.dy[i] + off0) = pack8(o0);
+      if (ok1) *reinterpret_cast<uint4*>(t.dy[i] + off1) = pack8(o1);
+    }
+  }
+}
+
 // Grid of the channel-owning elementwise passes: ~kUnroll pixels per thread per loop trip, <= 8192 blocks.
 int grid_rows(long P, int CG) {
   const long R = kBlock / CG;
@@ -513,6 +669,38 @@ void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const
   const FinBwd f{count, pscale, scale, invstd, mean, dgamma, dbeta, coef};
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(Cp, kFinCols)), dim3(kFinCols * kFinParts), 0, s, tmp, S, C, Cp,
                      f);
+}
+
+long bn_tail_blocks(long P, int Cp) { return bn_partial_blocks(P, Cp); }
+
+static TailArgs tail_args(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu,
+                          int k, const uint16_t* const* y, const float* const* st, const float* const* coef,
+                          unsigned relu, uint16_t* const* dy, int Cp) {
+  TailArgs t{};
+  t.dz = dz; t.ys = ys; t.oscale = ostats; t.oshift = ostats + Cp; t.ocoef = ocoef; t.orelu = orelu; t.k = k;
+  for (int i = 0; i < k; ++i) {
+    t.y[i] = y[i]; t.st[i] = st[i];
+    t.coef[i] = coef != nullptr ? coef[i] : nullptr;
+    t.dy[i] = dy != nullptr ? dy[i] : nullptr;
+  }
+  t.relu = relu;
+  return t;
+}
+
+void bn_tail_partial(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
+                     const uint16_t* const* y, const float* const* st, unsigned relu, float* part, long P, int Cp,
+                     hipStream_t s) {
+  const TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, nullptr, relu, nullptr, Cp);
+  const size_t lds = ((size_t)k * 3 * Cp + 2 * kBlock * 8) * sizeof(float);
+  hipLaunchKernelGGL(bn_tail_partial_kernel, dim3(bn_tail_blocks(P, Cp)), dim3(kBlock), lds, s, t, part, P, Cp);
+}
+
+void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
+                   const uint16_t* const* y, const float* const* st, const float* const* coef, unsigned relu,
+                   uint16_t* const* dy, long P, int Cp, hipStream_t s) {
+  const TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, coef, relu, dy, Cp);
+  const size_t lds = (size_t)k * 5 * Cp * sizeof(float);
+  hipLaunchKernelGGL(bn_tail_apply_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
 }
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

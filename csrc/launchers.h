@@ -73,7 +73,16 @@ void unpack_wgrad(const float* src, float* dst, int nrow, int nch, int T, int Cp
 
 // bn.hip  (P = number of pixels, Cp = padded channels; partial buffers are [nblk][2][Cp] fp32)
 constexpr int kMaxSumInputs = 8;
+constexpr int kTailMax = 6;           // branch-last BNs summed by a DUCK tail (bn_tail_*)
+constexpr int kTailMaxCp = 512;       // LDS coefficient tables of the tail passes
 long bn_partial_blocks(long P, int Cp);
+long bn_tail_blocks(long P, int Cp);
+void bn_tail_partial(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
+                     const uint16_t* const* y, const float* const* st, unsigned relu, float* part, long P, int Cp,
+                     hipStream_t s);
+void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
+                   const uint16_t* const* y, const float* const* st, const float* const* coef, unsigned relu,
+                   uint16_t* const* dy, long P, int Cp, hipStream_t s);
 // coefs[i] (nullable array / entries): deferred-BN prologue of input i (stats rows, ld = Cp), bit i of
 // relu_mask its ReLU -- the branch sums that feed a BN read the branches' pre-BN tensors directly.
 void sum_stats(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,

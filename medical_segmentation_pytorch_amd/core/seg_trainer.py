@@ -22,7 +22,7 @@ from PIL import Image
 
 from ..models import get_teacher_model
 from ..ops.bn import flush_pending
-from ..runtime.trainer_engine import capture_mode
+from ..runtime.trainer_engine import capture_mode, no_gc
 from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
 from .base_trainer import BaseTrainer
 from ..ops.resample import colorize, resize_bilinear
@@ -92,7 +92,7 @@ class GraphedStep:
         if self.graph is None:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
+            with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
                 self.loss, self.kd = self._body()
         self.graph.replay()
         t._last_kd = self.kd.clone() if self.kd is not None else None   # static graph output

@@ -401,3 +401,206 @@ def bn_act_reference(xs, st: BNState, relu=True, training=True):
     z = torch.zeros(*y.shape[:-1], Cp, dtype=torch.bfloat16, device=y.device)
     z[..., :st.C] = out.to(torch.bfloat16)
     return z
+
+
+# ------------------------------------------------------------------------------------------------
+class BNSpec:
+    """A training-mode BN(+ReLU) the caller has NOT applied yet: ``act(BN(sum(xs)))`` (``xs``: tensors
+    and/or :class:`Deferred`; ``part_info`` as in :func:`bn_act`).  The DUCK tail takes the six
+    branch-last BNs in this form so that their backward runs fused with out_bn's (:func:`duck_tail`)."""
+    __slots__ = ('xs', 'st', 'relu', 'part_info')
+
+    def __init__(self, xs, st, relu, part_info=None):
+        self.xs, self.st, self.relu, self.part_info = list(xs), st, relu, part_info
+
+    def apply(self, training, deferred=True):
+        """The plain path: this BN as its own autograd node (eval mode, or the tail fusion off)."""
+        return bn_act(self.xs, self.st, self.relu, training, self.part_info, deferred=deferred, defer_bwd=True)
+
+
+def _stats_local(C, xs, coefs, rmask, part_info, P, Cp, dev):
+    """(y, part, nblk, width, col_off) of a training BN's input sum (y written only for sums / prologues)."""
+    summed = len(xs) > 1 or bool(coefs)
+    y = torch.empty_like(xs[0]) if summed else xs[0]
+    if part_info is not None and not summed:
+        part, width, col_off = part_info
+        return y, part, part.shape[0], width, col_off
+    nblk = C.bn_partial_blocks(P, Cp)
+    part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+    C.sum_stats(xs, y if summed else None, part, P, Cp, coefs, rmask)
+    return y, part, nblk, Cp, 0
+
+
+def _finalize_many(C, jobs, group, dev):
+    """Forward finalize of several BNs: jobs = [(st, part, nblk, width, col_off, Cp, count, stats)].  One
+    launch each on a single rank; under SyncBN ONE all-reduce of every BN's (sum, sum^2) row."""
+    world = _world(group)
+    if world == 1:
+        for st, part, nblk, width, col_off, Cp, count, stats in jobs:
+            tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
+            g_ = st.weight.detach() if st.weight is not None else None
+            b_ = st.bias.detach() if st.bias is not None else None
+            C.bn_reduce_finalize(part, nblk, width, col_off, st.C, Cp, tmp, _counters(dev), count, g_, b_,
+                                 st.running_mean, st.running_var, st.momentum, st.eps, stats)
+        return
+    need_stats_all()
+    rows = [_channel_sums(C, part, nblk, width, col_off, Cp, group, dev, reduce=False)
+            for st, part, nblk, width, col_off, Cp, count, stats in jobs]
+    buf = torch.cat([r.reshape(-1) for r in rows])
+    dist.all_reduce(buf, group=group)
+    EXCHANGES[0] += 1
+    o = 0
+    for (st, part, nblk, width, col_off, Cp, count, stats), r in zip(jobs, rows):
+        g_ = st.weight.detach() if st.weight is not None else None
+        b_ = st.bias.detach() if st.bias is not None else None
+        C.bn_finalize(buf[o:o + r.numel()].view(1, -1), st.C, Cp, count, g_, b_, st.running_mean, st.running_var,
+                      st.momentum, st.eps, True, stats)
+        o += r.numel()
+
+
+def need_stats_all():
+    _FWD.flush()
+
+
+class _DuckTail(torch.autograd.Function):
+    """out_bn(act(sum_i act_i(BN_i(sum(xs_i))))) -- the DUCK block tail (reference ducknet.py:151-154) --
+    with the six branch-last BNs and out_bn as ONE autograd node.  Forward: the branch BNs' statistics
+    (one SyncBN collective for all six), then out_bn's sum + statistics pass over their deferred outputs.
+    Backward: out_bn's partial pass, then ``bn_tail_partial`` (every branch BN's channel partials, with
+    out_bn's data-gradient recomputed in registers -- it is never written), the branch finalizes (one
+    collective under SyncBN), and ``bn_tail_apply`` (every branch data-gradient in one pass)."""
+
+    @staticmethod
+    def forward(ctx, specs, out_st, out_relu, pros, nx, *args):
+        C = require()
+        ctx.set_materialize_grads(False)
+        k = len(specs)
+        flat = [a.contiguous() for a in args[:sum(nx)]]
+        y0 = flat[0]
+        Cp = y0.shape[-1]
+        P = y0.numel() // Cp
+        dev = y0.device
+        group = out_st.group
+        world = _world(group)
+        count = float(P * world)
+        ys, stats, jobs, o = [], [], [], 0
+        for sp, n, (coefs, rmask) in zip(specs, nx, pros):
+            xs = flat[o:o + n]
+            o += n
+            y, part, nblk, width, col_off = _stats_local(C, xs, coefs, rmask, sp.part_info, P, Cp, dev)
+            st_t = torch.empty(4, Cp, dtype=torch.float32, device=dev)
+            jobs.append((sp.st, part, nblk, width, col_off, Cp, count, st_t))
+            ys.append(y)
+            stats.append(st_t)
+        _finalize_many(C, jobs, group, dev)
+        # out_bn over the branches' deferred outputs
+        relu_mask = sum(int(bool(sp.relu)) << i for i, sp in enumerate(specs))
+        y_sum = torch.empty_like(y0)
+        nblk = C.bn_partial_blocks(P, Cp)
+        part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+        C.sum_stats(ys, y_sum, part, P, Cp, stats, relu_mask)
+        o_stats = torch.empty(4, Cp, dtype=torch.float32, device=dev)
+        _finalize_many(C, [(out_st, part, nblk, Cp, 0, Cp, count, o_stats)], group, dev)
+        for sp in list(specs) + [out_st]:
+            st = sp if isinstance(sp, BNState) else sp.st
+            if st.count_nbt and st.num_batches_tracked is not None:
+                st.num_batches_tracked.add_(1)
+        ctx.specs, ctx.out_st, ctx.out_relu, ctx.nx, ctx.k, ctx.count = specs, out_st, out_relu, nx, k, count
+        ctx.relu_mask = relu_mask
+        ctx.save_for_backward(y_sum, o_stats, *ys, *stats)
+        ctx.mark_non_differentiable(o_stats)
+        return y_sum, o_stats
+
+    @staticmethod
+    def backward(ctx, dz, _dstats=None):
+        C = require()
+        need_grads([dz])
+        k = ctx.k
+        saved = ctx.saved_tensors
+        y_sum, o_stats = saved[0], saved[1]
+        ys, stats = list(saved[2:2 + k]), list(saved[2 + k:2 + 2 * k])
+        Cp = y_sum.shape[-1]
+        P = y_sum.numel() // Cp
+        dev = y_sum.device
+        out_st: BNState = ctx.out_st
+        group = out_st.group
+        world = _world(group)
+        dz = torch.zeros_like(y_sum) if dz is None else dz.contiguous()
+        sts = [sp.st for sp in ctx.specs] + [out_st]
+        # parameter-gradient targets: arena sinks, else fresh buffers returned to autograd
+        gb = []
+        for st in sts:
+            g_t = st.weight_sink if st.weight_sink is not None else (
+                torch.zeros(Cp, dtype=torch.float32, device=dev) if st.weight is not None else None)
+            b_t = st.bias_sink if st.bias_sink is not None else (
+                torch.zeros(Cp, dtype=torch.float32, device=dev) if st.bias is not None else None)
+            gb.append((g_t, b_t))
+
+        def finalize(rows_parts, which):
+            """backward finalize of BNs ``which`` from their partials (one collective under SyncBN)."""
+            coefs = [torch.empty(3, Cp, dtype=torch.float32, device=dev) for _ in which]
+            if world == 1:
+                for (part, nblk), i, cf in zip(rows_parts, which, coefs):
+                    tmp = torch.empty(C.bn_reduce_splits(nblk), 2 * Cp, dtype=torch.float64, device=dev)
+                    st_i = o_stats if i == k else stats[i]
+                    C.bn_reduce_bwd_finalize(part, nblk, sts[i].C, Cp, tmp, _counters(dev), ctx.count, st_i,
+                                             gb[i][0], gb[i][1], cf, 1.0)
+                return coefs
+            rows = [_channel_sums(C, part, nblk, Cp, 0, Cp, group, dev, reduce=False) for part, nblk in rows_parts]
+            buf = torch.cat([r.reshape(-1) for r in rows])
+            dist.all_reduce(buf, group=group)
+            EXCHANGES[0] += 1
+            o = 0
+            for r, i, cf in zip(rows, which, coefs):
+                st_i = o_stats if i == k else stats[i]
+                C.bn_bwd_finalize(buf[o:o + r.numel()].view(1, -1), sts[i].C, Cp, ctx.count, st_i, gb[i][0], gb[i][1],
+                                  cf, 1.0 / world)
+                o += r.numel()
+            return coefs
+
+        nblk = C.bn_partial_blocks(P, Cp)
+        part = torch.empty(nblk, 2, Cp, dtype=torch.float32, device=dev)
+        C.bn_act_bwd_partial(dz, y_sum, o_stats, part, P, Cp, ctx.out_relu)
+        (o_coef,) = finalize([(part, nblk)], [k])
+        tb = C.bn_tail_blocks(P, Cp)
+        tpart = torch.empty(k, tb, 2, Cp, dtype=torch.float32, device=dev)
+        C.bn_tail_partial(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, ctx.relu_mask, tpart, P, Cp)
+        coefs = finalize([(tpart[i], tb) for i in range(k)], list(range(k)))
+        dys = [torch.empty_like(y_sum) for _ in range(k)]
+        C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, coefs, ctx.relu_mask, dys, P, Cp)
+        for st in sts:
+            if st.ready_hook is not None:
+                st.ready_hook([t for t in (st.weight, st.bias) if t is not None])
+        grads = []
+        for dy, n in zip(dys, ctx.nx):
+            grads += [dy] * n
+        pgrads = []
+        base = 5 + len(grads)   # forward inputs: specs, out_st, out_relu, pros, nx, *flat, (gamma, beta) per BN
+        for j, (st, (g_t, b_t)) in enumerate(zip(sts, gb)):
+            need_g = ctx.needs_input_grad[base + 2 * j] and st.weight_sink is None
+            need_b = ctx.needs_input_grad[base + 2 * j + 1] and st.bias_sink is None
+            pgrads.append(g_t[:st.C] if need_g else None)
+            pgrads.append(b_t[:st.C] if need_b else None)
+        ctx.specs = None   # drop the input references held since forward
+        return (None, None, None, None, None) + tuple(grads) + tuple(pgrads)
+
+
+def duck_tail(specs, out_st: BNState, out_relu=True):
+    """Training-mode DUCK tail over ``specs`` (:class:`BNSpec`, the branch-last BNs): returns out_bn's
+    output as a :class:`Deferred`.  Falls back to separate BN nodes where the fused passes do not apply."""
+    C = require()
+    widths = {(x.t if isinstance(x, Deferred) else x).shape[-1] for sp in specs for x in sp.xs}
+    if len(specs) > C.kTailMax or len(widths) != 1 or widths.pop() > C.kTailMaxCp:
+        outs = [sp.apply(True) for sp in specs]
+        return bn_act(outs, out_st, out_relu, True, deferred=True, defer_bwd=True)
+    flat, nx, pros = [], [], []
+    for sp in specs:
+        ts, cs, mask = split_inputs(sp.xs)
+        flat += ts
+        nx.append(len(ts))
+        pros.append((cs, mask))
+    params = []
+    for st in [sp.st for sp in specs] + [out_st]:
+        params += [st.weight, st.bias]
+    out, stats = _DuckTail.apply(specs, out_st, out_relu, pros, nx, *flat, *params)
+    return Deferred(out, stats, out_relu)

@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.bn import BNState, BwdStatsHandle, Deferred, bn_act, flush_pending, materialize
+from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
@@ -35,6 +35,8 @@ from ..ops.pool import add_act, maxpool, up2_cat
 _BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
 # env MSP_DEFER_BN=0 materialises every BN output (bn_act_apply pass) instead of deferring it (A/B switch)
 _DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
+# env MSP_DUCK_TAIL=0 runs the DUCK tail's seven BNs as separate autograd nodes (A/B switch; see ops.bn.duck_tail)
+_DUCK_TAIL = os.environ.get('MSP_DUCK_TAIL', '1') != '0'
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 
@@ -220,13 +222,17 @@ class FusedExecutor:
     # the level's statistic exchanges together (ops.bn._Pending: ONE collective per level instead of one
     # per BN); and since autograd runs ready nodes in reverse creation order, the backward reaches every
     # BN of a level before any conv of it, which batches the backward exchanges the same way.
-    def _g_cba(self, m, x, training, single=False):
+    def _g_cba(self, m, x, training, single=False, raw=False):
+        """``raw``: return the BN as a :class:`BNSpec` (applied later by the DUCK tail)."""
         xs = x if isinstance(x, (list, tuple)) else [x]
         plan = self.plan_conv(m[0], gi=len(xs))
         (y,), part = self._conv(plan, xs, training)
         yield
-        z = self._bn_out([y], self.bn(m[1]), _is_relu(m[2]), training, (part, plan.rows, 0) if training else None,
-                         single)
+        if raw:
+            z = BNSpec([y], self.bn(m[1]), _is_relu(m[2]), (part, plan.rows, 0))
+        else:
+            z = self._bn_out([y], self.bn(m[1]), _is_relu(m[2]), training,
+                             (part, plan.rows, 0) if training else None, single)
         yield
         return z
 
@@ -237,25 +243,29 @@ class FusedExecutor:
         yield
         return z
 
-    def _g_residual_tail(self, m, upper_y, low_fn, training, single_out=False):
+    def _g_residual_tail(self, m, upper_y, low_fn, training, single_out=False, raw=False):
         """ResidualBlock whose fused 3x3+1x1 launch already ran: (low BN) -> cba -> bn(upper + lower)."""
         low = yield from self._g_bn(low_fn)
         low = yield from self._g_cba(m.lower_branch[1], low, training)
+        if raw:
+            return (yield from self._g_bn(lambda: BNSpec([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]))))
         return (yield from self._g_bn(lambda: self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]),
                                                             training, single=single_out)))
 
-    def _g_residual(self, m, x, training, single_out=False):
+    def _g_residual(self, m, x, training, single_out=False, raw=False):
         plan = self.plan_fused3x3(('res', id(m)), [m.lower_branch[0][0]], [m.upper_branch])
         ys, part = self._conv(plan, [x], training)
         low_fn = lambda: self.bn_from_group(m.lower_branch[0][1], m.lower_branch[0][2], ys, part, plan, 0,  # noqa: E731
                                             training, single=True)
-        return (yield from self._g_residual_tail(m, ys[1], low_fn, training, single_out))
+        return (yield from self._g_residual_tail(m, ys[1], low_fn, training, single_out, raw))
 
-    def _g_chain(self, first, blocks, training):
-        """``first`` (a branch generator) followed by residual ``blocks``, each feeding the next only."""
+    def _g_chain(self, first, blocks, training, raw=False):
+        """``first`` (a branch generator) followed by residual ``blocks``, each feeding the next only;
+        ``raw``: the last block's BN comes back as a :class:`BNSpec`."""
         o = yield from first
         for k, blk in enumerate(blocks):
-            o = yield from self._g_residual(blk, o, training, single_out=k + 1 < len(blocks))
+            o = yield from self._g_residual(blk, o, training, single_out=k + 1 < len(blocks),
+                                            raw=raw and k + 1 == len(blocks))
         return o
 
     def _g_parallel(self, gens):
@@ -327,30 +337,37 @@ class FusedExecutor:
             ys_l, part_l, plan_l, j = src[g]
             return lambda: self.bn_from_group(seq[1], seq[2], ys_l, part_l, plan_l, j, training, single=True)
 
+        # training: each branch's LAST BN comes back unapplied (BNSpec) and runs inside the fused tail
+        raw = training and _DUCK_TAIL and _DEFER_BN
+
         def wide():      # d1 -> d2 -> d3
             o = yield from self._g_bn(bnz(b1[0], 0))
             o = yield from self._g_cba(b1[1], o, training, single=True)
-            return (yield from self._g_cba(b1[2], o, training))
+            return (yield from self._g_cba(b1[2], o, training, raw=raw))
 
         def mid():       # d1 -> d2
             o = yield from self._g_bn(bnz(b2[0], 1))
-            return (yield from self._g_cba(b2[1], o, training))
+            return (yield from self._g_cba(b2[1], o, training, raw=raw))
 
         def sep():       # 1x7 -> 7x1
             o = yield from self._g_cba(b6[0], xb, training, single=True)
-            return (yield from self._g_cba(b6[1], o, training))
+            return (yield from self._g_cba(b6[1], o, training, raw=raw))
 
         rest4, rest5 = list(b4)[1:], list(b5)[1:]
         # residual x1 / x2 / x3: the first block's two convs come from the fused launch; inside a chain a
         # block's output feeds only the next block's fused conv
         branches = [wide(), mid(),
-                    self._g_residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training),
+                    self._g_residual_tail(b3, ys[5], bnz(b3.lower_branch[0], 2), training, raw=raw),
                     self._g_chain(self._g_residual_tail(r4, ys[6], bnz(r4.lower_branch[0], 3), training,
-                                                        single_out=bool(rest4)), rest4, training),
+                                                        single_out=bool(rest4), raw=raw and not rest4),
+                                  rest4, training, raw=raw),
                     self._g_chain(self._g_residual_tail(r5, ys[7], bnz(r5.lower_branch[0], 4), training,
-                                                        single_out=bool(rest5)), rest5, training),
+                                                        single_out=bool(rest5), raw=raw and not rest5),
+                                  rest5, training, raw=raw),
                     sep()]
         outs = yield from self._g_parallel(branches)
+        if raw:   # six branch-last BNs + out_bn: one fused backward (ops.bn.duck_tail)
+            return (yield from self._g_bn(lambda: duck_tail(outs, self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]))))
         return (yield from self._g_bn(lambda: bn_act(outs, self.bn(m.out_bn[0]), _is_relu(m.out_bn[1]), training,
                                                      deferred=_DEFER_BN, defer_bwd=True)))
 

@@ -8,7 +8,9 @@ only per-step host work is writing the OneCycle values into the hyper-parameter 
 """
 from __future__ import annotations
 
+import contextlib
 import copy
+import gc
 
 import torch
 import torch.distributed as dist
@@ -115,10 +117,25 @@ class FusedStep:
         if self.graph is None:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
+            with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
                 self.loss = self._body()
         self.graph.replay()
         return self.loss
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Cyclic GC off while a step is captured: a collection that frees objects from an earlier graph or
+    trainer (their CUDA-graph / event destructors) in the middle of a capture aborts the process (seen
+    when the allocations of a captured step crossed a GC threshold).  torch.cuda.graph collects right
+    before the capture, so nothing is left pending."""
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def capture_mode():

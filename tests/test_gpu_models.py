@@ -154,3 +154,27 @@ def test_bn_epilogue_on_off_full_model(gpu, monkeypatch):
     assert _cos(res[0][0], res[1][0]) > 0.9999
     cs = [_cos(a, b) for a, b in zip(res[0][1], res[1][1]) if b.abs().sum() > 0]
     assert min(cs) > 0.99 and sum(cs) / len(cs) > 0.999, (min(cs), sum(cs) / len(cs))
+
+
+def test_duck_tail_fused_matches_separate_nodes(gpu, monkeypatch):
+    """The fused DUCK tail (six branch-last BNs + out_bn as one node: bn_tail_partial / bn_tail_apply)
+    vs the same BNs as seven separate autograd nodes: same logits, parameter grads and running stats."""
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    torch.manual_seed(0)
+    base = DuckNet(2, 3, 17).to(gpu).train()
+    x = torch.randn(2, 3, 96, 96, device=gpu)
+    tgt = torch.randint(0, 2, (2, 96, 96), device=gpu)
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(fused_model, '_DUCK_TAIL', on)
+        model = copy.deepcopy(base)
+        out = FusedExecutor(model)(x, training=True)
+        F.cross_entropy(out, tgt).backward()
+        torch.cuda.synchronize()
+        res.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()],
+                    [b.clone() for b in model.buffers()]))
+    assert _cos(res[0][0], res[1][0]) > 0.9999
+    cs = [_cos(a, b) for a, b in zip(res[0][1], res[1][1]) if b.abs().sum() > 0]
+    assert min(cs) > 0.99 and sum(cs) / len(cs) > 0.999, (min(cs), sum(cs) / len(cs))
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)
