@@ -461,6 +461,9 @@ DEVI void tail_dys(const uint4& gz, const uint4& yv, const float* a, const float
   }
 }
 
+// KM: compile-time branch capacity (the 2 x KM x 8 accumulators dominate the register budget; the host
+// runs six branches as two KM = 3 launches, which re-read dz and ys once but double the occupancy)
+template <int KM>
 __global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, float* __restrict__ part, long P, int Cp) {
   extern __shared__ float tsm[];          // [k][3][Cp] branch scale, shift, mean; then red[2][kBlock][8]
   float* red = tsm + t.k * 3 * Cp;
@@ -472,9 +475,9 @@ __global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, flo
   float a[8], sh[8], k1[8], k2[8], k3[8];
   load8f(t.oscale + c0, a); load8f(t.oshift + c0, sh);
   load8f(t.ocoef + c0, k1); load8f(t.ocoef + Cp + c0, k2); load8f(t.ocoef + 2 * Cp + c0, k3);
-  float s[kTailMax][8], q[kTailMax][8];
+  float s[KM][8], q[KM][8];
 #pragma unroll
-  for (int i = 0; i < kTailMax; ++i)
+  for (int i = 0; i < KM; ++i)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s[i][e] = 0.f; q[i][e] = 0.f; }
   __syncthreads();
@@ -484,14 +487,14 @@ __global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, flo
       const long off = p * Cp + c0;
       const uint4 gz = *reinterpret_cast<const uint4*>(t.dz + off);
       const uint4 yv = *reinterpret_cast<const uint4*>(t.ys + off);
-      uint4 yi[kTailMax];
+      uint4 yi[KM];
 #pragma unroll
-      for (int i = 0; i < kTailMax; ++i)
+      for (int i = 0; i < KM; ++i)
         yi[i] = i < t.k ? *reinterpret_cast<const uint4*>(t.y[i] + off) : make_uint4(0, 0, 0, 0);
       float d[8];
       tail_dys(gz, yv, a, sh, k1, k2, k3, t.orelu != 0, d);
 #pragma unroll
-      for (int i = 0; i < kTailMax; ++i) {
+      for (int i = 0; i < KM; ++i) {
         if (i >= t.k) break;
         float sc[8], shf[8], mu[8], v[8];
         lds8(tsm + i * 3 * Cp + c0, sc);           // 16-B LDS reads (rows are 32-B aligned: Cp % 8 == 0)
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, flo
   // per branch: block column reduction -> part[i][blk][2][Cp] (fixed order: deterministic)
   const long nblk = gridDim.x;
 #pragma unroll
-  for (int i = 0; i < kTailMax; ++i) {
+  for (int i = 0; i < KM; ++i) {
     if (i >= t.k) break;
 #pragma unroll
     for (int e = 0; e < 8; ++e) { red[(0 * kBlock + tid) * 8 + e] = s[i][e]; red[(1 * kBlock + tid) * 8 + e] = q[i][e]; }
@@ -692,7 +695,11 @@ void bn_tail_partial(const uint16_t* dz, const uint16_t* ys, const float* ostats
                      hipStream_t s) {
   const TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, nullptr, relu, nullptr, Cp);
   const size_t lds = ((size_t)k * 3 * Cp + 2 * kBlock * 8) * sizeof(float);
-  hipLaunchKernelGGL(bn_tail_partial_kernel, dim3(bn_tail_blocks(P, Cp)), dim3(kBlock), lds, s, t, part, P, Cp);
+  if (k <= 3)
+    hipLaunchKernelGGL(bn_tail_partial_kernel<3>, dim3(bn_tail_blocks(P, Cp)), dim3(kBlock), lds, s, t, part, P, Cp);
+  else
+    hipLaunchKernelGGL(bn_tail_partial_kernel<kTailMax>, dim3(bn_tail_blocks(P, Cp)), dim3(kBlock), lds, s, t, part, P,
+                       Cp);
 }
 
 void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,

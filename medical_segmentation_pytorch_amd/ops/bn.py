@@ -462,6 +462,9 @@ def need_stats_all():
     _FWD.flush()
 
 
+_TAIL_SPLIT = __import__('os').environ.get('MSP_TAIL_SPLIT', '1') != '0'
+
+
 class _DuckTail(torch.autograd.Function):
     """out_bn(act(sum_i act_i(BN_i(sum(xs_i))))) -- the DUCK block tail (reference ducknet.py:151-154) --
     with the six branch-last BNs and out_bn as ONE autograd node.  Forward: the branch BNs' statistics
@@ -564,7 +567,13 @@ class _DuckTail(torch.autograd.Function):
         (o_coef,) = finalize([(part, nblk)], [k])
         tb = C.bn_tail_blocks(P, Cp)
         tpart = torch.empty(k, tb, 2, Cp, dtype=torch.float32, device=dev)
-        C.bn_tail_partial(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, ctx.relu_mask, tpart, P, Cp)
+        # branch partials in launches of <= 3 branches (half the accumulator registers -> twice the occupancy
+        # of one six-branch launch, for one extra read of dz and ys; env MSP_TAIL_SPLIT=0: one launch)
+        step = 3 if _TAIL_SPLIT else k
+        for b0 in range(0, k, step):
+            b1 = min(k, b0 + step)
+            C.bn_tail_partial(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys[b0:b1], stats[b0:b1],
+                              ctx.relu_mask >> b0, tpart[b0:b1], P, Cp)
         coefs = finalize([(tpart[i], tb) for i in range(k)], list(range(k)))
         dys = [torch.empty_like(y_sum) for _ in range(k)]
         C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, coefs, ctx.relu_mask, dys, P, Cp)
