@@ -123,3 +123,25 @@ def test_fused_engine_coverage_of_smp_hub():
         assert [f.shape[-1] for f in e(x)][-1] == 64 // os_
     m = smp.DeepLabV3Plus(encoder_name='mobilenet_v2', encoder_weights=None, classes=2).eval()
     assert m(x).shape == (1, 2, 64, 64)
+
+
+def test_duck_split_partitions():
+    """The DUCK first-conv launch split (runtime.fused_model.duck_split): every width's default and every
+    env override is a partition of the 8 convs into consecutive runs (3x3 convs 0-4 first)."""
+    import os
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    for c in (17, 34, 68, 136, 272, 544):
+        parts = fused_model.duck_split(c)
+        assert sorted(i for p in parts for i in p) == list(range(8))
+        assert all(p == list(range(p[0], p[0] + len(p))) for p in parts)
+    assert fused_model.duck_split(17) == [list(range(8))]
+    assert fused_model.duck_split(68) == [[0, 1, 2, 3, 4], [5, 6, 7]]
+    old = os.environ.get('MSP_DUCK_SPLIT')
+    try:
+        os.environ['MSP_DUCK_SPLIT'] = '3+2+3'
+        assert fused_model.duck_split(17) == [[0, 1, 2], [3, 4], [5, 6, 7]]
+    finally:
+        if old is None:
+            os.environ.pop('MSP_DUCK_SPLIT')
+        else:
+            os.environ['MSP_DUCK_SPLIT'] = old
