@@ -1713,7 +1713,12 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
   const long M = (long)g.N * g.OH * g.OW;
   const long nchunks = (M + WG_M - 1) / WG_M;
   P.co_t = rows <= 32 ? 32 : 64;
-  P.k_t = KT <= 64 ? 64 : 128;
+  // K tile 64: the 64 x 128 tile needs 149 VGPRs + 128 AGPRs (1 wave/SIMD); at 64 (2 waves/SIMD) the
+  // strided weight gradients run 1.5-1.9x faster (L1 3x3 s2: 50 -> 76 TF, L3: 80 -> 155 TF; step +0.8 %,
+  // profiles/r02/conv_bench_s2_wgrad_kt.log).  env MSP_DW_GEN_KT=128 restores the wide tile (A/B).
+  static int kt_cap = -1;
+  if (kt_cap < 0) { const char* e = getenv("MSP_DW_GEN_KT"); kt_cap = (e != nullptr && atoi(e) == 128) ? 128 : 64; }
+  P.k_t = (KT <= 64 || kt_cap == 64) ? 64 : 128;
   P.gx = cdiv(KT, P.k_t);
   P.gy = cdiv(rows, P.co_t);
   P.nsplit = std::max(1L, std::min(2048L / ((long)P.gx * P.gy), nchunks));
