@@ -59,8 +59,9 @@ ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>&
 void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys,
               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& stat_part,
               std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
-              OptTensors xc, int64_t xrelu) {
+              OptTensors xc, int64_t xrelu, bool accumulate) {
   ConvGeom g = make_geom(dims, dy, dx);
+  TORCH_CHECK(!accumulate || !(stat_part.has_value() && stat_part->defined()), "accumulate: no stats epilogue");
   TORCH_CHECK((int)xs.size() == g.Gi && (int)ys.size() == g.Go, "group count mismatch");
   ConvArgs a{};
   for (int i = 0; i < g.Gi; ++i) {
@@ -83,6 +84,7 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   a.stat_part = f32_opt_mut(stat_part);
   fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), a.xc);
   a.xrelu = (unsigned)xrelu;
+  a.accum = accumulate ? 1 : 0;
   a.g = g;
   conv_igemm(a, trans, cur_stream());
 }
@@ -626,7 +628,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
   m.def("conv_fwd", &conv_fwd, py::arg("xs"), py::arg("wp"), py::arg("ys"), py::arg("bias"), py::arg("stat_part"),
         py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{},
-        py::arg("xrelu") = 0);
+        py::arg("xrelu") = 0, py::arg("accumulate") = false);
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_wgrad", &conv_wgrad_t, py::arg("dys"), py::arg("xs"), py::arg("dw"), py::arg("dims"), py::arg("dy"),
         py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{}, py::arg("xrelu") = 0);

@@ -247,9 +247,15 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
           mo = (n * g.OH + (long)qa * pa.s + pa.py) * g.OW + (long)qb * pa.s + pa.px;
         }
         float v[4];
+        float old[4] = {0.f, 0.f, 0.f, 0.f};
+        if (!BNE && a.accum) {   // y += conv(x): add the stored bf16 output (sibling launches' dgrads)
+          const uint2 ov = *reinterpret_cast<const uint2*>(yb + mo * g.Cgo);
+          old[0] = __uint_as_float(ov.x << 16); old[1] = __uint_as_float(ov.x & 0xffff0000u);
+          old[2] = __uint_as_float(ov.y << 16); old[3] = __uint_as_float(ov.y & 0xffff0000u);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] : 0.f;
+          const float o = (cl + r < g.Cgo_l) ? acc[i][j][r] + bv[r] + old[r] : 0.f;
           v[r] = bf2f(f2bf(o));
         }
         if constexpr (BNE) {   // BN-backward partials (Go == 1: cl == cb); y prefetched per row group
@@ -1229,7 +1235,12 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           if (yb[i] == nullptr) continue;
-          const f32x4_t v = acc[i][j];
+          f32x4_t v = acc[i][j];
+          if (a.accum) {   // y += conv(x) (sibling launches' data-gradients)
+            const uint2 ov = *reinterpret_cast<const uint2*>(yb[i] + pm);
+            v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
+            v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
+          }
           if (!(hg.dbg & 1))
             *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
 #pragma unroll
@@ -1252,6 +1263,11 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
           float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = rv[i][r] ? acc[i][j][r] + bv[i][r] : 0.f;
+          if (a.accum) {
+            const uint2 ov = *reinterpret_cast<const uint2*>(yb[i] + pm);
+            o[0] += __uint_as_float(ov.x << 16); o[1] += __uint_as_float(ov.x & 0xffff0000u);
+            o[2] += __uint_as_float(ov.y << 16); o[3] += __uint_as_float(ov.y & 0xffff0000u);
+          }
           const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
           if (!(hg.dbg & 1)) *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
           const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);

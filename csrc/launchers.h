@@ -42,6 +42,9 @@ struct ConvArgs {
   // [4][Cgi] stats (scale row 0, shift row 1) or nullptr; bit i of xrelu = the BN's ReLU.
   const float* xc[kMaxGroups];
   unsigned xrelu;
+  // accumulate: y += conv(x) (the stored bf16 output is read, added in fp32 and re-rounded -- exactly a
+  // separate bf16 add); data-gradients of sibling launches that read the same input.  No BN epilogue.
+  int accum;
   ConvGeom g;
 };
 

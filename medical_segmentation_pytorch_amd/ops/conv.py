@@ -337,6 +337,93 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0)):
     return res
 
 
+class _MultiConvFn(torch.autograd.Function):
+    """Sibling launches over ONE input tensor (the DUCK first convs split per width,
+    ``runtime.fused_model.duck_split``) as one autograd node: the backward writes the input gradient
+    once -- the first plan's data-gradient stores it, every later plan's ACCUMULATES in its epilogue
+    (``conv_fwd(accumulate=True)``: bitwise a separate bf16 add, minus its three tensor passes) --
+    then runs each plan's weight gradient.  Stride-1, single input group, no bias."""
+
+    @staticmethod
+    def forward(ctx, plans, want_stats, pro, x, *weights):
+        C = require()
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        coefs, rmask = pro
+        n, ih, iw, _ = x.shape
+        dev = x.device
+        outs, parts = [], []
+        for plan in plans:
+            oh, ow = plan.out_hw(ih, iw)
+            ys = [torch.empty(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) for _ in range(plan.Go)]
+            dims = plan.fwd_dims(n, ih, iw, oh, ow)
+            dy, dx = _taps(plan.taps_fwd)
+            part = None
+            if want_stats:
+                part = torch.empty(C.conv_stat_blocks(dims, dy, dx), 2, plan.rows, dtype=torch.float32, device=dev)
+            C.conv_fwd([x], plan.pack_fwd(dev), ys, None, part, dims, dy, dx, False, coefs, rmask)
+            outs += ys
+            parts.append(part if part is not None else torch.empty(0, device=dev))
+        ctx.plans, ctx.pro, ctx.shape = plans, pro, (n, ih, iw)
+        ctx.save_for_backward(x)
+        ctx.mark_non_differentiable(*parts)
+        return (*outs, *parts)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        from .bn import need_grads
+        C = require()
+        need_grads(grads)
+        (x,) = ctx.saved_tensors
+        n, ih, iw = ctx.shape
+        dev = x.device
+        dxt, o, per_plan = None, 0, []
+        for plan in ctx.plans:
+            oh, ow = plan.out_hw(ih, iw)
+            gys = [torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None else g.contiguous()
+                   for g in grads[o:o + plan.Go]]
+            o += plan.Go
+            per_plan.append(gys)
+            if ctx.needs_input_grad[3]:
+                wd, Kp_d = plan.pack_dgrad(dev)
+                first = dxt is None
+                if first:
+                    dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
+                dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
+                dy, dx = _taps(plan.taps_bwd)
+                C.conv_fwd(gys, wd, [dxt], None, None, dims_d, dy, dx, False, accumulate=not first)
+        wgrads = []
+        for plan, gys in zip(ctx.plans, per_plan):
+            oh, ow = plan.out_hw(ih, iw)
+            wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro)
+            if plan.ready_hook is not None:
+                plan.ready_hook([b.weight for b in plan.branches])
+        ctx.plans = None
+        return (None, None, None, dxt) + tuple(wgrads)
+
+
+def conv_multi(plans, x, want_stats=False):
+    """Several stride-1 single-group plans on the same input ``x`` (tensor or Deferred) as one node;
+    returns [(outputs, stat partials)] per plan."""
+    from .bn import Deferred, materialize, split_inputs
+    for p in plans:
+        assert p.stride == 1 and p.Gi == 1 and not p.transposed and p.bias is None
+    if isinstance(x, Deferred) and x.z is None:
+        n, ih, iw, _ = x.shape
+        if any(not p.uses_halo(n, ih, iw) for p in plans) and plans[0].Cgi >= 64:
+            x = materialize(x)   # the gather kernel's per-k-step prologue costs more than one pass (see conv)
+    x = x.z if isinstance(x, Deferred) and x.z is not None else x
+    (t,), coefs, mask = split_inputs([x])
+    weights = [b.weight for p in plans for b in p.branches]
+    out = _MultiConvFn.apply(plans, want_stats, (coefs, mask), t, *weights)
+    res, o = [], 0
+    ngo = sum(p.Go for p in plans)
+    for i, p in enumerate(plans):
+        res.append((list(out[o:o + p.Go]), out[ngo + i] if want_stats else None))
+        o += p.Go
+    return res
+
+
 def conv(plan: ConvPlan, xs, want_stats=False, bn_handle=None):
     """Run ``plan`` on input groups ``xs`` (tensors or ``ops.bn.Deferred`` BN outputs, whose
     normalise+ReLU runs as this conv's load prologue); returns (list of Go output tensors, stat

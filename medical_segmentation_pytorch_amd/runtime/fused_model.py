@@ -26,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
-from ..ops.conv import Branch, ConvPlan, PackProgram, conv
+from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
 
@@ -323,12 +323,17 @@ class FusedExecutor:
         # the 8 convs reading xb as one or more multi-output launches (duck_split); src[g] = (outputs,
         # partials, plan, index) of conv g
         src = [None] * 8
+        plans, orders = [], []
         for li, idx in enumerate(duck_split(allc[0].out_channels)):
             i3, i1 = [i for i in idx if i < 5], [i for i in idx if i >= 5]
-            plan = (self.plan_fused3x3(('duck', id(m), li), [allc[i] for i in i3], [allc[i] for i in i1]) if i3
-                    else self.plan_fused1x1(('duck', id(m), li), [allc[i] for i in i1]))
-            ys_l, part_l = conv(plan, [xb], want_stats=training)
-            for j, i in enumerate(i3 + i1):   # plan output groups: 3x3 convs first, then the 1x1s
+            plans.append(self.plan_fused3x3(('duck', id(m), li), [allc[i] for i in i3], [allc[i] for i in i1])
+                         if i3 else self.plan_fused1x1(('duck', id(m), li), [allc[i] for i in i1]))
+            orders.append(i3 + i1)   # plan output groups: 3x3 convs first, then the 1x1s
+        # several launches: one autograd node whose data-gradients accumulate into one dL/dxb
+        outs = ([conv(plans[0], [xb], want_stats=training)] if len(plans) == 1
+                else conv_multi(plans, xb, want_stats=training))
+        for plan, order, (ys_l, part_l) in zip(plans, orders, outs):
+            for j, i in enumerate(order):
                 src[i] = (ys_l, part_l, plan, j)
         ys = [src[i][0][src[i][3]] for i in range(8)]
 

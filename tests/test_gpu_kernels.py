@@ -113,6 +113,42 @@ def test_conv_groups_fused_siblings(gpu):
         assert _rel(c.weight.grad, wv.grad) < 2e-2
 
 
+@pytest.mark.parametrize('c,deferred', [(17, False), (72, True)])
+def test_conv_multi_accumulates_dgrad(gpu, c, deferred):
+    """Sibling launches on one input as one node (ops.conv.conv_multi, the DUCK split): outputs, weight
+    grads and the input gradient (later plans' dgrads accumulate in the epilogue) vs separate launches."""
+    from medical_segmentation_pytorch_amd.ops.bn import Deferred
+    from medical_segmentation_pytorch_amd.ops.conv import conv_multi
+    torch.manual_seed(7)
+    n, h, w = 2, 20, 24
+    c3 = [nn.Conv2d(c, c, 3, 1, 1, bias=False).to(gpu) for _ in range(3)]
+    c1 = [nn.Conv2d(c, c, 1, bias=False).to(gpu) for _ in range(2)]
+    x0 = to_fm_reference(_bf(torch.randn(n, c, h, w, device=gpu)))
+    stats = torch.zeros(4, x0.shape[-1], device=gpu)
+    stats[0, :c] = torch.rand(c, device=gpu) + 0.5
+    stats[1, :c] = torch.randn(c, device=gpu) * 0.1
+    res = []
+    for multi in (False, True):
+        for m in c3 + c1:
+            m.weight.grad = None
+        p3 = ConvPlan(3, 3, c, c, [Branch(m.weight, g, 0, 9) for g, m in enumerate(c3)], padding=(1, 1), Go=3)
+        p1 = ConvPlan(1, 1, c, c, [Branch(m.weight, g, 0, 1) for g, m in enumerate(c1)], Go=2)
+        xt = x0.clone().requires_grad_(True)
+        x = Deferred(xt, stats, True) if deferred else xt
+        if multi:
+            (ya, _), (yb, _) = conv_multi([p3, p1], x)
+        else:
+            ya, _ = conv(p3, [x])
+            yb, _ = conv(p1, [x])
+        outs = list(ya) + list(yb)
+        gs = [to_fm_reference(_bf(torch.randn(n, c, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(k))))
+              for k in range(5)]
+        torch.autograd.backward(outs, gs)
+        res.append([o.float() for o in outs] + [xt.grad.float()] + [m.weight.grad.clone() for m in c3 + c1])
+    for a, b in zip(res[0], res[1]):
+        assert _rel(b, a) < 5e-3, _rel(b, a)
+
+
 def test_conv_group_inputs(gpu):
     """UNet concat: conv over two input tensors without materialising torch.cat."""
     torch.manual_seed(2)
