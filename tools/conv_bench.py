@@ -31,6 +31,10 @@ def layers(b=17):
             L.append((f'L{lvl + 1} fused{gsz} {c}->{gsz}x{c}', lvl, c, c, (3, 3), 1, (1, 1), (1, 1), gsz))
         L.append((f'L{lvl + 1} fused3-1x1 {c}->3x{c}', lvl, c, c, (1, 1), 1, (0, 0), (1, 1), 3))
         L.append((f'L{lvl + 1} 3x3s2 {c}->{2 * c}', lvl, c, 2 * c, (3, 3), 2, (1, 1), (1, 1), 1))
+    # the first DUCK reads the 3-channel image (in_bn(x)): its first convs at 3 -> b
+    L.append((f'L1in fused8 3->8x{b}', 0, 3, b, (3, 3), 1, (1, 1), (1, 1), 8))
+    L.append((f'L1in fused5 3->5x{b}', 0, 3, b, (3, 3), 1, (1, 1), (1, 1), 5))
+    L.append((f'L1in fused3-1x1 3->3x{b}', 0, 3, b, (1, 1), 1, (0, 0), (1, 1), 3))
     L.append(('L6 3x3 544->544', 5, 32 * b, 32 * b, (3, 3), 1, (1, 1), (1, 1), 1))
     L.append(('L6 fused2 544->2x544', 5, 32 * b, 32 * b, (3, 3), 1, (1, 1), (1, 1), 2))
     return L
