@@ -530,6 +530,7 @@ __global__ __launch_bounds__(kBlock) void bn_tail_partial_kernel(TailArgs t, flo
   }
 }
 
+template <int KM>
 __global__ __launch_bounds__(kBlock) void bn_tail_apply_kernel(TailArgs t, long P, int Cp) {
   extern __shared__ float tsm[];          // [k][5][Cp] branch scale, shift, k1, k2, k3
   const int CG = Cp >> 3, R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG, c0 = 8 * cg;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(kBlock) void bn_tail_apply_kernel(TailArgs t, long 
              ok1 ? *reinterpret_cast<const uint4*>(t.ys + off1) : make_uint4(0, 0, 0, 0), a, sh, k1, k2, k3,
              t.orelu != 0, d1);
 #pragma unroll
-    for (int i = 0; i < kTailMax; ++i) {
+    for (int i = 0; i < KM; ++i) {
       if (i >= t.k) break;
       const uint4 y0 = *reinterpret_cast<const uint4*>(t.y[i] + off0);
       const uint4 y1 = ok1 ? *reinterpret_cast<const uint4*>(t.y[i] + off1) : make_uint4(0, 0, 0, 0);
@@ -707,7 +708,10 @@ void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, 
                    uint16_t* const* dy, long P, int Cp, hipStream_t s) {
   const TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, coef, relu, dy, Cp);
   const size_t lds = (size_t)k * 5 * Cp * sizeof(float);
-  hipLaunchKernelGGL(bn_tail_apply_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
+  if (k <= 3)
+    hipLaunchKernelGGL(bn_tail_apply_kernel<3>, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
+  else
+    hipLaunchKernelGGL(bn_tail_apply_kernel<kTailMax>, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
 }
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
