@@ -15,6 +15,7 @@ the statistics pass is skipped entirely.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -171,6 +172,11 @@ def need_stats(xs):
     """Flush the forward queue if any Deferred in ``xs`` has coefficients still parked in it."""
     if _FWD.keys and any(isinstance(x, Deferred) and x.stats.data_ptr() in _FWD.keys for x in xs):
         _FWD.flush()
+
+
+def need_stats_all():
+    """Flush every parked forward exchange (before a collective issued outside the queue)."""
+    _FWD.flush()
 
 
 def need_grads(gs):
@@ -458,13 +464,10 @@ def _finalize_many(C, jobs, group, dev):
         o += r.numel()
 
 
-def need_stats_all():
-    _FWD.flush()
-
-
-_TAIL_SPLIT = __import__('os').environ.get('MSP_TAIL_SPLIT', '1') != '0'
+# env MSP_TAIL_SPLIT=0: the partial pass as one six-branch launch (A/B)
+_TAIL_SPLIT = os.environ.get('MSP_TAIL_SPLIT', '1') != '0'
 # env MSP_TAIL_APPLY_SPLIT=1: the apply pass as 3-branch launches too (A/B)
-_TAIL_APPLY_SPLIT = __import__('os').environ.get('MSP_TAIL_APPLY_SPLIT', '0') == '1'
+_TAIL_APPLY_SPLIT = os.environ.get('MSP_TAIL_APPLY_SPLIT', '0') == '1'
 
 
 class _DuckTail(torch.autograd.Function):
