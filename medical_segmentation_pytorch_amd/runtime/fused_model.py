@@ -58,7 +58,8 @@ def _default_split(cout):
 def duck_split(cout):
     """Launches of a DUCK block's first convs (``cout`` output channels each): consecutive runs of the
     order 0..7."""
-    spec = os.environ.get('MSP_DUCK_SPLIT') or _default_split(cout)
+    spec = (os.environ.get('MSP_DUCK_SPLIT') or os.environ.get(f'MSP_DUCK_SPLIT_{cout}')   # per-width override
+            or _default_split(cout))
     sizes = [int(n) for n in spec.split('+')]
     assert sum(sizes) == 8 and min(sizes) > 0, f'bad DUCK split {spec}'
     starts = [sum(sizes[:i]) for i in range(len(sizes))]
