@@ -1,0 +1,25 @@
+"""Dev: how well-conditioned is the DuckNet fused-vs-fp32 parity check?  Logits / mean grad cosine of the fused
+engine and of bf16 autocast against the fp32 native-kernel reference at several input sizes."""
+sys.path.insert(0, '.')
+from medical_segmentation_pytorch_amd.models.ducknet import DuckNet
+from medical_segmentation_pytorch_amd.runtime.fused_model import FusedExecutor
+def cos(a, b): return F.cosine_similarity(a.flatten().float(), b.flatten().float(), dim=0).item()
+gpu = torch.device('cuda', 0)
+for size, batch in [(128, 4), (192, 4), (256, 4), (256, 8)]:
+    torch.manual_seed(0)
+    model = DuckNet(2, 3, 17).to(gpu).train()
+    ref, ref16 = copy.deepcopy(model), copy.deepcopy(model)
+    x = torch.randn(batch, 3, size, size, device=gpu)
+    tgt = torch.randint(0, 2, (batch, size, size), device=gpu)
+    out = FusedExecutor(model)(x, training=True)
+    with torch.backends.cudnn.flags(enabled=False):
+        o32 = ref(x)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        o16 = ref16(x).float()
+    F.cross_entropy(out, tgt).backward()
+    with torch.backends.cudnn.flags(enabled=False):
+        F.cross_entropy(o32, tgt).backward()
+    F.cross_entropy(o16, tgt).backward()
+    cf = [cos(p.grad, q.grad) for p, q in zip(model.parameters(), ref.parameters()) if q.grad.abs().sum() > 0]
+    cb = [cos(r.grad, q.grad) for r, q in zip(ref16.parameters(), ref.parameters()) if q.grad.abs().sum() > 0]
+    print(size, batch, 'logits', round(cos(out, o32), 4), round(cos(o16, o32), 4), 'grads', round(sum(cf)/len(cf), 4), round(sum(cb)/len(cb), 4), flush=True)
