@@ -1,5 +1,11 @@
 """Dev: how well-conditioned is the DuckNet fused-vs-fp32 parity check?  Logits / mean grad cosine of the fused
 engine and of bf16 autocast against the fp32 native-kernel reference at several input sizes."""
+import copy
+import sys
+
+import torch
+import torch.nn.functional as F
+
 sys.path.insert(0, '.')
 from medical_segmentation_pytorch_amd.models.ducknet import DuckNet
 from medical_segmentation_pytorch_amd.runtime.fused_model import FusedExecutor
