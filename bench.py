@@ -224,13 +224,13 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps({
             'metric': ('images/sec (whole node) + val Dice, DUCKNet-17 352x352 at 1/2/4/8 MI355X'
-                       if args.model == 'ducknet' and args.base_channel == 17 and not args.teacher
+                       if args.model == 'ducknet' and args.base_channel == 17 and not args.teacher and args.size == 352
                        else f'images/sec (whole node), {model_label(args)} {args.size}x{args.size}'),
             'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': round(value / baseline, 3) if baseline else None,
             'dtype': 'bf16',
-            'data': ('synthetic 352x352 polyp images/masks, random-init weights; ' +
+            'data': (f'synthetic {args.size}x{args.size} polyp images/masks, random-init weights; ' +
                      ('fresh GPU-augmented batch per step (MyConfig aug) inside the timed loop'
                       if args.data == 'augment' else 'one resident batch replayed')),
             'val_dice': None if dice is None else round(dice, 4),
