@@ -37,6 +37,8 @@ _BN_EPILOGUE = os.environ.get('MSP_BN_EPILOGUE', '1') != '0'
 _DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
 # env MSP_DUCK_TAIL=0 runs the DUCK tail's seven BNs as separate autograd nodes (A/B switch; see ops.bn.duck_tail)
 _DUCK_TAIL = os.environ.get('MSP_DUCK_TAIL', '1') != '0'
+# env MSP_DUCK_MULTI=0 launches the separated branch's 1x7 on its own (its dgrad then adds through autograd)
+_MULTI = os.environ.get('MSP_DUCK_MULTI', '1') != '0'
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 
@@ -330,9 +332,17 @@ class FusedExecutor:
             plans.append(self.plan_fused3x3(('duck', id(m), li), [allc[i] for i in i3], [allc[i] for i in i1])
                          if i3 else self.plan_fused1x1(('duck', id(m), li), [allc[i] for i in i1]))
             orders.append(i3 + i1)   # plan output groups: 3x3 convs first, then the 1x1s
-        # several launches: one autograd node whose data-gradients accumulate into one dL/dxb
-        outs = ([conv(plans[0], [xb], want_stats=training)] if len(plans) == 1
-                else conv_multi(plans, xb, want_stats=training))
+        # the separated branch's 1x7 reads xb too: it joins the same node (its data-gradient accumulates
+        # into dL/dxb as well -- no autograd add pass for xb's gradient at all)
+        sep_plan = self.plan_conv(b6[0][0])
+        multi = _MULTI and sep_plan.stride == 1 and sep_plan.bias is None
+        if multi:
+            outs = conv_multi(plans + [sep_plan], xb, want_stats=training)
+            sep_y, sep_part = outs[-1][0][0], outs[-1][1]
+            outs = outs[:-1]
+        else:
+            outs = ([conv(plans[0], [xb], want_stats=training)] if len(plans) == 1
+                    else conv_multi(plans, xb, want_stats=training))
         for plan, order, (ys_l, part_l) in zip(plans, orders, outs):
             for j, i in enumerate(order):
                 src[i] = (ys_l, part_l, plan, j)
@@ -356,7 +366,12 @@ class FusedExecutor:
             return (yield from self._g_cba(b2[1], o, training, raw=raw))
 
         def sep():       # 1x7 -> 7x1
-            o = yield from self._g_cba(b6[0], xb, training, single=True)
+            if multi:    # the 1x7 already ran in the shared launch node
+                o = yield from self._g_bn(lambda: self._bn_out(
+                    [sep_y], self.bn(b6[0][1]), _is_relu(b6[0][2]), training,
+                    (sep_part, sep_plan.rows, 0) if training else None, single=True))
+            else:
+                o = yield from self._g_cba(b6[0], xb, training, single=True)
             return (yield from self._g_cba(b6[1], o, training, raw=raw))
 
         rest4, rest5 = list(b4)[1:], list(b5)[1:]
