@@ -9,7 +9,7 @@ EMA update.  W untimed warmup steps, then K steps bracketed by barrier + synchro
 elapsed over ranks is reported.  Data: synthetic 352x352 polyp images/masks, random-init weights.
 
 Per-GPU micro-batch defaults to 384 images on the fused engine: the north star sizes micro-batches to
-fill the 288 GB of HBM3E, and 384 x 352^2 DUCKNet-17 peaks at 200 GiB (measured on one MI355X: 434 img/s
+fill the 288 GB of HBM3E, and 384 x 352^2 DUCKNet-17 peaks at ~229 GiB (measured on one MI355X: 434 img/s
 at 128 / 67 GiB, 445 at 256 / 134 GiB, 450 at 384 / 200 GiB -- the small deep layers fill the chip
 better).  The eager engine defaults to 128 (its NCHW step needs ~103 GiB there).  At the reference's
 16 the step is dominated by fixed-cost launches and, under DDP, SyncBN exchanges; ``--batch 16``
@@ -38,7 +38,7 @@ def parse_args(argv=None):
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--batch', type=int, default=None,
-                   help='per-GPU micro-batch (images); default 384 fused (200 GiB of the 288 GiB HBM3E), 128 eager')
+                   help='per-GPU micro-batch (images); default 384 fused (~229 GiB of the 288 GB HBM3E), 128 eager')
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
     p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
