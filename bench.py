@@ -243,6 +243,8 @@ def main(argv=None):
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
                        'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph,
                        'peak_mem_gib': round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
+                       if torch.cuda.is_available() else None,
+                       'peak_reserved_gib': round(torch.cuda.max_memory_reserved() / 2 ** 30, 1)
                        if torch.cuda.is_available() else None},
         }), flush=True)
     if dist is not None:
