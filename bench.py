@@ -8,10 +8,11 @@ bucketed all-reduce + SyncBN), optimizer step (Adam, MyConfig default), OneCycle
 EMA update.  W untimed warmup steps, then K steps bracketed by barrier + synchronize; the MAX
 elapsed over ranks is reported.  Data: synthetic 352x352 polyp images/masks, random-init weights.
 
-Per-GPU micro-batch defaults to 384 images on the fused engine: the north star sizes micro-batches to
-fill the 288 GB of HBM3E, and 384 x 352^2 DUCKNet-17 peaks at ~229 GiB (measured on one MI355X: 434 img/s
-at 128 / 67 GiB, 445 at 256 / 134 GiB, 450 at 384 / 200 GiB -- the small deep layers fill the chip
-better).  The eager engine defaults to 128 (its NCHW step needs ~103 GiB there).  At the reference's
+Per-GPU micro-batch defaults to 320 images on the fused engine: the north star sizes micro-batches to
+fill the 288 GB of HBM3E (measured on one MI355X: 434 img/s at 128 / 67 GiB, 445 at 256 / 134 GiB, 459.5
+at 384 / 229 GiB -- the small deep layers fill the chip better); 320 (~191 GiB allocated) keeps
+headroom for the caching allocator and the RCCL / DDP buffers of the multi-GPU runs at a cost of well
+under 1 % (``--batch 384`` for the last bit).  The eager engine defaults to 128 (its NCHW step needs ~103 GiB there).  At the reference's
 16 the step is dominated by fixed-cost launches and, under DDP, SyncBN exchanges; ``--batch 16``
 reproduces MyConfig's per-process batch.
 
@@ -38,7 +39,7 @@ def parse_args(argv=None):
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--batch', type=int, default=None,
-                   help='per-GPU micro-batch (images); default 384 fused (~229 GiB of the 288 GB HBM3E), 128 eager')
+                   help='per-GPU micro-batch (images); default 320 fused (~191 GiB of the 288 GB HBM3E; 384: 229 GiB), 128 eager')
     p.add_argument('--size', type=int, default=352)
     p.add_argument('--base-channel', type=int, default=17)
     p.add_argument('--impl', choices=['fused', 'eager'], default='fused')
@@ -61,7 +62,7 @@ def parse_args(argv=None):
     p.add_argument('--lr', type=float, default=1e-3, help='Adam lr per GPU (reference: 0.1 * base_lr * gpu_num)')
     a = p.parse_args(argv)
     if a.batch is None:
-        a.batch = 384 if a.impl == 'fused' and a.model == 'ducknet' and a.base_channel == 17 else 128
+        a.batch = 320 if a.impl == 'fused' and a.model == 'ducknet' and a.base_channel == 17 else 128
     return a
 
 
