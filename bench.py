@@ -150,6 +150,11 @@ def main(argv=None):
         import torch.distributed as dist
         torch.cuda.set_device(dev_index)
         backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
+        if args.graph_ddp:
+            # RCCL inside a captured graph: the process group's shared event cache can hand an event that a
+            # captured collective recorded to the watchdog's query (hipErrorCapturedEvent, seen as a
+            # sporadic SIGABRT); per-work events keep captured and watched events apart
+            os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
         kw = {'device_id': torch.device('cuda', dev_index)} if backend == 'nccl' else {}
         dist.init_process_group(backend, **kw)
     device = torch.device('cuda', dev_index)

@@ -86,7 +86,8 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   a.xrelu = (unsigned)xrelu;
   a.accum = accumulate ? 1 : 0;
   a.g = g;
-  conv_igemm(a, trans, cur_stream());
+  const int rc = conv_igemm(a, trans, cur_stream());
+  TORCH_CHECK(rc == 0, conv_error_string(rc));
 }
 
 // Data-gradient launch with the BN-backward epilogue (see ConvArgs::bn_y): stat_part receives the
@@ -120,7 +121,8 @@ void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<a
   a.bn_coef = f32(bn_coef);
   a.bn_relu = relu ? 1 : 0;
   a.g = g;
-  conv_igemm(a, false, cur_stream());
+  const int rc = conv_igemm(a, false, cur_stream());
+  TORCH_CHECK(rc == 0, conv_error_string(rc));
 }
 
 void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const at::Tensor& dw,
@@ -637,6 +639,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_stat_blocks", &conv_stat_blocks_t);
   m.def("conv_uses_halo", &conv_uses_halo_t);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
+  m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });
+  m.def("conv_gemm_force_cfg", [](int64_t c) { conv_gemm_force_cfg((int)c); });
+  m.def("conv_gemm_num_cfgs", []() { return conv_gemm_num_cfgs(); });
+  m.def("conv_uses_gemm", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+    return conv_gemm_ok(make_geom(dims, dy, dx), trans);
+  });
   m.def("conv_set_small_halo", [](bool on) { conv_set_small_halo(on ? 1 : 0); });
   m.def("conv_set_phase", [](bool on) { conv_set_phase(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);

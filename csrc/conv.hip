@@ -780,6 +780,13 @@ struct HaloGeom {
   float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
 };
 
+// Perf knock-outs of the halo kernel (profiling only): compiled in with -DMSP_HALO_KNOCKOUTS=1 and
+// selected by env MSP_HALO_DBG; in production builds HALO_KO is the constant false and folds away.
+#ifndef MSP_HALO_KNOCKOUTS
+#define MSP_HALO_KNOCKOUTS 0
+#endif
+#define HALO_KO(hg, bit) (MSP_HALO_KNOCKOUTS && ((hg).dbg & (bit)))
+
 constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel) units each)
 constexpr int kHaloWaves = 4;
 constexpr int kHaloMaxRows = 512;
@@ -877,7 +884,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
         const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
         const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
         dst[u] = __mul24(hp, hg.pitch) + c8 * 8;
-        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(hg.dbg & 2)) {
+        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
           const int ci = c0 + c8 * 8;
           const int pix = iy * g.IW + ix;
           if (g.Gi == 1) {
@@ -953,7 +960,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
       if (tid + u * 64 * kHaloWaves < total) {
         const int iy = iy0 + hy, ix = ix0 + hx;
         pd[u] = __mul24(hp, hg.pitch) + c8 * 8;
-        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(hg.dbg & 2)) {
+        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
           const int ci = c8 * 8;
           const int pix = iy * g.IW + ix;
           pd[u] |= (c8 + 1) << 16;
@@ -1028,7 +1035,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
     int c8 = tid % C8c, hp = tid / C8c;
     int hy = hp / hg.HWD, hx = hp - hy * hg.HWD;
     const int iy0 = ty0 + hg.ey0, ix0 = tx0 + hg.ex0;
-    for (int base = tid; base < ((hg.dbg & 8) ? 0 : total); base += 64 * kHaloWaves * kHaloLd) {
+    for (int base = tid; base < ((HALO_KO(hg, 8)) ? 0 : total); base += 64 * kHaloWaves * kHaloLd) {
       uint4 v[kHaloLd];
       int dst[kHaloLd], cc[kHaloLd];
 #pragma unroll
@@ -1039,7 +1046,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
         if (base + u * 64 * kHaloWaves < total) {
           const int iy = iy0 + hy, ix = ix0 + hx;
           dst[u] = __mul24(hp, hg.pitch) + c8 * 8;
-          if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(hg.dbg & 2)) {
+          if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
             const int ci = c8 * 8;
             const int pix = iy * g.IW + ix;
             cc[u] = c8;
@@ -1139,7 +1146,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
         uint4 B[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
-        if (!(hg.dbg & 4)) {
+        if (!(HALO_KO(hg, 4))) {
 #pragma unroll
           for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1153,7 +1160,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
         }
       }
     }
-    if (hg.dbg & 16) {   // knock-out: no epilogue (keep the accumulators alive)
+    if (HALO_KO(hg, 16)) {   // knock-out: no epilogue (keep the accumulators alive)
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -1241,7 +1248,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
             v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
             v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
-          if (!(hg.dbg & 1))
+          if (!(HALO_KO(hg, 1)))
             *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1269,7 +1276,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
             o[2] += __uint_as_float(ov.y << 16); o[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
           const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
-          if (!(hg.dbg & 1)) *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
+          if (!(HALO_KO(hg, 1))) *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
           const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
           const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
           cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
@@ -1526,6 +1533,7 @@ void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
 void conv_set_small_halo(int on) { g_small_tile = on ? 1 : 0; }
 bool conv_uses_halo(const ConvGeom& g, bool trans) {
   HaloGeom hg;
+  if (conv_gemm_ok(g, trans)) return false;   // wide inputs: the LDS-tiled GEMM kernel (conv_gemm.hip)
   return halo_enabled() && conv_halo_ok(g, trans, hg);
 }
 
@@ -1536,6 +1544,7 @@ static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
 
 long conv_stat_blocks(const ConvGeom& g) {
   HaloGeom hg;
+  if (conv_gemm_ok(g, false)) return conv_gemm_stat_blocks(g);
   if (halo_enabled() && conv_halo_ok(g, false, hg)) return halo_blocks(g, hg);
   const int mi = conv_pick_mi(g.Go * g.Cgo);
   const int nj = conv_pick_nj(g, mi);
@@ -1583,12 +1592,13 @@ static void conv_igemm_phased(const ConvArgs& a, int mi, hipStream_t s) {
     }
 }
 
-void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
+int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   const int mi = conv_pick_mi(a.g.Go * a.g.Cgo);
   if (trans && a.g.stride > 1 && a.stat_part == nullptr && phase_enabled()) {
     conv_igemm_phased(a, mi, s);
-    return;
+    return 0;
   }
+  if (conv_gemm_ok(a.g, trans)) return conv_gemm(a, s);
   HaloGeom hg;
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
     const unsigned blocks = (unsigned)halo_blocks(a.g, hg);
@@ -1599,7 +1609,7 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     static int dbg = -1;
     if (dbg < 0) { const char* e = getenv("MSP_HALO_DBG"); dbg = e != nullptr ? atoi(e) : 0; }
     hg.dbg = dbg;
-    if (hg.xtab && a.bn_y != nullptr) abort();   // BN prologue (forward) and BN epilogue (dgrad) never meet
+    if (hg.xtab && a.bn_y != nullptr) return 3;   // BN prologue (forward) and BN epilogue (dgrad) never meet
     const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) + (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0) +
                        (hg.pipe ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
     // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers.
@@ -1618,24 +1628,24 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
 #define HS_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe && hg.nj == 2) {                                                  \
       HC_LAUNCH_((conv_halo_kernel<MI_, 2, false, BNE_>))                                                    \
-      return;                                                                                                \
+      return 0;                                                                                              \
     }
 #define HC_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe) {                                                                \
       if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))                  \
       else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>))                             \
-      return;                                                                                                \
+      return 0;                                                                                              \
     }
 #define HP_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && pipe) {                                                                 \
       HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_, true>))                                              \
-      return;                                                                                                \
+      return 0;                                                                                              \
     }
     const bool bne = a.bn_y != nullptr;
     HS_(3, false) HS_(4, false) HS_(3, true) HS_(4, true)
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
     HP_(2, false) HP_(3, false) HP_(2, true) HP_(3, true)
-    abort();   // no instantiation for this row-group size
+    return 4;   // no instantiation for this row-group size
 #undef HP_
 #undef HS_
 #undef HC_
@@ -1646,6 +1656,18 @@ void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   if (trans) dispatch_igemm<true>(a, mi, nj, wpx, s);
   else if (a.bn_y != nullptr) dispatch_igemm<false, true>(a, mi, nj, wpx, s);
   else dispatch_igemm<false>(a, mi, nj, wpx, s);
+  return 0;
+}
+
+const char* conv_error_string(int rc) {
+  switch (rc) {
+    case 0: return "ok";
+    case 1: return "conv_gemm: no instantiation for the chosen tile configuration";
+    case 2: return "conv_gemm: deferred-BN input prologue on the GEMM path (materialise wide inputs first)";
+    case 3: return "halo conv: a BN prologue (forward) and a BN epilogue (data-gradient) in one launch";
+    case 4: return "halo conv: no instantiation for this row-group size";
+  }
+  return "conv: unknown error";
 }
 
 static size_t wgrad_halo_lds(const DwTile& tl, int ncb) {
@@ -1872,7 +1894,7 @@ int conv_plan_selfcheck(int verbose) {
                 if (cdiv(rows, 16 * hg.mi) * 16 * hg.mi > conv_rows_alloc(rows)) fail("weight rows under-allocated", g);
                 const long blocks = halo_blocks(g, hg);
                 if (blocks < 1 || blocks > (1L << 31) - 1) fail("halo grid size", g);
-                if (blocks != conv_stat_blocks(g)) fail("stat partial rows != launch grid", g);
+                if (!conv_gemm_ok(g, false) && blocks != conv_stat_blocks(g)) fail("stat partial rows != launch grid", g);
               }
               if (cdiv(rows, 16 * conv_pick_mi(rows)) * 16 * conv_pick_mi(rows) > conv_rows_alloc(rows))
                 fail("igemm weight rows under-allocated", g);

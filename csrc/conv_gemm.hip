@@ -1,0 +1,489 @@
+// LDS-tiled implicit-GEMM convolution for CDNA4 (gfx950): the wide-channel forward and stride-1
+// data-gradient path (input width >= 64 channels), on v_mfma_f32_32x32x16_bf16.
+//
+// Replaces the register-direct gather kernel (conv.hip conv_igemm_kernel) for the MFMA-friendly layers of
+// the reference's convolutions (3x3 d1/d2/d3, 1x7/7x1, 1x1, 3x3 s2, 2x2 s2 at 68..544
+// channels; reference models/ducknet.py:95-96,144-149,160-178, models/modules.py:73-85).
+//
+// GEMM view:  D[co][m] = sum_k  W[co][k] * X[k][m]      m = output pixel, k = (tap t, input channel c)
+//   block tile  TCO co-rows x TPX pixels, K staged 64 at a time (one 128-B row per co / pixel);
+//   WM x WN waves, each owns FM x FN 32x32 accumulator tiles.
+// Staging: both operands go global -> LDS with global_load_lds_dwordx4 (LDS-DMA; no VGPR round trip).
+// One wave-instruction fills 8 rows x 128 B; the per-lane SOURCE address is free, so
+//   * the im2col gather of X is just the lane's source address (tap shift + bounds check; the zero
+//     padding and the K / M tails read a 64-B zero page),
+//   * the LDS image is XOR-swizzled on the source side (16-B slot ^= (row >> 1) & 7): the 16 rows of a
+//     ds_read_b128 lane group then sit on 16 distinct bank slots -> conflict-free fragment reads.
+// Pipeline: 2 LDS stages; the DMA of stage k+1 is issued before the MFMAs of stage k, one
+// vmcnt(0) + barrier per stage.
+// Epilogue: bias / accumulate / bf16 round, 8-B NHWC stores into the row's output group, and the
+// per-channel BatchNorm partials (sum, sum^2 of the stored values -- or, for the data-gradient of a
+// BN output, the BN-backward partials) reduced across lanes and waves in LDS, one row per pixel tile.
+#include <algorithm>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+DEVI f32x16_t mfma32(const uint4& a, const uint4& b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+// 64 zero bytes in global memory: the DMA source of every padding / out-of-range vector
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
+
+// LDS-DMA of 16 B per lane: LDS[lds + 16*lane] = *src (lds wave-uniform, in an SGPR via M0).  Inline asm
+// on purpose: with the builtin the compiler drains every DMA in flight (vmcnt(0)) before ANY later
+// ds_read, since it cannot prove the read does not alias the DMA's destination -- that would serialise
+// the software pipeline.  Here the pipeline's own counted vmcnt waits + barriers order the DMAs
+// against the reads; nothing else in the main loop touches the vector-memory counter.
+DEVI void glds16(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+
+struct KPos { int t, gi, cl; };
+
+DEVI KPos kpos_init(int k, int Cgi, int Gi) {
+  const int Cip = Gi * Cgi;
+  KPos p;
+  p.t = k / Cip;
+  const int rem = k - p.t * Cip;
+  p.gi = rem / Cgi;
+  p.cl = rem - p.gi * Cgi;
+  return p;
+}
+
+DEVI void kpos_advance(KPos& p, int by, int Cgi, int Gi) {
+  p.cl += by;
+  while (p.cl >= Cgi) {
+    p.cl -= Cgi;
+    if (++p.gi == Gi) { p.gi = 0; ++p.t; }
+  }
+}
+
+constexpr int kBK = 64;          // k per stage
+constexpr int kRowB = kBK * 2;   // bytes per staged row
+
+struct GemmGeom {
+  long M, OHW;
+  int n_co, nk;
+};
+
+template <int WM, int WN, int FM, int FN, int NS>
+struct GemmCfg {
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int TCO = 32 * WM * FM, TPX = 32 * WN * FN;
+  static constexpr int A_BYTES = TCO * kRowB, B_BYTES = TPX * kRowB, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_INS = TCO / 8 / NW, B_INS = TPX / 8 / NW;   // DMA instructions per wave per stage
+  // (the epilogue's stats scratch reuses the stages)
+  static constexpr int LDS = NS * STAGE;
+  static_assert(TCO % (8 * NW) == 0 && TPX % (8 * NW) == 0, "tile rows must split evenly over the waves");
+  static_assert(2 * WN * TCO * 4 <= NS * STAGE, "stats scratch must fit in the staging LDS");
+  static_assert(NS >= 2 && NS <= 4 && 2 * (A_INS + B_INS) < 64, "pipeline depth / vmcnt range");
+};
+
+// Regular tap grid (every conv this path takes): tap t = (r, c), r = t / kw, c = t % kw, offset
+// (dy, dx) = (y0 + r * ys, x0 + c * xs) -- forward taps (r*dil - pad) and data-gradient taps (pad - r*dil)
+// alike.  Kept as scalars so that the DMA address generation reads NO memory: an LDS or global read
+// between two LDS-DMAs makes the compiler drain every DMA in flight (vmcnt(0)) before it.
+struct TapGrid { int kw, y0, ys, x0, xs; };
+
+template <int WM, int WN, int FM, int FN, int NS, bool BNE>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, GemmGeom gg, TapGrid tg) {
+  using C = GemmCfg<WM, WN, FM, FN, NS>;
+  const ConvGeom& g = a.g;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t sbase = (uint32_t)(uintptr_t)(lds_u8_t*)smem;   // LDS byte address of the stages
+
+  // XCD-aware bijective remap: the co tiles of one pixel tile (which share its B operand) and
+  // neighbouring pixel tiles (which share input rows through the tap halo) run on one XCD's L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int co_t = wgid % gg.n_co;
+  const long px_t = wgid / gg.n_co;
+  const int co0 = co_t * C::TCO;
+  const long px0 = px_t * C::TPX;
+  const int rows = g.Go * g.Cgo;
+  const int Cgi = g.Cgi, Gi = g.Gi;
+  const int IHW = g.IH * g.IW;
+  const uint16_t* x0p = a.x[0];
+
+  // ---- DMA roles: instruction j of this wave fills tile rows 8*(j*NW + wave) .. +7; lane -> row
+  // (lane >> 3), physical 16-B slot (lane & 7) = logical slot ^ ((row >> 1) & 7)
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page);
+  const uint16_t* a_src[C::A_INS];
+  int a_k[C::A_INS];
+#pragma unroll
+  for (int j = 0; j < C::A_INS; ++j) {
+    const int row = 8 * (j * C::NW + wave) + (lane >> 3);
+    const int ls = (lane & 7) ^ ((row >> 1) & 7);
+    const int co = co0 + row;
+    a_k[j] = co < rows ? 8 * ls : 1 << 30;   // rows past the layer read the zero page
+    a_src[j] = a.w + (long)(co < rows ? co : 0) * g.Kp + 8 * ls;
+  }
+  // B (im2col) lanes: output pixel -> (image base, oh*stride, ow*stride); k position -> tap (tr, tc),
+  // input group gi, channel cl, advanced by 64 per stage with register arithmetic only
+  int b_pn[C::B_INS], b_ph[C::B_INS], b_pw[C::B_INS], b_tr[C::B_INS], b_tc[C::B_INS], b_gi[C::B_INS], b_cl[C::B_INS];
+#pragma unroll
+  for (int j = 0; j < C::B_INS; ++j) {
+    const int row = 8 * (j * C::NW + wave) + (lane >> 3);
+    const int ls = (lane & 7) ^ ((row >> 1) & 7);
+    const long m = px0 + row;
+    if (m < gg.M) {
+      const int n = (int)(m / gg.OHW);
+      const int r = (int)(m - (long)n * gg.OHW);
+      const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
+      b_pn[j] = n * IHW;
+      b_ph[j] = oh * g.stride + tg.y0;
+      b_pw[j] = ow * g.stride + tg.x0;
+    } else {
+      b_pn[j] = -1; b_ph[j] = 0; b_pw[j] = 0;
+    }
+    const int Cip = Gi * Cgi, k = 8 * ls;
+    const int t = k / Cip, rem = k - (k / Cip) * Cip;
+    b_tr[j] = t / tg.kw;
+    b_tc[j] = t - (t / tg.kw) * tg.kw;
+    b_gi[j] = rem / Cgi;
+    b_cl[j] = rem - (rem / Cgi) * Cgi;
+  }
+  const int kh = g.T / tg.kw;
+
+  auto stage = [&](int kt, uint32_t sb) {
+    const int kb = kt * kBK;
+#pragma unroll
+    for (int j = 0; j < C::A_INS; ++j) {
+      const bool ok = kb + a_k[j] < g.Kp;
+      glds16(ok ? (const void*)(a_src[j] + kb) : (const void*)zero, sb + (8 * (j * C::NW + wave)) * kRowB);
+    }
+#pragma unroll
+    for (int j = 0; j < C::B_INS; ++j) {
+      const void* src = zero;
+      if (b_pn[j] >= 0 && b_tr[j] < kh) {
+        const int ih = b_ph[j] + b_tr[j] * tg.ys, iw = b_pw[j] + b_tc[j] * tg.xs;
+        if ((unsigned)ih < (unsigned)g.IH && (unsigned)iw < (unsigned)g.IW) {
+          const uint16_t* xb = x0p;
+          if (Gi > 1) {   // group pointer from the kernel arguments (scalars), no memory read
+#pragma unroll
+            for (int q = 1; q < kMaxGroups; ++q) xb = b_gi[j] == q ? a.x[q] : xb;
+          }
+          src = xb + ((long)(b_pn[j] + ih * g.IW + iw) * Cgi + b_cl[j]);
+        }
+      }
+      glds16(src, sb + C::A_BYTES + (8 * (j * C::NW + wave)) * kRowB);
+      // advance k by 64 (Cgi >= 64: at most one group / tap wrap)
+      b_cl[j] += kBK;
+      if (b_cl[j] >= Cgi) {
+        b_cl[j] -= Cgi;
+        if (++b_gi[j] == Gi) {
+          b_gi[j] = 0;
+          if (++b_tc[j] == tg.kw) { b_tc[j] = 0; ++b_tr[j]; }
+        }
+      }
+    }
+  };
+
+  // ---- fragment reads: lane (r = lane & 31, h = lane >> 5) takes 8 k at logical slot 2s + h of row r
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int key = (lane >> 1) & 7;   // == (row >> 1) & 7 for every fragment row (bases are multiples of 32)
+  int soff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) soff[s] = (((2 * s + lh) ^ key) << 4);
+  const int a_row0 = (wm * FM * 32 + lr) * kRowB;
+  const int b_row0 = C::A_BYTES + (wn * FN * 32 + lr) * kRowB;
+
+  f32x16_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // ---- software pipeline over NS LDS stages: the DMA of stage kt + NS - 1 is issued right after the
+  // barrier that retires stage kt, so NS - 1 stages of loads stay in flight under the MFMAs.  Each wave
+  // waits only for ITS OWN DMAs of stage kt (counted vmcnt: every wave issues exactly INS per stage),
+  // then the barrier makes every wave's landed data visible (and frees the buffer stage kt - 1 used).
+  constexpr int INS = C::A_INS + C::B_INS;
+  const int nk = gg.nk;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) stage(p, sbase + p * C::STAGE);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1 - kt, NS - 2);   // stages issued after kt and still allowed in flight
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * INS) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, sbase + ((kt + NS - 1) % NS) * C::STAGE);
+    const uint8_t* cur = smem + (kt % NS) * C::STAGE;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const uint4*>(cur + a_row0 + i * 32 * kRowB + soff[s]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(cur + b_row0 + j * 32 * kRowB + soff[s]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+    }
+  }
+  __syncthreads();   // every wave is done with the stages before the epilogue reuses them
+
+  // ---- epilogue.  32x32 D layout: lane holds column (pixel) lr, rows 8q + 4h + r in register 4q + r.
+  float* s_st = reinterpret_cast<float*>(smem);   // [WN][2][TCO] per-pixel-wave-column channel partials
+  const bool stats = a.stat_part != nullptr;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int rb = wm * FM * 32 + i * 32;   // tile-local row base of this fragment row
+    uint16_t* yb[4];
+    int cl4[4];
+    float cs[16], cq[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cb = co0 + rb + 8 * q + 4 * lh;
+      const int og = cb < rows ? cb / g.Cgo : 0;
+      cl4[q] = cb - og * g.Cgo;
+      uint16_t* yg = a.y[0];
+#pragma unroll
+      for (int t = 1; t < kMaxGroups; ++t) yg = og == t ? a.y[t] : yg;
+      yb[q] = cb < rows ? yg + cl4[q] : nullptr;
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { cs[e] = 0.f; cq[e] = 0.f; }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const long m = px0 + wn * FN * 32 + j * 32 + lr;
+      if (m >= gg.M) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (yb[q] == nullptr) continue;
+        uint16_t* yp = yb[q] + m * g.Cgo;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * q + r];
+        if (a.bias != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = cl4[q] + r < g.Cgo_l ? v[r] + a.bias[cl4[q] + r] : 0.f;
+        }
+        if (!BNE && a.accum) {   // y += conv(x): sibling launches' data-gradients into one tensor
+          const uint2 ov = *reinterpret_cast<const uint2*>(yp);
+          v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
+          v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
+        }
+        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(yp) = make_uint2(lo, hi);
+        // statistics of the STORED (bf16-rounded) values, as a BN reading this tensor sees them
+        const float w4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+        if constexpr (BNE) {   // BN-backward partials of the BN whose output this data-gradient is (Go == 1)
+          const int cb = cl4[q];
+          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + m * g.Cgo + cb);
+          const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
+          const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
+          const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
+          const float y4[4] = {__uint_as_float(yy.x << 16), __uint_as_float(yy.x & 0xffff0000u),
+                               __uint_as_float(yy.y << 16), __uint_as_float(yy.y & 0xffff0000u)};
+          const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w};
+          const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gr = (!a.bn_relu || fmaf(y4[r], s4[r], h4[r]) > 0.f) ? w4[r] : 0.f;
+            cs[4 * q + r] += gr;
+            cq[4 * q + r] = fmaf(gr, y4[r] - m4[r], cq[4 * q + r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            cs[4 * q + r] += w4[r];
+            cq[4 * q + r] = fmaf(w4[r], w4[r], cq[4 * q + r]);
+          }
+        }
+      }
+    }
+    if (stats) {
+      // sum over the 32 pixel lanes of each half: DPP row sums (16 lanes) + one swap of the row pair
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float s = row16_sum(cs[e]), q = row16_sum(cq[e]);
+        s += __shfl_xor(s, 16, 64);
+        q += __shfl_xor(q, 16, 64);
+        if (lr == 0) {
+          const int row = rb + 8 * (e >> 2) + 4 * lh + (e & 3);
+          s_st[(wn * 2 + 0) * C::TCO + row] = s;
+          s_st[(wn * 2 + 1) * C::TCO + row] = q;
+        }
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    // one partial row per 128 pixels (kGemmTPX): a 256-pixel tile writes two; rows past the layer's
+    // pixel count (an empty tail half) are not written
+    constexpr int HALVES = C::TPX / 128, WPH = WN / HALVES;   // waves per 128-pixel half
+    static_assert(C::TPX % 128 == 0 && WN % HALVES == 0, "128-pixel stat rows");
+    const long nrow = (gg.M + 127) / 128;
+    for (int e = tid; e < HALVES * C::TCO; e += C::NT) {
+      const int hb = e / C::TCO, c = e - hb * C::TCO;
+      const int co = co0 + c;
+      const long srow = px0 / 128 + hb;
+      if (co >= rows || srow >= nrow) continue;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPH; ++w) {
+        const int wv = hb * WPH + w;
+        s += s_st[(wv * 2 + 0) * C::TCO + c];
+        q += s_st[(wv * 2 + 1) * C::TCO + c];
+      }
+      a.stat_part[(srow * 2 + 0) * rows + co] = s;
+      a.stat_part[(srow * 2 + 1) * rows + co] = q;
+    }
+  }
+}
+
+// ---- configurations ------------------------------------------------------------------------------
+// (WM, WN, FM, FN): TCO = 32*WM*FM co rows x TPX = 32*WN*FN pixels per block
+struct CfgId { int wm, wn, fm, fn, ns; };
+// Two LDS stages everywhere: two blocks per CU (8 waves) measured 1.5-2x faster than one block with
+// a third stage (profiles/r03/gemm_cfg_sweep_bs128.log); the tile height is the main lever (B-operand
+// reuse), so the planner picks the tallest tile whose row padding stays small.
+constexpr CfgId kCfgs[] = {
+    {2, 2, 3, 2, 2},   // 192 x 128 (80 KB)
+    {2, 2, 2, 2, 2},   // 128 x 128 (64 KB)
+    {1, 4, 3, 1, 2},   //  96 x 128 (56 KB)
+    {1, 4, 5, 1, 2},   // 160 x 128 (72 KB)
+    {2, 2, 1, 2, 2},   //  64 x 128 (48 KB)
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+constexpr int kGemmTPX = 128;   // stat partial rows = pixel tiles of 128 (a 256-pixel tile writes two rows)
+
+int g_gemm_mode = -1;     // env MSP_CONV_GEMM: 0 off, else on (default on)
+int g_gemm_min_c = -1;    // env MSP_CONV_GEMM_MINC: minimum input channels per group (default 64)
+int g_gemm_cfg = -2;      // env MSP_CONV_GEMM_CFG: force one configuration index (A/B), -1 = planner
+
+void gemm_env() {
+  if (g_gemm_mode < 0) {
+    const char* e = getenv("MSP_CONV_GEMM");
+    g_gemm_mode = (e == nullptr || e[0] != '0') ? 1 : 0;
+  }
+  if (g_gemm_min_c < 0) {
+    const char* e = getenv("MSP_CONV_GEMM_MINC");
+    g_gemm_min_c = (e != nullptr && atoi(e) > 64) ? atoi(e) : 64;   // the DMA k walk needs >= 64
+  }
+  if (g_gemm_cfg == -2) {
+    const char* e = getenv("MSP_CONV_GEMM_CFG");
+    g_gemm_cfg = (e != nullptr && atoi(e) >= 0 && atoi(e) < kNumCfgs) ? atoi(e) : -1;
+  }
+}
+
+// co-tile choice: minimise (padded MFMA rows) + (pixel-operand re-staging per extra co tile)
+int gemm_pick_cfg(int rows) {
+  if (g_gemm_cfg >= 0) return g_gemm_cfg;
+  int best = 0;
+  double best_cost = 1e30;
+  for (int c = 0; c < kNumCfgs; ++c) {
+    const int tco = 32 * kCfgs[c].wm * kCfgs[c].fm;
+    const int tiles = cdiv(rows, tco);
+    const double cost = (double)tiles * (tco + 48.0);   // + the B-operand staging each co tile repeats
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = c; }
+  }
+  return best;
+}
+
+// the tap table as a regular grid (see TapGrid); false if it is not one
+bool tap_grid(const ConvGeom& g, TapGrid& tg) {
+  for (int kw = 1; kw <= g.T; ++kw) {
+    if (g.T % kw != 0) continue;
+    const int kh = g.T / kw;
+    tg.kw = kw; tg.y0 = g.dy[0]; tg.x0 = g.dx[0];
+    tg.ys = kh > 1 ? g.dy[kw] - g.dy[0] : 0;
+    tg.xs = kw > 1 ? g.dx[1] - g.dx[0] : 0;
+    bool ok = true;
+    for (int t = 0; t < g.T && ok; ++t)
+      ok = g.dy[t] == tg.y0 + (t / kw) * tg.ys && g.dx[t] == tg.x0 + (t % kw) * tg.xs;
+    if (ok) return true;
+  }
+  return false;
+}
+
+template <int WM, int WN, int FM, int FN, int NS, bool BNE>
+void launch_gemm(const ConvArgs& a, hipStream_t s) {
+  using C = GemmCfg<WM, WN, FM, FN, NS>;
+  const ConvGeom& g = a.g;
+  GemmGeom gg;
+  gg.OHW = (long)g.OH * g.OW;
+  gg.M = (long)g.N * gg.OHW;
+  gg.n_co = cdiv(g.Go * g.Cgo, C::TCO);
+  gg.nk = cdiv(g.Kp, kBK);
+  const long blocks = (long)cdiv(gg.M, C::TPX) * gg.n_co;
+  static bool attr = false;
+  if (!attr) {   // > 64 KB dynamic LDS: opted into once per instantiation, before any graph capture
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<WM, WN, FM, FN, NS, BNE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  TapGrid tg;
+  (void)tap_grid(g, tg);   // conv_gemm_ok checked it
+  hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BNE>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
+                     tg);
+}
+
+template <bool BNE>
+int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 0: launch_gemm<2, 2, 3, 2, 2, BNE>(a, s); return 0;
+    case 1: launch_gemm<2, 2, 2, 2, 2, BNE>(a, s); return 0;
+    case 2: launch_gemm<1, 4, 3, 1, 2, BNE>(a, s); return 0;
+    case 3: launch_gemm<1, 4, 5, 1, 2, BNE>(a, s); return 0;
+    case 4: launch_gemm<2, 2, 1, 2, 2, BNE>(a, s); return 0;
+  }
+  return 1;
+}
+
+}  // namespace
+
+// Eligibility: a forward (or stride-1 data-gradient) conv whose every input group is >= 64 channels
+// wide, no transposed indexing (phase-decomposed elsewhere) and no deferred-BN input prologue (the
+// callers materialise wide deferred inputs: one normalise pass beats a per-k-step transform).
+bool conv_gemm_ok(const ConvGeom& g, bool trans) {
+  gemm_env();
+  if (!g_gemm_mode || trans) return false;
+  if (g.Cgi < g_gemm_min_c || g.Cgi % 8 != 0 || g.T > kMaxTaps) return false;
+  TapGrid tg;
+  if (!tap_grid(g, tg)) return false;
+  const long M = (long)g.N * g.OH * g.OW;
+  return M >= 1 && (long)cdiv(M, kGemmTPX) * cdiv(g.Go * g.Cgo, 64) < (1L << 31);
+}
+
+void conv_gemm_set(int on) { gemm_env(); g_gemm_mode = on ? 1 : 0; }
+void conv_gemm_force_cfg(int cfg) { gemm_env(); g_gemm_cfg = (cfg >= 0 && cfg < kNumCfgs) ? cfg : -1; }
+int conv_gemm_num_cfgs() { return kNumCfgs; }
+
+long conv_gemm_stat_blocks(const ConvGeom& g) { return cdiv((long)g.N * g.OH * g.OW, kGemmTPX); }
+
+int conv_gemm(const ConvArgs& a, hipStream_t s) {
+  for (int i = 0; i < a.g.Gi; ++i)
+    if (a.xc[i] != nullptr) return 2;   // no prologue on this path (see conv_gemm_ok)
+  const int cfg = gemm_pick_cfg(a.g.Go * a.g.Cgo);
+  return a.bn_y != nullptr ? dispatch_gemm<true>(a, cfg, s) : dispatch_gemm<false>(a, cfg, s);
+}
+
+int conv_gemm_cfg_tco(int rows) {
+  gemm_env();
+  const int c = gemm_pick_cfg(rows);
+  return 32 * kCfgs[c].wm * kCfgs[c].fm;
+}

@@ -56,7 +56,18 @@ void conv_set_small_halo(int on);   // opt-in 128-pixel halo tiles (tests / A-B)
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
 bool conv_uses_halo(const ConvGeom& g, bool trans);
 long conv_stat_blocks(const ConvGeom& g);
-void conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
+// returns 0, or an error code (conv_error_string) -- the bindings raise it as a Python error
+int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
+const char* conv_error_string(int rc);
+
+// conv_gemm.hip: LDS-tiled implicit GEMM (32x32x16 MFMA, LDS-DMA staging) for >= 64-channel inputs
+bool conv_gemm_ok(const ConvGeom& g, bool trans);
+long conv_gemm_stat_blocks(const ConvGeom& g);
+int conv_gemm(const ConvArgs& a, hipStream_t s);
+void conv_gemm_set(int on);
+void conv_gemm_force_cfg(int cfg);   // tests / A-B: one tile configuration for every launch (-1: planner)
+int conv_gemm_num_cfgs();
+int conv_gemm_cfg_tco(int rows);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
 int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
 int conv_wgrad_replicas(const ConvGeom& g, bool trans);

@@ -169,6 +169,8 @@ class BaseTrainer:
                 self.train_itrs = ckpt.get('train_itrs', self.cur_epoch * config.iters_per_epoch)
                 if ckpt.get('scaler') is not None:
                     self.scaler.load_state_dict(ckpt['scaler'])
+                if hasattr(self.scaler, 'sync_optimizer_step'):   # fused fp16 Adam: restore its device step
+                    self.scaler.sync_optimizer_step(self.optimizer)
                 self._pending_ema = ckpt.get('ema_state_dict')
                 rng = ckpt.get('rng')
                 if rng is not None:

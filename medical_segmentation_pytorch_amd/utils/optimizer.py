@@ -170,6 +170,13 @@ class FusedGradScaler:
         self.state[0] = float(sd['scale'])
         self.state[1] = float(sd.get('_growth_tracker', 0))
 
+    def sync_optimizer_step(self, optimizer):
+        """After a resume: the fused Adam kernels take the bias-correction step from the scaler's device
+        count (state[3], applied = non-skipped updates), which the checkpoint stores as the optimizer's
+        'step' -- write it back so the next update continues the interrupted run's t, not t = 1."""
+        if self._enabled and isinstance(optimizer, FusedOptimizer):
+            self.state[3] = float(optimizer.step_count)
+
 
 def get_optimizer(config, model):
     fused = getattr(config, '_fused', False)

@@ -111,6 +111,41 @@ def test_fused_grad_scaler_matches_torch(gpu):
     assert sc1.state_dict()['_growth_tracker'] == sc2.state_dict()['_growth_tracker']
 
 
+def test_fused_fp16_adam_resume_continues_step(gpu):
+    """Resume with fp16 loss scaling: the fused Adam takes its bias-correction step from the scaler's
+    device count; after optimizer + scaler state_dict round trips (what a checkpoint resume does) the
+    next updates equal those of the uninterrupted run (not restarted at t = 1)."""
+    import torch.nn as nn
+    from medical_segmentation_pytorch_amd.utils.optimizer import FusedGradScaler, FusedOptimizer
+    torch.manual_seed(0)
+    ma = nn.Sequential(nn.Linear(32, 16), nn.Linear(16, 4)).to(gpu)
+    mb = nn.Sequential(nn.Linear(32, 16), nn.Linear(16, 4)).to(gpu)
+    mb.load_state_dict(ma.state_dict())
+    oa, sa = FusedOptimizer(ma, 'adam', lr=1e-2), FusedGradScaler(gpu, init_scale=256.0)
+    xs = [torch.randn(4, 32, device=gpu) for _ in range(10)]
+
+    def step(m, o, sc, x):
+        o.zero_grad()
+        sc.scale(m(x).pow(2).mean()).backward()
+        sc.step(o)
+        sc.update()
+
+    for x in xs[:5]:
+        step(ma, oa, sa, x)
+    # "checkpoint" after 5 steps, resume into fresh objects
+    osd, ssd = oa.state_dict(), sa.state_dict()
+    mb.load_state_dict(ma.state_dict())
+    ob, sb = FusedOptimizer(mb, 'adam', lr=1e-2), FusedGradScaler(gpu, init_scale=1.0)
+    ob.load_state_dict(osd)
+    sb.load_state_dict(ssd)
+    sb.sync_optimizer_step(ob)
+    for x in xs[5:]:
+        step(ma, oa, sa, x)
+        step(mb, ob, sb, x)
+    for p, q in zip(ma.parameters(), mb.parameters()):
+        assert torch.allclose(p, q, atol=1e-6, rtol=1e-5)
+
+
 def test_trainer_fp16_amp_graph(gpu, tmp_path):
     """amp_dtype='fp16' on the fused engine keeps the hipGraph (loss scaling on device state)."""
     from medical_segmentation_pytorch_amd.core import SegTrainer

@@ -61,6 +61,7 @@ def main():
     ap.add_argument('--miopen', action='store_true')
     ap.add_argument('--halo', type=int, default=1, help='1: halo-tiled stride-1 kernel where eligible, 0: gather only')
     ap.add_argument('--only', default='', help='substring filter on layer names')
+    ap.add_argument('--levels', default='', help='comma list of levels to run (e.g. 3,4,5,6)')
     ap.add_argument('--prologue', action='store_true',
                     help='input is a deferred BN(+ReLU) output: fwd / wgrad apply the BN prologue while staging')
     a = ap.parse_args()
@@ -72,6 +73,8 @@ def main():
     tot = {'fwd': 0.0, 'dgrad': 0.0, 'wgrad': 0.0}
     for name, lvl, ci, co, k, s, p, d, groups in layers():
         if a.only and a.only not in name:
+            continue
+        if a.levels and str(lvl + 1) not in a.levels.split(','):
             continue
         hw = a.size >> lvl
         n = a.batch
