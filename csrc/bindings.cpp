@@ -139,7 +139,8 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   const float* cf[kMaxGroups];
   fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), cf);
   TORCH_CHECK(!trans || xc.empty(), "no BN prologue on transposed weight-gradients");
-  conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream());
+  const int rc = conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream());
+  TORCH_CHECK(rc == 0, conv_error_string(rc));
 }
 
 int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
@@ -642,6 +643,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });
   m.def("conv_gemm_force_cfg", [](int64_t c) { conv_gemm_force_cfg((int)c); });
   m.def("conv_gemm_num_cfgs", []() { return conv_gemm_num_cfgs(); });
+  m.def("conv_set_wgrad_gemm", [](int64_t mode) { conv_wgrad_gemm_set((int)mode); });
+  m.def("conv_wgrad_gemm_force_cfg", [](int64_t c) { conv_wgrad_gemm_force_cfg((int)c); });
+  m.def("conv_wgrad_gemm_num_cfgs", []() { return conv_wgrad_gemm_num_cfgs(); });
+  m.def("conv_uses_wgrad_gemm", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+    return conv_wgrad_gemm_ok(make_geom(dims, dy, dx), trans);
+  });
   m.def("conv_uses_gemm", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
     return conv_gemm_ok(make_geom(dims, dy, dx), trans);
   });

@@ -324,12 +324,6 @@ DEVI uint2 tr_read(const uint16_t* p) {
   union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
 }
 
-struct WgradPtrs {
-  const uint16_t* dy[kMaxGroups];
-  const uint16_t* x[kMaxGroups];
-  const float* xc[kMaxGroups];   // deferred-BN prologue of the x groups (see ConvArgs::xc)
-  unsigned xrelu;
-};
 
 template <int CO_T, int K_T, bool TRANS>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g, int KT) {
@@ -1666,6 +1660,8 @@ const char* conv_error_string(int rc) {
     case 2: return "conv_gemm: deferred-BN input prologue on the GEMM path (materialise wide inputs first)";
     case 3: return "halo conv: a BN prologue (forward) and a BN epilogue (data-gradient) in one launch";
     case 4: return "halo conv: no instantiation for this row-group size";
+    case 5: return "wgrad: no instantiation for the chosen tile configuration";
+    case 6: return "wgrad (halo / gather): no instantiation for this plan";
   }
   return "conv: unknown error";
 }
@@ -1764,16 +1760,32 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
 }
 
 // number of dW slabs the caller allocates ([nsplit][rows][KT] fp32) and unpack_wgrad sums
-int conv_wgrad_replicas(const ConvGeom& g, bool trans) { return (int)wgrad_plan(g, trans).nsplit; }
+// Weight-gradient kernel choice: the LDS-tiled GEMM (conv_wgrad_gemm.hip) for wide inputs, strided and
+// 1x1 convs; the halo kernel keeps the narrow stride-1 multi-tap layers (17/34-channel DUCK levels), where
+// staging the input halo once per tile beats re-gathering it per tap (profiles/r03/conv_bench_v4_*.log:
+// L1 3x3 with a BN prologue 0.64 ms halo vs 1.23 ms GEMM; L5 fused-5 2.21 -> 0.69 ms on the GEMM).
+static bool wgrad_use_gemm(const ConvGeom& g, bool trans) {
+  if (!conv_wgrad_gemm_ok(g, trans)) return false;
+  if (conv_wgrad_gemm_mode() == 2) return true;
+  DwTile tl;
+  return g.Cgi >= 64 || g.stride > 1 || g.T == 1 || trans || !wgrad_halo_ok(g, tl);
+}
 
-void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-                const float* const* xc, unsigned xrelu, hipStream_t s) {
+int conv_wgrad_replicas(const ConvGeom& g, bool trans) {
+  if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm_replicas(g);
+  return (int)wgrad_plan(g, trans).nsplit;
+}
+
+int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
+               const float* const* xc, unsigned xrelu, hipStream_t s) {
   const int KT = g.T * g.Gi * g.Cgi;
   WgradPtrs P{};
   for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
   for (int i = 0; i < g.Gi; ++i) P.x[i] = x[i];
-  for (int i = 0; i < g.Gi; ++i) P.xc[i] = xc != nullptr ? xc[i] : nullptr;
+  bool pro = false;
+  for (int i = 0; i < g.Gi; ++i) { P.xc[i] = xc != nullptr ? xc[i] : nullptr; pro |= P.xc[i] != nullptr; }
   P.xrelu = xrelu;
+  if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm(P, dw, g, pro, s);
   const WgradPlan W = wgrad_plan(g, trans);
   if (W.halo) {
     const size_t lds = wgrad_halo_lds(W.tl, W.ncb);
@@ -1792,21 +1804,22 @@ void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, 
       }                                                                                                 \
       hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, W.tl, KT, \
                          W.ntiles);                                                                     \
-      return;                                                                                           \
+      return 0;                                                                                         \
     }
     HW_(1, 1) HW_(2, 1) HW_(3, 1) HW_(1, 2) HW_(2, 2) HW_(3, 2) HW_(1, 3) HW_(2, 3) HW_(3, 3)
 #undef HW_
-    return;
+    return 6;
   }
   dim3 grid(W.gx, W.gy, (unsigned)W.nsplit);
 #define WG(CO_, K_)                                                                                  \
   if (W.co_t == CO_ && W.k_t == K_) {                                                                \
     if (trans) hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, true>), grid, dim3(256), 0, s, P, dw, g, KT); \
     else hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, false>), grid, dim3(256), 0, s, P, dw, g, KT);      \
-    return;                                                                                          \
+    return 0;                                                                                        \
   }
   WG(32, 64) WG(32, 128) WG(64, 64) WG(64, 128)
 #undef WG
+  return 6;
 }
 
 void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base, int c_base,

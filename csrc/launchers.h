@@ -48,6 +48,23 @@ struct ConvArgs {
   ConvGeom g;
 };
 
+// weight-gradient operands: dY groups, x groups and the x groups' deferred-BN prologue (ConvArgs::xc)
+struct WgradPtrs {
+  const uint16_t* dy[kMaxGroups];
+  const uint16_t* x[kMaxGroups];
+  const float* xc[kMaxGroups];
+  unsigned xrelu;
+};
+
+// conv_wgrad_gemm.hip: LDS-tiled weight-gradient GEMM (LDS-DMA staging, transposed fragment reads)
+bool conv_wgrad_gemm_ok(const ConvGeom& g, bool trans);
+int conv_wgrad_gemm_replicas(const ConvGeom& g);
+int conv_wgrad_gemm(const WgradPtrs& P, float* dw, const ConvGeom& g, bool prologue, hipStream_t s);
+void conv_wgrad_gemm_set(int mode);   // 0 off, 1 auto (planner), 2 every eligible conv
+int conv_wgrad_gemm_mode();
+void conv_wgrad_gemm_force_cfg(int cfg);
+int conv_wgrad_gemm_num_cfgs();
+
 // conv.hip
 int conv_pick_mi(int rows);
 int conv_rows_alloc(int rows);
@@ -72,8 +89,8 @@ int conv_gemm_cfg_tco(int rows);
 int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
 int conv_wgrad_replicas(const ConvGeom& g, bool trans);
 // xc / xrelu: the deferred-BN prologue of the x groups (see ConvArgs; xc may be nullptr)
-void conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-                const float* const* xc, unsigned xrelu, hipStream_t s);
+int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
+               const float* const* xc, unsigned xrelu, hipStream_t s);
 // dst[row][(t_base + t)*Cpk + c_base + c] = src[row*s_row + c*s_ch + t], row < nrow, c < nch, t < T
 void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base,
                  int c_base, long s_row, long s_ch, hipStream_t s);

@@ -134,6 +134,8 @@ class BaseConfig:
         self.teacher_base_channel = None
         self.graph_warmup = 3          # eager iterations before the hipGraph capture
         self.graph_ddp = False         # also capture multi-GPU steps (RCCL inside the graph)
+        self.val_fp32 = False          # validate the EMA model in fp32 eager PyTorch exactly as the reference
+                                       # (core/seg_trainer.py:114); False: the bf16 fused executor (fast)
         self.progress_bar = True
         self.trace = False             # roctx ranges around step phases + per-phase HIP-event timing
         self.watchdog_timeout_s = 0    # >0: dump stacks + exit(75) after this long without a step

@@ -204,8 +204,9 @@ class SegTrainer(BaseTrainer):
     # ------------------------------------------------------------------------------------------------
     def _ema_forward(self, images):
         ema = self.ema_model.ema
-        if not self.fused:
-            return ema(images)
+        if not self.fused or getattr(self.config_ref, 'val_fp32', False):
+            # reference protocol: the EMA model in fp32 without autocast (core/seg_trainer.py:114)
+            return ema(images).float()
         owner, ex = self._ema_exec
         if owner is not ema:
             ex = FusedModel(ema).eval()
@@ -214,6 +215,7 @@ class SegTrainer(BaseTrainer):
 
     @torch.no_grad()
     def validate(self, config, loader, val_best=False):
+        self.config_ref = config
         pbar = _tqdm(loader, self.main_rank and config.progress_bar)
         for images, masks in pbar:
             images = images.to(self.device, dtype=torch.float32)

@@ -29,6 +29,7 @@ def ext():
     yield C
     C.conv_gemm_force_cfg(-1)
     C.conv_set_gemm(True)
+    C.conv_set_wgrad_gemm(1)
 
 
 GEMM_CASES = [
@@ -134,3 +135,61 @@ def test_gemm_accumulate_and_bn_epilogue(gpu, ext):
     tot = part.sum(0)
     assert _rel(tot[0], s_ref) < 1e-4 and _rel(tot[1], q_ref) < 1e-4
     assert _rel(from_fm_reference(out, co), yr) < 1e-2
+
+
+WGRAD_CASES = [
+    # N, H, W, Cin, Cout, (kh, kw), stride, pad, dil, groups
+    (2, 17, 19, 24, 24, (3, 3), 1, (1, 1), (1, 1), 1),     # L1-like narrow rows
+    (2, 12, 11, 40, 40, (1, 7), 1, (0, 3), (1, 1), 5),     # fused 5 groups, ragged pixel stages
+    (1, 9, 9, 72, 136, (3, 3), 1, (3, 3), (3, 3), 1),      # dilated
+    (2, 8, 10, 136, 272, (3, 3), 2, (1, 1), (1, 1), 1),    # strided (3x3 s2 downsample)
+    (3, 6, 6, 272, 96, (1, 1), 1, (0, 0), (1, 1), 2),      # 1x1, K < tile
+    (2, 10, 10, 24, 48, (2, 2), 2, (0, 0), (1, 1), 1),     # 2x2 s2 shortcut
+]
+
+
+@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize('prologue', [False, True])
+@pytest.mark.parametrize('case', WGRAD_CASES)
+def test_wgrad_gemm(gpu, ext, case, prologue, cfg):
+    """Weight gradient on the LDS-tiled GEMM kernel vs fp32 torch, every tile configuration, with and
+    without the deferred-BN(+ReLU) prologue on x (re-normalised in LDS; zero padding stays zero)."""
+    C = ext
+    n, h, w, ci, co, (kh, kw), s, pad, dil, groups = case
+    C.conv_wgrad_gemm_force_cfg(cfg)
+    C.conv_set_wgrad_gemm(2)   # the GEMM kernel for every eligible shape (the planner keeps narrow ones on halo)
+    try:
+        torch.manual_seed(7)
+        ms = [nn.Conv2d(ci, co, (kh, kw), s, pad, dil, bias=False).to(gpu) for _ in range(groups)]
+        plan = ConvPlan(kh, kw, ci, co, [Branch(m.weight, g, 0, kh * kw) for g, m in enumerate(ms)], stride=s,
+                        padding=pad, dilation=dil, Go=groups)
+        x = _bf(torch.randn(n, ci, h, w, device=gpu))
+        xf = to_fm_reference(x)
+        oh, ow = plan.out_hw(h, w)
+        dims = plan.fwd_dims(n, h, w, oh, ow)
+        dy = [t[0] for t in plan.taps_fwd]
+        dx = [t[1] for t in plan.taps_fwd]
+        assert C.conv_uses_wgrad_gemm(dims, dy, dx, False)
+        gys = [to_fm_reference(_bf(torch.randn(n, co, oh, ow, device=gpu))) for _ in range(groups)]
+        xc, xr = [], 0
+        z = x
+        if prologue:
+            st = torch.zeros(4, plan.Cgi, device=gpu)
+            st[0, :ci] = torch.rand(ci, device=gpu) + 0.5
+            st[1, :ci] = torch.randn(ci, device=gpu) * 0.3
+            xc, xr = [st], 1
+            z = _bf(torch.relu(x * st[0, :ci].view(1, -1, 1, 1) + st[1, :ci].view(1, -1, 1, 1)))
+        KT = plan.T * plan.Cip
+        nrep = C.conv_wgrad_replicas(dims, dy, dx, False)
+        dwp = torch.empty(nrep * plan.rows * KT, device=gpu)
+        C.conv_wgrad(gys, [xf], dwp, dims, dy, dx, False, xc, xr)
+        tot = dwp.view(nrep, plan.rows, KT).sum(0)          # [rows][t*Cip + c]
+        for g_, m in enumerate(ms):
+            zr = z.clone().requires_grad_(False)
+            wr = m.weight.detach().clone().requires_grad_(True)
+            yr = F.conv2d(zr, wr, None, s, pad, dil)
+            yr.backward(from_fm_reference(gys[g_], co))
+            got = tot[g_ * plan.Cgo:g_ * plan.Cgo + co].view(co, plan.T, plan.Cip)[:, :, :ci].permute(0, 2, 1)
+            assert _rel(got.reshape(co, ci, kh, kw), wr.grad) < 1e-2, g_
+    finally:
+        C.conv_wgrad_gemm_force_cfg(-1)

@@ -57,7 +57,9 @@ def test_fused_matches_eager(gpu, model_fn, size, batch):
     ref = copy.deepcopy(model)
     ref16 = copy.deepcopy(model)
     x = torch.randn(batch, 3, size, size, device=gpu)
-    tgt = torch.randint(0, 2, (batch, size, size), device=gpu)
+    # labels correlated with the input: random per-pixel labels give a heavily cancelling gradient (a sum
+    # of noise) whose direction even bf16 autocast only reproduces at cos 0.1-0.2 vs fp32 on DUCKNet
+    tgt = (F.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long()
     ex = FusedExecutor(model)
     out = ex(x, training=True)
     # the fp32 oracle runs on PyTorch's native kernels, not MIOpen: MIOpen's solver choice under a short
@@ -87,11 +89,10 @@ def test_fused_matches_eager(gpu, model_fn, size, batch):
     mf = sum(cf) / len(cf)
     mb = sum(cb) / len(cb)
     print(f'grad cos mean: fused {mf:.4f} autocast-bf16 {mb:.4f}; min fused {min(cf):.4f} bf16 {min(cb):.4f}')
-    # random-init DUCKNet in training mode is chaotic under ANY bf16 rounding: autocast-bf16 vs fp32 grad
-    # cos is 0.11-0.21 at 128-256 px (tools/dev/parity_probe.py) and the fused engine lands within +-0.045
-    # of it -- a noise-level comparison, so a wider margin there (its blocks are checked tightly below)
-    margin = 0.1 if mb < 0.5 else 0.05
-    assert mf > mb - margin
+    # every model: mean within 0.03 of autocast-bf16's own distance to fp32, and no parameter far off
+    assert mb > 0.9, f'oracle not conditioned (autocast-bf16 grad cos {mb:.3f})'
+    assert mf > mb - 0.03
+    assert min(cf) > min(0.8, min(cb) - 0.1), (min(cf), min(cb))
     for (k, a), (_, b) in zip(model.state_dict().items(), ref.state_dict().items()):
         if 'num_batches_tracked' in k:
             assert int(a) == int(b), k
