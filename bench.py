@@ -60,6 +60,9 @@ def parse_args(argv=None):
                    help='synthetic train split size (per rank; a larger --batch spans several epochs of it)')
     p.add_argument('--val-images', type=int, default=32, help='held-out synthetic val split for the Dice (0 = skip)')
     p.add_argument('--lr', type=float, default=1e-3, help='Adam lr per GPU (reference: 0.1 * base_lr * gpu_num)')
+    p.add_argument('--comm-steps', type=int, default=3,
+                   help='multi-GPU evidence pass after the timed region (0 = off): per-bucket RCCL timings, SyncBN '
+                        'exchange count/time, and the step time with every collective knocked out')
     a = p.parse_args(argv)
     if a.batch is None:
         a.batch = 320 if a.impl == 'fused' and a.model == 'ducknet' and a.base_channel == 17 else 128
@@ -115,6 +118,77 @@ def val_dice(model, args, device, seed):
     return float(dice.mean()), float(dice[1])
 
 
+def comm_evidence(step, args, dist, step_ms):
+    """Multi-GPU evidence, measured AFTER the timed region (and after the Dice): (1) ``comm_steps``
+    instrumented steps -- per gradient bucket its size, RCCL on-stream time, how long before the end of
+    backward it was issued (the compute it can hide under) and whether it only left at finish(); every
+    SyncBN exchange's RCCL time; (2) ``comm_steps`` steps with EVERY collective knocked out (local BN
+    statistics, no gradient averaging: a timing probe that leaves the ranks' weights diverged, hence last)
+    -> exposed communication = step time - that.  Reference comm pattern: utils/parallel.py:35-39."""
+    import statistics
+    from medical_segmentation_pytorch_amd.ops import bn as bnmod
+    bk = getattr(step, 'bucketer', None)
+    n = args.comm_steps
+    world = dist.get_world_size()
+    dev = torch.cuda.current_device()
+    out = {'world_size': world, 'backend': dist.get_backend(),
+           'rccl_version': '.'.join(str(v) for v in torch.cuda.nccl.version()) if torch.cuda.is_available() else None,
+           'timed_step_ms': round(step_ms, 3)}
+    if bk is not None:
+        bk.instrument = True
+    bnmod.COMM['instrument'] = True
+    bnmod.COMM['works'] = []
+    ex0 = bnmod.EXCHANGES[0]
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize(dev)
+    out['instrumented_step_ms'] = round((time.perf_counter() - t0) / n * 1e3, 3)
+    out['syncbn_exchanges_per_step'] = (bnmod.EXCHANGES[0] - ex0) / n
+    durs = []
+    for _, w in bnmod.COMM['works']:
+        try:
+            durs.append(float(w._get_duration()))
+        except Exception:
+            pass
+    out['syncbn_rccl_ms_per_step'] = round(sum(durs) / n, 3) if durs else None
+    out['syncbn_bytes_per_step'] = sum(b for b, _ in bnmod.COMM['works']) / n
+    bnmod.COMM['instrument'] = False
+    bnmod.COMM['works'] = []
+    if bk is not None:
+        recs = bk.collect()
+        bk.instrument = False
+        per = {}
+        for r in recs:
+            per.setdefault(r['bucket'], []).append(r)
+        out['buckets'] = [{'bucket': b, 'mib': rs[0]['mib'],
+                           'rccl_ms': (round(statistics.median([r['rccl_ms'] for r in rs if r['rccl_ms'] is not None]), 3)
+                                       if any(r['rccl_ms'] is not None for r in rs) else None),
+                           'issue_to_bwd_end_ms': round(statistics.median([r['issue_to_bwd_end_ms'] for r in rs]), 3),
+                           'late': any(r['late'] for r in rs)} for b, rs in sorted(per.items())]
+        out['grad_ready_order_monotone'] = bk.ready_order == sorted(bk.ready_order, reverse=True)
+    # knock-out pass
+    if bk is not None:
+        bk.enabled = False
+    bnmod.COMM['enabled'] = False
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize(dev)
+    t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], device=torch.device('cuda', dev), dtype=torch.float64)
+    bnmod.COMM['enabled'] = True
+    if bk is not None:
+        bk.enabled = True
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out['step_ms_comm_off'] = round(t.item(), 3)
+    out['exposed_comm_ms'] = round(step_ms - t.item(), 3)
+    return out
+
+
 def model_label(args):
     if args.model == 'ducknet':
         name = f'DUCKNet-{args.base_channel}'
@@ -150,6 +224,8 @@ def main(argv=None):
         import torch.distributed as dist
         torch.cuda.set_device(dev_index)
         backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
+        # per-collective on-stream durations for the evidence pass (Work._get_duration)
+        os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
         if args.graph_ddp:
             # RCCL inside a captured graph: the process group's shared event cache can hand an event that a
             # captured collective recorded to the watchdog's query (hipErrorCapturedEvent, seen as a
@@ -157,6 +233,7 @@ def main(argv=None):
             os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
         kw = {'device_id': torch.device('cuda', dev_index)} if backend == 'nccl' else {}
         dist.init_process_group(backend, **kw)
+        world, rank = dist.get_world_size(), dist.get_rank()   # the process group's own view (n_gpus)
     device = torch.device('cuda', dev_index)
 
     impl = args.impl
@@ -211,6 +288,9 @@ def main(argv=None):
     # of BASELINE.md's protocol: the same step in eager PyTorch-ROCm on one MI355X at its best measured
     # config (profiles/eager_reference_speed.json), times the GPU count (weak scaling; generous to the
     # eager side, whose DDP+SyncBN would scale sub-linearly).
+    comm = None
+    if dist is not None and args.comm_steps > 0 and impl == 'fused' and not use_graph:
+        comm = comm_evidence(step, args, dist, ms)
     baseline = None
     here = os.path.dirname(os.path.abspath(__file__))
     try:
@@ -244,6 +324,7 @@ def main(argv=None):
             'val_dice_note': (f'macro Dice (reference metric) on {args.val_images} held-out synthetic images after '
                               f'this run\'s {args.warmup + args.steps} training steps (OneCycle over those steps); '
                               'converged accuracy: tools/train_synthetic.py') if dice is not None else None,
+            **({'comm': comm} if comm is not None else {}),
             'config': {'model': model_label(args), 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,

@@ -156,8 +156,7 @@ class _Pending:
         rows, jobs, group = self.rows, self.jobs, self.group
         self.rows, self.jobs, self.keys, self.group = [], [], set(), None
         buf = torch.cat([r.reshape(-1) for r in rows]) if len(rows) > 1 else rows[0].reshape(-1)
-        dist.all_reduce(buf, group=group)
-        EXCHANGES[0] += 1
+        _exchange(buf, group)
         o = 0
         for r, job in zip(rows, jobs):
             job(buf[o:o + r.numel()].view(1, -1))
@@ -166,6 +165,23 @@ class _Pending:
 
 _FWD, _BWD = _Pending(), _Pending()
 EXCHANGES = [0]   # SyncBN collectives issued by this process (tests count them)
+# Comm instrumentation (bench.py's multi-GPU evidence pass): 'enabled' False knocks the SyncBN exchanges
+# out (local statistics -- a timing probe only); 'instrument' True keeps each exchange's RCCL work so its
+# duration (TORCH_NCCL_ENABLE_TIMING=1) can be read after the step.
+COMM = {'enabled': True, 'instrument': False, 'works': []}
+
+
+def _exchange(buf, group):
+    """One SyncBN statistic all-reduce (SUM, in place)."""
+    EXCHANGES[0] += 1
+    if not COMM['enabled']:
+        return
+    if COMM['instrument']:
+        w = dist.all_reduce(buf, group=group, async_op=True)
+        w.wait()
+        COMM['works'].append((buf.numel() * buf.element_size(), w))
+    else:
+        dist.all_reduce(buf, group=group)
 
 
 def need_stats(xs):
@@ -220,8 +236,7 @@ def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev, reduce=True):
         out = torch.empty(1, 2 * Cp, dtype=torch.float64, device=dev)
         C.bn_collapse(tmp, Cp, out)
         if reduce:
-            dist.all_reduce(out, group=group)
-            EXCHANGES[0] += 1
+            _exchange(out, group)
         return out
     return tmp
 
@@ -453,8 +468,7 @@ def _finalize_many(C, jobs, group, dev):
     rows = [_channel_sums(C, part, nblk, width, col_off, Cp, group, dev, reduce=False)
             for st, part, nblk, width, col_off, Cp, count, stats in jobs]
     buf = torch.cat([r.reshape(-1) for r in rows])
-    dist.all_reduce(buf, group=group)
-    EXCHANGES[0] += 1
+    _exchange(buf, group)
     o = 0
     for (st, part, nblk, width, col_off, Cp, count, stats), r in zip(jobs, rows):
         g_ = st.weight.detach() if st.weight is not None else None
@@ -556,8 +570,7 @@ class _DuckTail(torch.autograd.Function):
                 return coefs
             rows = [_channel_sums(C, part, nblk, Cp, 0, Cp, group, dev, reduce=False) for part, nblk in rows_parts]
             buf = torch.cat([r.reshape(-1) for r in rows])
-            dist.all_reduce(buf, group=group)
-            EXCHANGES[0] += 1
+            _exchange(buf, group)
             o = 0
             for r, i, cf in zip(rows, which, coefs):
                 st_i = o_stats if i == k else stats[i]

@@ -137,44 +137,89 @@ class GradBucketer:
             for i in members:
                 self.owner[i] = b
         self.pidx = arena.param_index()
+        # evidence knobs (bench.py's multi-GPU pass): enabled=False skips the all-reduces (timing probe);
+        # instrument=True records, per bucket, an event at issue time and the RCCL work (its on-stream
+        # duration needs TORCH_NCCL_ENABLE_TIMING=1), read back by collect() after the step
+        self.enabled = True
+        self.instrument = False
+        self.records = []
+        self.ready_order = []   # parameter indices in the order their gradients landed (first step)
         self.reset()
 
     def reset(self):
         self.pending = [set(m) for _, _, m in self.buckets]
         self.works = []
         self.launched = [False] * len(self.buckets)
+        self.launch_order = []
 
     def ready(self, params):
         for p in params:
             i = self.pidx.get(id(p))
             if i is None:
                 continue
+            if len(self.ready_order) < len(self.arena.params):
+                self.ready_order.append(i)
             b = self.owner[i]
             self.pending[b].discard(i)
             if not self.pending[b] and not self.launched[b]:
                 self._launch(b)
 
-    def _launch(self, b):
+    def _launch(self, b, late=False):
         lo, hi, _ = self.buckets[b]
         self.launched[b] = True
+        self.launch_order.append((b, late))
         buf = self.arena.grad[lo:hi]
         if self.shadow is not None:
             buf = self.shadow[lo:hi]
             buf.copy_(self.arena.grad[lo:hi])
-        self.works.append((b, dist.all_reduce(buf, group=self.group, async_op=True)))
+        ev = None
+        if self.instrument:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        w = dist.all_reduce(buf, group=self.group, async_op=True) if self.enabled else None
+        self.works.append((b, w, ev))
 
     def finish(self):
         from ..ops.bn import flush_pending
         flush_pending()   # parked SyncBN backward jobs report their gamma/beta grads ready
+        end = None
+        if self.instrument:   # backward's end on the compute stream (every bucket's data is ready by now)
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
         for b in range(len(self.buckets)):
             if not self.launched[b]:
-                self._launch(b)
-        for b, w in self.works:
-            w.wait()
+                self._launch(b, late=True)
+        for b, w, ev in self.works:
+            if w is not None:
+                w.wait()
             if self.shadow is not None:
                 lo, hi, _ = self.buckets[b]
                 self.arena.grad[lo:hi].copy_(self.shadow[lo:hi])
+        if self.instrument:
+            self.records.append((list(self.works), end, list(self.launch_order)))
         self.reset()
+
+    def collect(self):
+        """Per-bucket evidence of the instrumented steps (host-syncs; call after the timed region):
+        MiB, RCCL on-stream ms, ms between the bucket's issue and backward's end (the compute it could
+        hide under), and whether it launched only at finish() (not overlapped at all)."""
+        torch.cuda.synchronize()
+        out = []
+        for works, end, order in self.records:
+            late = {b: lt for b, lt in order}
+            for b, w, ev in works:
+                lo, hi, _ = self.buckets[b]
+                dur = None
+                if w is not None:
+                    try:
+                        dur = float(w._get_duration())
+                    except Exception:
+                        dur = None
+                out.append({'bucket': b, 'mib': round((hi - lo) * 4 / 2 ** 20, 2), 'rccl_ms': dur,
+                            'issue_to_bwd_end_ms': round(ev.elapsed_time(end), 3) if ev is not None and end is not None
+                            else None, 'late': bool(late.get(b, False))})
+        self.records = []
+        return out
 
 
 class StagedScalars:

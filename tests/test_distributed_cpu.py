@@ -117,3 +117,27 @@ def test_ddp_trainer_gloo(tmp_path):
     res = sorted([q.get() for _ in range(2)])
     assert res[0][1] == res[1][1]                      # same all-reduced validation score
     assert all(abs(a - b) < 1e-5 for a, b in zip(res[0][2], res[1][2]))   # replicas stay in sync
+
+
+@pytest.mark.slow
+def test_main_spawns_dataparallel_workers(tmp_path):
+    """``python main.py`` without a launcher on an N-device box starts N workers (one per device, torchrun
+    environment) with DataParallel's global batch and lr: rehearsed with MSP_SPAWN_PROCS=2 on gloo/CPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('LOCAL_RANK', 'RANK', 'WORLD_SIZE')}
+    env.update(PYTHONPATH=root, MSP_SPAWN_PROCS='2')
+    cmd = [sys.executable, os.path.join(root, 'main.py'), '--dataset', 'synthetic', '--synthetic_num', '8', '4', '4',
+           '--synthetic_size', '64', '--crop_size', '64', '--total_epoch', '1', '--warmup_epochs', '0',
+           '--train_bs', '2', '--val_bs', '2', '--base_workers', '0', '--model', 'unet', '--base_channel', '8',
+           '--no_progress_bar', '--save_dir', str(tmp_path / 'save'), '--data_root', str(tmp_path / 'data'),
+           '--engine', 'eager']
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    cfg = json.load(open(tmp_path / 'save' / 'config.json'))
+    assert cfg['DDP'] and cfg['gpu_num'] == 2 and cfg['train_bs'] == 2   # per-process 2 -> global 4
+    assert cfg['synBN'] is False          # DataParallel: per-replica BatchNorm statistics
+    assert abs(cfg['lr'] - cfg['base_lr'] * 0.1 * 2) < 1e-12   # adam: 0.1 * base_lr * gpu_num
+    assert os.path.isfile(tmp_path / 'save' / 'last.pth')

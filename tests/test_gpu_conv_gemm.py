@@ -42,6 +42,8 @@ GEMM_CASES = [
     (2, 8, 8, 72, 144, (2, 2), 2, (0, 0), (1, 1), 1, False),       # 2x2 s2 (DUCKNet shortcut)
     (2, 5, 7, 544, 96, (1, 1), 1, (0, 0), (1, 1), 2, False),       # 1x1, wide K, two groups
     (2, 7, 5, 272, 24, (3, 3), 1, (1, 1), (1, 1), 1, True),        # bias, narrow output (one co tile)
+    (4, 16, 16, 256, 256, (3, 3), 1, (2, 2), (2, 2), 1, False),    # DeepLabV3 (output stride 8) layer3
+    (4, 16, 16, 512, 512, (3, 3), 1, (4, 4), (4, 4), 1, False),    # ... layer4: dilation 4 on a 16x16 map
 ]
 
 

@@ -129,6 +129,10 @@ def test_bench_ddp_path_two_ranks(gpu, tmp_path):
     d = json.loads(line[0])
     assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'dp2' and d['config']['global_batch'] == 4
     assert d['value'] > 0 and d['steps'] == 3 and d['warmup'] == 2 and d['config']['syncbn']
+    # the multi-GPU evidence pass: bucket timings, SyncBN exchange count, knock-out step time
+    c = d['comm']
+    assert c['world_size'] == 2 and c['buckets'] and c['syncbn_exchanges_per_step'] > 0
+    assert c['step_ms_comm_off'] > 0 and c['instrumented_step_ms'] > 0
 
 
 @pytest.mark.parametrize('graph', [False, True])
@@ -150,3 +154,7 @@ def test_bench_rccl_path_world1(gpu, tmp_path, graph):
     assert len(line) == 1, r.stdout
     d = json.loads(line[0])
     assert d['n_gpus'] == 1 and d['value'] > 0 and d['config']['hipgraph'] == graph
+    if not graph:   # RCCL on-stream durations of every gradient bucket (TORCH_NCCL_ENABLE_TIMING)
+        c = d['comm']
+        assert c['world_size'] == 1 and c['rccl_version'] and c['buckets']
+        assert all(b['rccl_ms'] is not None and b['rccl_ms'] >= 0 for b in c['buckets']), c['buckets']
