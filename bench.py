@@ -214,7 +214,6 @@ def main(argv=None):
     if world != args.gpus and rank == 0:
         print(f'[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
 
-    from medical_segmentation_pytorch_amd.runtime.bench_step import build_bench_step
     dist = None
     # test hooks: BENCH_DIST_BACKEND=gloo + BENCH_SAME_DEVICE=1 rehearse the N-rank path on one GPU
     # (RCCL refuses two ranks per device); the driver's runs use RCCL, one rank per GPU
@@ -238,12 +237,29 @@ def main(argv=None):
 
     impl = args.impl
     use_graph = not args.no_graph and (not ddp or args.graph_ddp)
-    feed = make_feed(args, device, seed=1000 + rank) if args.data == 'augment' else None
-    step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
-                            base_channel=args.base_channel, device=device,
-                            channels_last=args.channels_last, use_graph=use_graph,
-                            distributed=ddp, model_name=args.model, teacher_name=args.teacher,
-                            feed=feed, total_steps=args.warmup + args.steps, lr=args.lr * world)
+    total_steps = args.warmup + args.steps + 2 * args.comm_steps + 2
+    save_dir = None
+    if impl == 'fused':
+        # the benched step IS the trainer's: SegTrainer.train_step on its own DeviceAugLoader batches
+        import tempfile
+        from medical_segmentation_pytorch_amd.runtime.bench_step import TrainerStep, bench_config
+        save_dir = os.environ.get('BENCH_SAVE_DIR') or os.path.join(
+            tempfile.gettempdir(), f'msp_bench_{os.getuid()}_{os.environ.get("MASTER_PORT", os.getpid())}')
+        same_dev = os.environ.get('BENCH_SAME_DEVICE') == '1'
+        cfg = bench_config(args.model, args.base_channel, args.batch, args.size, args.lr, total_steps,
+                           args.train_images, args.val_images, save_dir,
+                           device_index=dev_index if (not ddp or same_dev) else None, teacher_name=args.teacher,
+                           use_graph=use_graph, dist_backend=os.environ.get('BENCH_DIST_BACKEND') if ddp else None,
+                           world=world)
+        step = TrainerStep(cfg, fixed=args.data == 'fixed')
+    else:
+        from medical_segmentation_pytorch_amd.runtime.bench_step import build_bench_step
+        feed = make_feed(args, device, seed=1000 + rank) if args.data == 'augment' else None
+        step = build_bench_step(impl=impl, batch=args.batch, size=args.size,
+                                base_channel=args.base_channel, device=device,
+                                channels_last=args.channels_last, use_graph=use_graph,
+                                distributed=ddp, model_name=args.model, teacher_name=args.teacher,
+                                feed=feed, total_steps=total_steps, lr=args.lr * world)
 
     t_w = time.perf_counter()
     if rank == 0:   # heartbeat: MIOpen's first-call kernel search (eager impl) can be silent for minutes
@@ -281,8 +297,11 @@ def main(argv=None):
     global_batch = args.batch * world
     value = global_batch * args.steps / elapsed
     dice = fg_dice = None
-    if args.val_images > 0 and rank == 0 and args.model in ('ducknet', 'unet') and hasattr(step, 'ema_model'):
-        # the EMA model (= live weights with use_ema=False, MyConfig) after this run's W+K steps
+    if args.val_images > 0 and hasattr(step, 'validate') and args.model in ('ducknet', 'unet'):
+        # the trainer's own validation (EMA model = live weights with use_ema=False, MyConfig) after this
+        # run's W+K steps; every rank takes part (the confusion matrix is all-reduced)
+        dice, fg_dice = step.validate()
+    elif args.val_images > 0 and rank == 0 and args.model in ('ducknet', 'unet') and hasattr(step, 'ema_model'):
         dice, fg_dice = val_dice(step.ema_model, args, device, seed=99)
     # The reference publishes no throughput; the baseline is the in-house "reference speed"
     # of BASELINE.md's protocol: the same step in eager PyTorch-ROCm on one MI355X at its best measured
@@ -317,16 +336,19 @@ def main(argv=None):
             'scaling': 'weak', 'vs_baseline': round(value / baseline, 3) if baseline else None,
             'dtype': 'bf16',
             'data': (f'synthetic {args.size}x{args.size} polyp images/masks, random-init weights; ' +
-                     ('fresh GPU-augmented batch per step (MyConfig aug) inside the timed loop'
+                     (('fresh batch per step from the trainer\'s DeviceAugLoader (HBM-resident split, MyConfig '
+                       'augmentation on the GPU) inside the timed loop' if impl == 'fused' else
+                       'fresh GPU-augmented batch per step (MyConfig aug) inside the timed loop')
                       if args.data == 'augment' else 'one resident batch replayed')),
             'val_dice': None if dice is None else round(dice, 4),
             'val_dice_fg': None if fg_dice is None else round(fg_dice, 4),
             'val_dice_note': (f'macro Dice (reference metric) on {args.val_images} held-out synthetic images after '
-                              f'this run\'s {args.warmup + args.steps} training steps (OneCycle over those steps); '
+                              f'this run\'s {args.warmup + args.steps} training steps, by SegTrainer.validate (EMA model); '
                               'converged accuracy: tools/train_synthetic.py') if dice is not None else None,
             **({'comm': comm} if comm is not None else {}),
             'config': {'model': model_label(args), 'global_batch': global_batch,
                        'per_gpu_batch': args.batch, 'seq_len': args.size * args.size,
+                       'step': 'SegTrainer.train_step' if impl == 'fused' else 'eager reference step',
                        'image_size': args.size, 'parallelism': f'dp{world}', 'impl': impl,
                        'optimizer': 'adam', 'loss': 'ce', 'syncbn': world > 1, 'hipgraph': use_graph,
                        'peak_mem_gib': round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
@@ -335,7 +357,11 @@ def main(argv=None):
                        if torch.cuda.is_available() else None},
         }), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+    if save_dir is not None and rank == 0 and not os.environ.get('BENCH_SAVE_DIR'):
+        import shutil
+        shutil.rmtree(save_dir, ignore_errors=True)
 
 
 if __name__ == '__main__':

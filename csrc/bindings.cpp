@@ -625,6 +625,118 @@ void confmat_update_t(const at::Tensor& logits, const at::Tensor& target, const 
                  cur_stream());
 }
 
+
+// ---- decoder-hub ops (decoder.hip)
+void resize_bilinear_t(const at::Tensor& x, const at::Tensor& y, double sh, double sw, bool align, bool accum,
+                       bool backward) {
+  CHECK_BF16(x); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3) && x.size(3) % 8 == 0,
+              "resize: NHWC bf16 maps with equal N and padded C");
+  // forward: x [N,IH,IW,C] -> y [N,OH,OW,C]; backward: x = dY [N,OH,OW,C] -> y = dX [N,IH,IW,C]
+  if (!backward)
+    resize_bilinear_fwd(bf(x), bf(y), x.size(0), x.size(1), x.size(2), y.size(1), y.size(2), x.size(3), (float)sh,
+                        (float)sw, align ? 1 : 0, accum ? 1 : 0, cur_stream());
+  else
+    resize_bilinear_bwd(bf(x), bf(y), y.size(0), y.size(1), y.size(2), x.size(1), x.size(2), x.size(3), (float)sh,
+                        (float)sw, align ? 1 : 0, cur_stream());
+}
+
+int64_t nc_sums_blocks_t(int64_t HW, int64_t Cp) { return nc_sums_blocks(HW, (int)Cp); }
+
+void nc_sums_t(const at::Tensor& x, const c10::optional<at::Tensor>& dz, const c10::optional<at::Tensor>& tab,
+               bool relu, const at::Tensor& part) {
+  CHECK_BF16(x); CHECK_F32(part);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0 && x.size(3) <= 2048, "nc_sums: NHWC bf16, C <= 2048");
+  const int N = x.size(0), Cp = x.size(3);
+  const long HW = x.size(1) * x.size(2);
+  TORCH_CHECK(part.dim() == 4 && part.size(0) == N && part.size(2) == 2 && part.size(3) == Cp, "part [N][nblk][2][Cp]");
+  const uint16_t* g = nullptr;
+  if (dz.has_value() && dz->defined()) {
+    CHECK_BF16(*dz);
+    TORCH_CHECK(dz->sizes() == x.sizes(), "dz shape");
+    g = bf(*dz);
+    TORCH_CHECK(tab.has_value() && tab->numel() >= (int64_t)N * 4 * Cp, "nc_sums backward needs the [N][4][Cp] table");
+  }
+  nc_sums(bf(x), g, f32_opt(tab), relu ? 1 : 0, N, HW, Cp, f32(part), part.size(1), cur_stream());
+}
+
+void gn_finalize_t(const at::Tensor& part, int64_t C, int64_t G, double eps, const c10::optional<at::Tensor>& gamma,
+                   const c10::optional<at::Tensor>& beta, int64_t HW, const at::Tensor& tab) {
+  CHECK_F32(part); CHECK_F32(tab);
+  const int N = part.size(0), nblk = part.size(1), Cp = part.size(3);
+  TORCH_CHECK(C % G == 0 && C <= Cp && tab.numel() == (int64_t)N * 4 * Cp, "gn_finalize shapes");
+  gn_finalize(f32(part), nblk, N, C, Cp, G, (float)eps, f32_opt(gamma), f32_opt(beta), HW, f32(tab), cur_stream());
+}
+
+void gn_bwd_finalize_t(const at::Tensor& part, int64_t C, int64_t G, const c10::optional<at::Tensor>& gamma,
+                       const at::Tensor& tab, int64_t HW, const c10::optional<at::Tensor>& dgamma,
+                       const c10::optional<at::Tensor>& dbeta, const at::Tensor& coef) {
+  CHECK_F32(part); CHECK_F32(tab); CHECK_F32(coef);
+  const int N = part.size(0), nblk = part.size(1), Cp = part.size(3);
+  TORCH_CHECK(C % G == 0 && coef.numel() == (int64_t)N * 3 * Cp, "gn_bwd_finalize shapes");
+  gn_bwd_finalize(f32(part), nblk, N, C, Cp, G, f32_opt(gamma), f32(tab), HW, f32_opt_mut(dgamma), f32_opt_mut(dbeta),
+                  f32(coef), cur_stream());
+}
+
+void affine_nc_t(const at::Tensor& x, const at::Tensor& tab, int64_t rows, const at::Tensor& z, bool relu) {
+  CHECK_BF16(x); CHECK_F32(tab); CHECK_BF16(z);
+  TORCH_CHECK(x.dim() == 4 && z.sizes() == x.sizes() && tab.numel() >= x.size(0) * rows * x.size(3), "affine_nc shapes");
+  affine_nc(bf(x), f32(tab), rows, bf(z), x.size(0), x.size(1) * x.size(2), x.size(3), relu ? 1 : 0, cur_stream());
+}
+
+void affine_nc_bwd_t(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& tab, const at::Tensor& coef,
+                     const at::Tensor& dx, bool relu) {
+  CHECK_BF16(dz); CHECK_BF16(x); CHECK_F32(tab); CHECK_F32(coef); CHECK_BF16(dx);
+  TORCH_CHECK(x.dim() == 4 && dz.sizes() == x.sizes() && dx.sizes() == x.sizes(), "affine_nc_bwd shapes");
+  TORCH_CHECK(tab.numel() >= x.size(0) * 4 * x.size(3) && coef.numel() >= x.size(0) * 3 * x.size(3), "tables");
+  affine_nc_bwd(bf(dz), bf(x), f32(tab), f32(coef), bf(dx), x.size(0), x.size(1) * x.size(2), x.size(3),
+                relu ? 1 : 0, cur_stream());
+}
+
+void adaptive_avgpool_t(const at::Tensor& x, const at::Tensor& y, bool backward) {
+  CHECK_BF16(x); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3) && x.size(3) % 8 == 0 &&
+              x.size(3) <= 2048, "adaptive_avgpool: NHWC bf16, C <= 2048");
+  if (!backward)   // x [N,H,W,C] -> y [N,OH,OW,C]
+    adaptive_avgpool_fwd(bf(x), bf(y), x.size(0), x.size(1), x.size(2), y.size(1), y.size(2), x.size(3), cur_stream());
+  else             // x = dY [N,OH,OW,C] -> y = dX [N,H,W,C]
+    adaptive_avgpool_bwd(bf(x), bf(y), y.size(0), y.size(1), y.size(2), x.size(1), x.size(2), x.size(3), cur_stream());
+}
+
+void dwconv_fwd_t(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, const at::Tensor& y,
+                  std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  CHECK_BF16(x); CHECK_F32(w); CHECK_BF16(y);
+  const int T = dy.size();
+  TORCH_CHECK(T >= 1 && T <= kMaxTaps && (int)dx.size() == T, "dwconv taps");
+  TORCH_CHECK(x.dim() == 4 && y.sizes() == x.sizes() && x.size(3) % 8 == 0 && w.numel() == (int64_t)T * x.size(3),
+              "dwconv: stride-1 NHWC bf16, w [T][Cp]");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  dwconv_fwd(bf(x), f32(w), f32_opt(bias), bf(y), x.size(0), x.size(1), x.size(2), x.size(3), T, ty, tx, cur_stream());
+}
+
+int64_t dwconv_wgrad_blocks_t(int64_t P, int64_t Cp) { return dwconv_wgrad_blocks(P, (int)Cp); }
+
+void dwconv_wgrad_t(const at::Tensor& x, const at::Tensor& dyv, const at::Tensor& part, std::vector<int64_t> dy,
+                    std::vector<int64_t> dx) {
+  CHECK_BF16(x); CHECK_BF16(dyv); CHECK_F32(part);
+  const int T = dy.size();
+  TORCH_CHECK(T >= 1 && T <= 9 && (int)dx.size() == T, "dwconv_wgrad: up to 9 taps");
+  TORCH_CHECK(dyv.sizes() == x.sizes() && part.dim() == 3 && part.size(1) == T + 1 && part.size(2) == x.size(3),
+              "dwconv_wgrad: part [nblk][T+1][Cp]");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = dwconv_wgrad(bf(x), bf(dyv), f32(part), part.size(0), x.size(0), x.size(1), x.size(2), x.size(3), T,
+                              ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "dwconv_wgrad: no instantiation");
+}
+
+void colsum_t(const at::Tensor& part, const at::Tensor& out, bool accum) {
+  CHECK_F32(part); CHECK_F32(out);
+  const int64_t ncol = out.numel();
+  TORCH_CHECK(part.numel() % ncol == 0, "colsum: part [nrow][ncol]");
+  colsum(f32(part), part.numel() / ncol, ncol, f32(out), accum ? 1 : 0, cur_stream());
+}
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -717,4 +829,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("amp_update", &amp_update_t);
   m.def("ema_update", &ema_update_t);
   m.def("confmat_update", &confmat_update_t);
+  m.def("resize_bilinear", &resize_bilinear_t, py::arg("x"), py::arg("y"), py::arg("sh"), py::arg("sw"),
+        py::arg("align"), py::arg("accum") = false, py::arg("backward") = false);
+  m.def("nc_sums_blocks", &nc_sums_blocks_t);
+  m.def("nc_sums", &nc_sums_t, py::arg("x"), py::arg("dz"), py::arg("tab"), py::arg("relu"), py::arg("part"));
+  m.def("gn_finalize", &gn_finalize_t);
+  m.def("gn_bwd_finalize", &gn_bwd_finalize_t);
+  m.def("affine_nc", &affine_nc_t);
+  m.def("affine_nc_bwd", &affine_nc_bwd_t);
+  m.def("adaptive_avgpool", &adaptive_avgpool_t, py::arg("x"), py::arg("y"), py::arg("backward") = false);
+  m.def("dwconv_fwd", &dwconv_fwd_t);
+  m.def("dwconv_wgrad_blocks", &dwconv_wgrad_blocks_t);
+  m.def("dwconv_wgrad", &dwconv_wgrad_t);
+  m.def("colsum", &colsum_t);
 }

@@ -214,3 +214,29 @@ void confmat_update(const float* logits, const int64_t* target, int64_t* confmat
 void bilinear_resize(const float* x, float* y, long NC, int IH, int IW, int OH, int OW, int align_corners,
                      hipStream_t s);
 void colorize(const float* logits, const uint8_t* lut, uint8_t* rgb, int N, int C, long HW, hipStream_t s);
+
+// decoder.hip: smp decoder-hub ops (bilinear resize, GroupNorm, adaptive pooling, depthwise conv)
+void resize_bilinear_fwd(const uint16_t* x, uint16_t* y, int N, int IH, int IW, int OH, int OW, int Cp, float sh,
+                         float sw, int align, int accum, hipStream_t s);
+void resize_bilinear_bwd(const uint16_t* dy, uint16_t* dx, int N, int IH, int IW, int OH, int OW, int Cp, float sh,
+                         float sw, int align, hipStream_t s);
+int nc_sums_blocks(long HW, int Cp);
+void nc_sums(const uint16_t* x, const uint16_t* dz, const float* tab, int relu, int N, long HW, int Cp, float* part,
+             int nblk, hipStream_t s);
+void gn_finalize(const float* part, int nblk, int N, int C, int Cp, int G, float eps, const float* gamma,
+                 const float* beta, long HW, float* tab, hipStream_t s);
+void gn_bwd_finalize(const float* part, int nblk, int N, int C, int Cp, int G, const float* gamma, const float* tab,
+                     long HW, float* dgamma, float* dbeta, float* coef, hipStream_t s);
+void affine_nc(const uint16_t* x, const float* tab, int rows, uint16_t* z, int N, long HW, int Cp, int relu,
+               hipStream_t s);
+void affine_nc_bwd(const uint16_t* dz, const uint16_t* x, const float* tab, const float* coef, uint16_t* dx, int N,
+                   long HW, int Cp, int relu, hipStream_t s);
+void adaptive_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int H, int W, int OH, int OW, int Cp, hipStream_t s);
+void adaptive_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int H, int W, int OH, int OW, int Cp,
+                          hipStream_t s);
+void dwconv_fwd(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W, int Cp, int T,
+                const int* dy, const int* dx, hipStream_t s);
+int dwconv_wgrad_blocks(long P, int Cp);
+int dwconv_wgrad(const uint16_t* x, const uint16_t* dyv, float* part, int nblk, int N, int H, int W, int Cp, int T,
+                 const int* dy, const int* dx, hipStream_t s);
+void colsum(const float* part, int nrow, int ncol, float* out, int accum, hipStream_t s);

@@ -141,6 +141,8 @@ class BaseConfig:
         self.watchdog_timeout_s = 0    # >0: dump stacks + exit(75) after this long without a step
         self.dist_timeout_min = 30     # process-group timeout (a dead peer errors instead of hanging)
         self.dist_group = None         # process sub-group (concurrent HPO trials); None = WORLD
+        self.device_index = None       # explicit GPU index: single-device run without DataParallel scaling
+                                       # (bench.py), or every DDP rank on that one device (gloo rehearsal)
 
     # ------------------------------------------------------------------
     def init_dependent_config(self):

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import os
 import random
+import time
 from copy import deepcopy
 
 import numpy as np
@@ -115,6 +116,7 @@ class BaseTrainer:
             rank = int(os.getenv('RANK', 0))
             self.watchdog = StepWatchdog(config.watchdog_timeout_s, config.save_dir, rank).start()
         start_epoch = self.cur_epoch
+        self._t_run = time.perf_counter()
         for cur_epoch in range(start_epoch, config.total_epoch):
             self.cur_epoch = cur_epoch
             self.train_one_epoch(config)
@@ -139,8 +141,21 @@ class BaseTrainer:
                 self.test_score = self.val_best(config, self.test_loader)
         if self.watchdog is not None:
             self.watchdog.stop()
+        if self.main_rank:
+            self.write_val_history(config, best_score)
         destroy_ddp_process(config)
         return best_score
+
+    def write_val_history(self, config, best_score):
+        """save_dir/val_history.json: every validation (epoch, iterations, wall seconds since run start,
+        score, per-class metrics) + the val_best score of the best checkpoint."""
+        import json
+        hist = getattr(self, 'val_history', [])
+        out = {'best_score': float(best_score), 'total_epoch': config.total_epoch, 'train_bs': config.train_bs,
+               'gpu_num': config.gpu_num, 'iters_per_epoch': getattr(config, 'iters_per_epoch', None),
+               'wall_s': round(time.perf_counter() - self._t_run, 2), 'history': hist}
+        with open(os.path.join(config.save_dir, 'val_history.json'), 'w') as f:
+            json.dump(out, f, indent=1)
 
     def parallel_model(self, config):
         self.model = parallel_model(config, self.model, self.local_rank, self.device, self.optimizer)

@@ -15,6 +15,7 @@ MI355X changes:
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
@@ -22,7 +23,7 @@ from PIL import Image
 
 from ..models import get_teacher_model
 from ..ops.bn import flush_pending
-from ..runtime.trainer_engine import capture_mode, no_gc
+from ..runtime.trainer_engine import StepEngine, iteration
 from ..utils import FusedModel, de_parallel, get_colormap, get_seg_metrics, sampler_set_epoch
 from .base_trainer import BaseTrainer
 from ..ops.resample import colorize, resize_bilinear
@@ -41,64 +42,6 @@ def _tqdm(it, enable):
         return it
 
 
-class GraphedStep:
-    """hipGraph capture of one fused training step (``torch.cuda.CUDAGraph`` = HIP graph on ROCm)."""
-
-    def __init__(self, trainer, config):
-        self.t, self.config = trainer, config
-        self.graph = None
-        self.images = self.masks = self.loss = self.kd = None
-        self.calls = 0
-
-    def _body(self):
-        """zero_grad -> repack -> forward -> loss (CE / device-side OHEM / BCE+Dice) [+ KD term with the
-        frozen fused teacher, reference core/seg_trainer.py:69-79] -> backward -> fused optimizer."""
-        t, config = self.t, self.config
-        t.optimizer.zero_grad()
-        ex = t.model.executor
-        ex.repack()
-        preds = t.model(self.images)
-        loss = t.loss_fn(preds, self.masks)
-        kd = None
-        if config.kd_training:
-            with torch.no_grad():
-                teacher_preds = t.teacher_model(self.images)
-            kd = kd_loss_fn(config, preds.float(), teacher_preds.detach().float())
-            loss = loss + config.kd_loss_coefficient * kd
-            kd = kd.detach()
-        t.scaler.scale(loss).backward()
-        flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
-        t.optimizer.launch(t.scaler)   # fp16 AMP: finite check + unscale / skip inside the graph
-        t.scaler.update()
-        return loss.detach(), kd
-
-    def __call__(self, images, masks):
-        t = self.t
-        self.calls += 1
-        if self.images is None:
-            self.images = torch.empty_like(images)
-            self.masks = torch.empty_like(masks)
-        if images.shape != self.images.shape or masks.shape != self.masks.shape:
-            return t.eager_step(images, masks)        # ragged batch: not capturable, run eagerly
-        self.images.copy_(images, non_blocking=True)
-        self.masks.copy_(masks, non_blocking=True)
-        ex = t.model.executor
-        if self.calls <= max(1, self.config.graph_warmup):
-            loss = t.eager_step(self.images, self.masks)
-            if ex.pack_program is None:
-                ex.build_pack_program(self.images.device)
-            return loss
-        t.optimizer.prepare()
-        if self.graph is None:
-            torch.cuda.synchronize()
-            self.graph = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
-                self.loss, self.kd = self._body()
-        self.graph.replay()
-        t._last_kd = self.kd.clone() if self.kd is not None else None   # static graph output
-        return self.loss
-
-
 class SegTrainer(BaseTrainer):
     def __init__(self, config):
         super().__init__(config)
@@ -113,9 +56,10 @@ class SegTrainer(BaseTrainer):
                         p.requires_grad_(False)
                     self.teacher_model = FusedModel(self.teacher_model).eval()
             self.metrics = [get_seg_metrics(config, m).to(self.device) for m in config.metrics]
-        self.graph_step = None
+        self.engine = None
         self._ema_exec = (None, None)
         self._loss_hist = []
+        self.val_history = []
 
     # ------------------------------------------------------------------------------------------------
     def eager_step(self, images, masks):
@@ -151,6 +95,34 @@ class SegTrainer(BaseTrainer):
         return (self.fused and config.use_graph and kd_ok and not config.use_aux
                 and (not config.DDP or config.gpu_num == 1 or config.graph_ddp))
 
+    def step_engine(self, config):
+        """The fused engine's device step (:class:`runtime.trainer_engine.StepEngine`) -- the same object
+        ``bench.py`` times; built on first use, after ``parallel_model`` wrapped the model."""
+        if self.engine is None and self.fused and isinstance(self.model, FusedModel):
+            kd_fn = (lambda s, t: kd_loss_fn(config, s, t)) if config.kd_training else None
+            self.engine = StepEngine(self.model, self.optimizer, self.loss_fn, self.scaler,
+                                     teacher=self.teacher_model if config.kd_training else None, kd_fn=kd_fn,
+                                     kd_coef=config.kd_loss_coefficient, use_graph=self._use_graph(config),
+                                     warmup=config.graph_warmup)
+        return self.engine
+
+    def train_step(self, images, masks):
+        """One training iteration (reference core/seg_trainer.py:24-95 body): the device step (fused
+        engine: :class:`StepEngine`, hipGraph-replayed; eager engine: autocast + GradScaler), then the
+        per-iteration scheduler step and EMA update.  ``train_one_epoch`` and ``bench.py`` call this."""
+        config = self.config_ref
+        self.train_itrs += 1
+        self._last_kd = None
+        engine = self.step_engine(config)
+        if engine is not None:
+            loss = iteration(engine, self.scheduler, self.ema_model, self.train_itrs, images, masks)
+            self._last_kd = engine.kd.clone() if engine.kd is not None else None
+            return loss
+        loss = self.eager_step(images, masks)
+        self.scheduler.step()
+        self.ema_model.update(self.model, self.train_itrs)
+        return loss
+
     def _flush_logs(self, config, pbar=None):
         if not self._loss_hist:
             return
@@ -174,26 +146,16 @@ class SegTrainer(BaseTrainer):
         self.config_ref = config
         self.model.train()
         sampler_set_epoch(config, self.train_loader, self.cur_epoch)
-        if self.graph_step is None and self._use_graph(config) and isinstance(self.model, FusedModel):
-            self.graph_step = GraphedStep(self, config)
         pbar = _tqdm(self.train_loader, self.main_rank and config.progress_bar)
         wd = getattr(self, 'watchdog', None)
         for cur_itrs, (images, masks) in enumerate(pbar):
             self.cur_itrs = cur_itrs
-            self.train_itrs += 1
             with trace_range('train/h2d'):
                 images = images.to(self.device, dtype=torch.float32, non_blocking=True)
                 masks = masks.to(self.device, dtype=torch.float32 if config.num_class == 1 else torch.long,
                                  non_blocking=True)
-            self._last_kd = None
             with trace_range('train/step'):
-                if self.graph_step is not None:
-                    loss = self.graph_step(images, masks)
-                else:
-                    loss = self.eager_step(images, masks)
-            with trace_range('train/sched_ema'):
-                self.scheduler.step()
-                self.ema_model.update(self.model, self.train_itrs)
+                loss = self.train_step(images, masks)
             if wd is not None:
                 wd.beat()
             self._loss_hist.append((self.train_itrs, loss.clone(), self._last_kd))
@@ -252,6 +214,13 @@ class SegTrainer(BaseTrainer):
                         for j in range(scores[i].numel()):
                             self.writer.add_scalar(f'val/IoU_cls{j:02d}', scores[i][j].item(), self.cur_epoch + 1)
         self.last_scores = {m: s.detach().cpu() for m, s in zip(config.metrics, scores)}
+        # per-validation record (save_dir/val_history.json, written by BaseTrainer.run): accuracy vs time
+        rec = {'epoch': int(self.cur_epoch), 'train_itrs': int(getattr(self, 'train_itrs', 0)),
+               'elapsed_s': round(time.perf_counter() - getattr(self, '_t_run', time.perf_counter()), 2),
+               'score': float(score), 'val_best': bool(val_best), 'fp32': bool(getattr(config, 'val_fp32', False))}
+        for m, v in self.last_scores.items():
+            rec[m] = v.tolist()
+        self.val_history.append(rec)
         for metric in self.metrics:
             metric.reset()
         return score

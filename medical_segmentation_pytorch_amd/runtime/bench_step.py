@@ -6,6 +6,7 @@ per-tensor EMA copy) -- the in-house reference speed.  ``fused``: the MI355X-nat
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -89,6 +90,126 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
     step.model_ref = model.module if distributed else model
     step.ema_model = ema
     return step
+
+
+def bench_config(model_name, base_channel, batch, size, lr, total_steps, train_images, val_images, save_dir,
+                 device_index=None, teacher_name=None, use_graph=True, dist_backend=None, world=1):
+    """The MyConfig a bench / tool run trains with: reference defaults (adam, CE, OneCycle 'cos_warmup',
+    MyConfig augmentation, use_ema False) on a synthetic polyp split of ``train_images``/``val_images``
+    images at ``size``, one OneCycle over ``total_steps`` iterations, lr = ``lr`` per GPU
+    (reference rule: 0.1 * base_lr * gpu_num)."""
+    from ..configs import MyConfig
+    cfg = MyConfig()
+    cfg.save_dir = save_dir
+    cfg.dataset = 'synthetic'
+    cfg.synthetic_num = (train_images, max(val_images, 1), 0)
+    cfg.synthetic_size = size
+    cfg.use_test_set = False
+    cfg.crop_size = size
+    if model_name in ('ducknet', 'unet'):
+        cfg.model, cfg.base_channel = model_name, base_channel
+    else:   # smp-<encoder> | smp-<decoder>-<encoder>
+        from .trainer_engine import smp_arch
+        parts = model_name.split('-')
+        cfg.model = 'smp'
+        cfg.decoder = smp_arch(parts[1]).lower() if len(parts) == 3 else 'unet'
+        cfg.encoder = parts[-1]
+        cfg.encoder_weights = None
+    cfg.train_bs = batch
+    cfg.base_lr = lr * 10.0
+    # one OneCycle over the run: iters_per_epoch as utils.scheduler.get_scheduler derives it (train_num =
+    # the split rounded down to whole batches; / world under DDP); a batch larger than the split spans
+    # epochs of it (DeviceAugLoader.stream)
+    ipe = max(-(-(train_images // batch * batch) // (batch * world)), 1)
+    cfg.total_epoch = -(-total_steps // ipe)
+    cfg.device_index = device_index
+    cfg.dist_backend = dist_backend
+    cfg.use_graph = use_graph
+    cfg.graph_warmup = 1
+    cfg.use_tb = False
+    cfg.progress_bar = False
+    cfg.save_ckpt = False
+    cfg.load_ckpt = False
+    cfg.val_bs = 16
+    if teacher_name:
+        parts = teacher_name.split('-')
+        from .trainer_engine import smp_arch
+        cfg.kd_training = True
+        cfg.teacher_model = 'smp'
+        cfg.teacher_decoder = smp_arch(parts[1]).lower() if len(parts) == 3 else 'unet'
+        cfg.teacher_encoder = parts[-1]
+        cfg.teacher_ckpt = os.path.join(save_dir, 'teacher_random_init.pth')
+    cfg.init_dependent_config()
+    return cfg
+
+
+class TrainerStep:
+    """``bench.py``'s fused step IS the trainer's: a real :class:`core.SegTrainer` built from
+    :func:`bench_config`, its model wrapped by ``parallel_model`` (FusedModel, SyncBN + RCCL buckets
+    under torch.distributed), and every call = one ``SegTrainer.train_step`` on the next batch of the
+    trainer's own ``DeviceAugLoader`` (HBM-resident split, MyConfig augmentation on the GPU), written
+    straight into the step engine's static graph inputs."""
+
+    def __init__(self, cfg, fixed=False):
+        import torch.distributed as dist
+        from ..core import SegTrainer
+        if cfg.kd_training:   # random-init teacher checkpoint (no weights can be downloaded here)
+            rank = dist.get_rank() if dist.is_initialized() else 0
+            if rank == 0 and not os.path.isfile(cfg.teacher_ckpt):
+                from ..models import decoder_hub
+                torch.manual_seed(1)
+                t = decoder_hub[cfg.teacher_decoder](encoder_name=cfg.teacher_encoder, encoder_weights=None,
+                                                     in_channels=3, classes=cfg.num_class)
+                tmp = cfg.teacher_ckpt + '.tmp'
+                torch.save({'state_dict': t.state_dict()}, tmp)
+                os.replace(tmp, cfg.teacher_ckpt)
+            if dist.is_initialized():
+                dist.barrier()
+        self.cfg = cfg
+        self.trainer = SegTrainer(cfg)
+        self.trainer.parallel_model(cfg)
+        self.trainer.config_ref = cfg
+        self.trainer.model.train()
+        self.loader = self.trainer.train_loader
+        self.order = self.loader.stream()
+        self.bucketer = getattr(self.trainer.optimizer, 'bucketer', None)
+        self.images = self.masks = None
+        self.fixed = fixed   # replay the first batch (isolates the model step from the data pipeline)
+        self._drawn = False
+
+    @property
+    def ema_model(self):
+        return self.trainer.ema_model.ema
+
+    @property
+    def engine(self):
+        return self.trainer.engine
+
+    def __call__(self):
+        eng = self.trainer.engine
+        if eng is not None and eng.images is not None:   # the loader writes into the graph inputs
+            out = (eng.images, eng.masks)
+        else:
+            if self.images is None:
+                B, S = self.cfg.train_bs, self.cfg.crop_size
+                dev = self.trainer.device
+                self.images = torch.empty(B, 3, S, S, device=dev)
+                self.masks = torch.empty(B, S, S, dtype=torch.long, device=dev)
+            out = (self.images, self.masks)
+        if self.fixed and self._drawn:
+            images, masks = out
+        else:
+            images, masks = self.loader.batch(next(self.order), out=out)
+            self._drawn = eng is not None and out[0] is eng.images
+        return self.trainer.train_step(images, masks)
+
+    def validate(self):
+        """The trainer's validation (EMA model, device confusion matrix, reference Dice/IoU) on the
+        synthetic val split -> (macro Dice, foreground Dice)."""
+        score = self.trainer.validate(self.cfg, self.trainer.val_loader)
+        iou_fg = float(self.trainer.last_scores['iou'][-1])   # per-class IoU -> foreground Dice = 2J / (1 + J)
+        self.trainer.model.train()
+        return float(score), 2 * iou_fg / (1 + iou_fg)
 
 
 def build_bench_step(impl, batch, size, base_channel, device, channels_last=False,

@@ -29,6 +29,7 @@ from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tai
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
 from ..ops.pool import add_act, maxpool, up2_cat
+from .fused_decoders import SmpDecoders, fused_decoder_kind
 
 
 # env MSP_BN_EPILOGUE=0 disables the dgrad-epilogue BN partials (A/B switch)
@@ -41,6 +42,8 @@ _DUCK_TAIL = os.environ.get('MSP_DUCK_TAIL', '1') != '0'
 _MULTI = os.environ.get('MSP_DUCK_MULTI', '1') != '0'
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
+# env MSP_FUSED_DECODERS=0 keeps every non-Unet smp decoder on the hybrid (eager decoder) path (A/B)
+_FUSED_DECODERS = os.environ.get('MSP_FUSED_DECODERS', '1') != '0'
 
 
 # How the DUCK block's 8 first convs (0-4: the 3x3 first convs of wide/mid/res1/res2/res3, 5-7: the
@@ -81,7 +84,7 @@ def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
 
 
-class FusedExecutor:
+class FusedExecutor(SmpDecoders):
     """Holds per-module plans/BN states; ``forward(model, images)`` returns NCHW fp32 logits."""
 
     def __init__(self, model: nn.Module, group=None, sinks=None, count_nbt=True, ready_hook=None):
@@ -501,9 +504,10 @@ class FusedExecutor:
         return feats
 
     def smp_hybrid(self, model, images, training):
-        """Any smp decoder (FPN, DeepLabV3/V3+, Linknet, MAnet, PAN, PSPNet, Unet++) over a ResNet
-        encoder: the encoder -- the bulk of the FLOPs -- runs on the fused kernels, the decoder and head
-        eagerly under bf16 autocast on the NCHW features (reference ``models/__init__.py:8-10,23-25``)."""
+        """smp decoders without a fused implementation (PAN, MAnet; any decoder with MSP_FUSED_DECODERS=0)
+        over a ResNet encoder: the encoder -- the bulk of the FLOPs -- runs on the fused kernels, the decoder
+        and head eagerly under bf16 autocast on the NCHW features (reference ``models/__init__.py:8-10,23-25``).
+        Unet++ / Linknet / FPN / DeepLabV3(+) / PSPNet run fully fused (``runtime.fused_decoders``)."""
         enc = model.encoder
         feats = self.resnet_encoder(enc, images, training)
         chans = list(enc.out_channels[1:])
@@ -552,6 +556,9 @@ class FusedExecutor:
         if _is_resnet_unet(model):
             return self.resnet_unet(model, images, training)
         if _is_resnet_smp(model):
+            kind = fused_decoder_kind(model)   # Unet++ / Linknet / FPN / DeepLabV3(+) / PSPNet: fully fused
+            if kind is not None and _FUSED_DECODERS:
+                return getattr(self, kind)(model, images, training)
             return self.smp_hybrid(model, images, training)
         raise NotImplementedError(f'no fused executor for {name}')
 
@@ -590,6 +597,8 @@ def _is_resnet_unet(model) -> bool:
 def eager_parts(model):
     """Attribute names of the sub-modules the fused executor runs eagerly (hybrid smp models)."""
     if type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_unet(model) or not _is_resnet_smp(model):
+        return []
+    if _FUSED_DECODERS and fused_decoder_kind(model) is not None:
         return []
     return ['decoder', 'segmentation_head']
 

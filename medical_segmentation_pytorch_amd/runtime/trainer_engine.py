@@ -1,16 +1,20 @@
-"""The fused MI355X training step used by ``bench.py`` (and, in full, by ``core.SegTrainer``).
+"""THE fused MI355X training step: one implementation, driven by ``core.SegTrainer`` (``main.py``),
+by ``bench.py`` (which builds a real ``SegTrainer``) and by the programmatic :class:`FusedStep`.
 
-One step = reference ``core/seg_trainer.py:24-95`` semantics: zero_grad, forward, CE loss,
+One step = reference ``core/seg_trainer.py:24-95`` semantics: zero_grad, forward, loss (+ KD term),
 backward with DDP-style averaged gradients (RCCL buckets overlapped with backward) and SyncBN,
-optimizer step, OneCycle lr/momentum step, EMA update -- nothing skipped.  The whole step is
-captured once into a hipGraph (``torch.cuda.CUDAGraph`` is HIP graphs on ROCm) and replayed; the
-only per-step host work is writing the OneCycle values into the hyper-parameter tensor.
+``scaler.step(optimizer)`` + ``scaler.update()``, then -- outside the device step -- the per-iteration
+``scheduler.step()`` and the EMA update.  :class:`StepEngine` owns the device part: after ``warmup``
+eager iterations (allocator / autograd warm-up, every conv plan created, then the weight pack program
+built) the whole device step is captured once into a hipGraph (``torch.cuda.CUDAGraph`` is HIP graphs
+on ROCm) and replayed; the only per-step host work left is writing the optimizer's hyper-parameters
+(lr / betas from OneCycle, bias corrections) into its staged device tensor.
 """
 from __future__ import annotations
 
 import contextlib
-import copy
 import gc
+from types import SimpleNamespace
 
 import torch
 import torch.distributed as dist
@@ -18,109 +22,176 @@ import torch.distributed as dist
 from ..ops._ext import require
 from ..ops.bn import flush_pending
 from ..ops.losses import cross_entropy, kd_kl_div
-from .engine import Arena, FlatOptimizer, GradBucketer, OneCycle, StagedScalars, stat_group
-from .fused_model import FusedExecutor
 
 
-class FusedStep:
-    def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
-                 total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
-                 syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
-                 kd_coef=1.0, feed=None):
-        require()
-        dev = images.device
-        self.model = model
-        self.images, self.masks = images, masks
-        self.ignore_index = ignore_index
-        self.world = dist.get_world_size() if distributed else 1
-        group = dist.group.WORLD if distributed else None
-        self.ema_model = copy.deepcopy(model).eval()
-        self.arena = Arena(model, dev)
-        self.bucketer = GradBucketer(self.arena, group, bucket_cap_mb) if distributed else None
-        self.ex = FusedExecutor(model, group=stat_group(group) if syncbn else None, sinks=self.arena.sinks(),
-                                count_nbt=False,
-                                ready_hook=self.bucketer.ready if self.bucketer else None)
-        kind = optimizer
-        self.opt = FlatOptimizer(self.arena, kind, lr=lr, weight_decay=weight_decay, momentum=momentum)
-        self.opt.grad_scale = 1.0 / self.world
-        self.sched = OneCycle(lr, total_steps, pct_start)
-        # EMA: flat copy of the parameter arena + running statistics (reference ModelEmaV2)
-        self.ema_arena = Arena(self.ema_model, dev, with_grad=False)
-        self.use_ema = use_ema
-        self.ema_staged = StagedScalars(1, dev)
-        self.ema_hyper = self.ema_staged.dev
-        self.total_steps = total_steps
-        self.itrs = 0
-        self.use_graph = use_graph
+class StepEngine:
+    """Device part of one fused training iteration (the trainer's and the bench's).
+
+    ``model``: a :class:`utils.parallel.FusedModel`; ``optimizer``: a :class:`utils.optimizer.FusedOptimizer`
+    (flat arena, one kernel; its bucketer -- if attached -- all-reduces the gradients during backward);
+    ``loss_fn(preds, masks)``; ``scaler``: :class:`utils.optimizer.FusedGradScaler` or None; ``teacher``: a
+    frozen eval-mode model (KD) with ``kd_fn(student, teacher)`` and ``kd_coef``.  ``static``: optional
+    (images, masks) tensors that ARE the graph inputs (the caller writes every batch into them); otherwise
+    each call copies its batch into engine-owned static buffers."""
+
+    def __init__(self, model, optimizer, loss_fn, scaler=None, teacher=None, kd_fn=None, kd_coef=1.0,
+                 use_graph=True, warmup=1, static=None):
+        self.model, self.optimizer, self.loss_fn, self.scaler = model, optimizer, loss_fn, scaler
+        self.teacher, self.kd_fn, self.kd_coef = teacher, kd_fn, kd_coef
+        self.use_graph, self.warmup = use_graph, max(1, int(warmup))
+        self.images, self.masks = static if static is not None else (None, None)
         self.graph = None
-        self.loss = None
-        # KD (reference core/seg_trainer.py:69-79): frozen eval-mode teacher on the same fused kernels
-        self.teacher = FusedExecutor(teacher) if teacher is not None else None
-        self.kd_temperature, self.kd_coef = kd_temperature, kd_coef
-        # feed(images, masks): writes the next (augmented) batch into the static input buffers on the
-        # current stream before each step -- the data pipeline runs inside the timed loop, outside the graph
-        self.feed = feed
+        self.loss = self.kd = None
+        self.calls = 0
+        self._nbt_inc = None   # 0/1 per arena BN counter: BNs the executor runs (one add per step)
 
-    def _body(self):
-        C = require()
-        self.arena.grad.zero_()
-        self.ex.repack()
-        out = self.ex(self.images, training=True)
-        loss = cross_entropy(out, self.masks, None, self.ignore_index)
-        if self.teacher is not None:
+    @property
+    def executor(self):
+        return self.model.executor
+
+    def _count_bn(self):
+        """num_batches_tracked of every executor-run BN in ONE add over the optimizer arena's counter
+        array (the executor is built with count_nbt=False; BNs run eagerly count themselves)."""
+        arena = getattr(self.optimizer, 'arena', None)
+        if arena is None or self.executor.count_nbt:
+            return
+        if self._nbt_inc is None:
+            import torch.nn as nn
+            run = {id(m) for m, _ in self.executor._bns.values()}
+            bns = [m for m in self.model.module.modules()
+                   if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.num_batches_tracked is not None]
+            inc = torch.zeros_like(arena.nbt)
+            inc[:len(bns)] = torch.tensor([1 if id(m) in run else 0 for m in bns], dtype=inc.dtype)
+            self._nbt_inc = inc
+        arena.nbt.add_(self._nbt_inc)
+
+    def body(self, images, masks):
+        """zero_grad -> repack -> forward -> loss [+ KD] -> backward -> optimizer (+ scaler) -- capturable."""
+        opt = self.optimizer
+        opt.zero_grad()
+        self.executor.repack()
+        preds = self.model(images)
+        loss = self.loss_fn(preds, masks)
+        kd = None
+        if self.teacher is not None:   # reference core/seg_trainer.py:69-79
             with torch.no_grad():
-                t_out = self.teacher(self.images, training=False)
-            loss = loss + self.kd_coef * kd_kl_div(out, t_out, self.kd_temperature)
-        loss.backward()
+                t_out = self.teacher(images)
+            kd = self.kd_fn(preds, t_out.detach())
+            loss = loss + self.kd_coef * kd
+            kd = kd.detach()
+        sc = self.scaler if self.scaler is not None and self.scaler.is_enabled() else None
+        (sc.scale(loss) if sc is not None else loss).backward()
         flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
-        if self.bucketer is not None:
-            self.bucketer.finish()
-        self.opt.step()
-        self.arena.nbt.add_(1)
-        C.ema_update(self.ema_arena.data, self.arena.data, self.ema_hyper)
-        C.ema_update(self.ema_arena.bufdata, self.arena.bufdata, self.ema_hyper)
-        return loss.detach()   # the autograd graph (and every ctx it holds) dies with this step
+        opt.launch(sc)    # bucket all-reduce wait + one optimizer kernel (fp16: finite check / skip)
+        if sc is not None:
+            sc.update()
+        if self.model.training:
+            self._count_bn()
+        return loss.detach(), kd   # the autograd graph (and every ctx it holds) dies with this step
 
-    def _prepare(self):
-        lr, mom = self.sched.values()
-        self.opt.lr = lr
-        if self.opt.kind in ('adam', 'adamw'):
-            self.opt.betas = (mom, self.opt.betas[1])
-        else:
-            self.opt.momentum = mom
-        self.opt.prepare()
-        self.itrs += 1
-        d = min(max(self.itrs / self.total_steps, 0.0), 1.0) if self.use_ema else 0.0
-        self.ema_staged.host()[0] = d
-        self.ema_staged.push()
-        self.sched.step()
-
-    def __call__(self):
-        """One training step (exactly one optimizer update per call).  Graph mode: call 1 runs eagerly
-        on a side stream (allocator / autograd warm-up, every plan created), call 2 builds the pack
-        program, captures the body and replays it; every later call is one replay."""
-        if self.feed is not None:
-            self.feed(self.images, self.masks)
-        self._prepare()
-        if self.ex.pack_program is None and self.itrs > 1:
-            self.ex.build_pack_program(self.images.device)
-        if not self.use_graph:
-            self.loss = self._body()
-            return self.loss
-        if self.itrs == 1:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                self.loss = self._body()
-            torch.cuda.current_stream().wait_stream(s)
+    def __call__(self, images=None, masks=None):
+        """One device step; returns the (device) loss.  Graph mode: calls 1..warmup run eagerly on a side
+        stream, the last of them builds the weight pack program; the next call captures the body and
+        replays it; every later call is one replay."""
+        self.calls += 1
+        if self.images is None:
+            self.images, self.masks = torch.empty_like(images), torch.empty_like(masks)
+        if images is not None and images is not self.images:
+            if images.shape != self.images.shape or masks.shape != self.masks.shape:
+                self.optimizer.prepare()     # ragged batch: not capturable, run eagerly
+                self.loss, self.kd = self.body(images, masks)
+                return self.loss
+            self.images.copy_(images, non_blocking=True)
+            self.masks.copy_(masks, non_blocking=True)
+        self.optimizer.prepare()
+        ex = self.executor
+        if not self.use_graph or self.calls <= self.warmup:
+            if self.use_graph and self.images.is_cuda:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    self.loss, self.kd = self.body(self.images, self.masks)
+                torch.cuda.current_stream().wait_stream(s)
+            else:
+                self.loss, self.kd = self.body(self.images, self.masks)
+            if ex.pack_program is None and (not self.use_graph or self.calls == self.warmup):
+                ex.build_pack_program(self.images.device)
             return self.loss
         if self.graph is None:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
             with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
-                self.loss = self._body()
+                self.loss, self.kd = self.body(self.images, self.masks)
         self.graph.replay()
         return self.loss
+
+
+def iteration(engine, scheduler, ema, itrs, images=None, masks=None):
+    """One training iteration exactly as ``SegTrainer.train_one_epoch`` runs it: device step, then the
+    per-iteration scheduler step and EMA update (reference core/seg_trainer.py:82-87)."""
+    loss = engine(images, masks)
+    scheduler.step()
+    ema.update(engine.model, itrs)
+    return loss
+
+
+class FusedStep:
+    """Programmatic training step (tests, tools) assembled from the SAME components ``SegTrainer`` uses:
+    :class:`FusedOptimizer` (+ :class:`GradBucketer` under torch.distributed), :class:`FusedModel`,
+    torch ``OneCycleLR``, :class:`ModelEmaV2` on the arena, driven by :class:`StepEngine` +
+    :func:`iteration`.  ``images`` / ``masks`` are the static graph inputs; ``feed(images, masks)``
+    (optional) writes the next batch into them before each step."""
+
+    def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
+                 total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
+                 syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
+                 kd_coef=1.0, feed=None):
+        from ..utils.model_ema import ModelEmaV2
+        from ..utils.optimizer import FusedOptimizer
+        from ..utils.parallel import FusedModel
+        from .engine import GradBucketer, stat_group
+        require()
+        dev = images.device
+        self.model = model
+        self.images, self.masks = images, masks
+        self.world = dist.get_world_size() if distributed else 1
+        group = dist.group.WORLD if distributed else None
+        self.opt = FusedOptimizer(model, optimizer, lr=lr, momentum=momentum, weight_decay=weight_decay,
+                                  device=dev)
+        self.arena = self.opt.arena
+        self.bucketer = None
+        if distributed and self.world > 1:
+            self.bucketer = GradBucketer(self.arena, group, bucket_cap_mb)
+            self.opt.attach_bucketer(self.bucketer)
+        self.fm = FusedModel(model, group=stat_group(group) if syncbn else None, sinks=self.arena.sinks(),
+                             ready_hook=self.bucketer.ready if self.bucketer else None, count_nbt=False)
+        self.sched = torch.optim.lr_scheduler.OneCycleLR(self.opt, max_lr=lr, total_steps=total_steps,
+                                                         pct_start=pct_start)
+        self.ema = ModelEmaV2(SimpleNamespace(use_ema=use_ema, total_itrs=total_steps), model, dev,
+                              src_arena=self.arena)
+        self.ema_model = self.ema.ema
+        t_fm = None
+        if teacher is not None:   # KD (reference core/seg_trainer.py:69-79): frozen eval-mode fused teacher
+            t_fm = FusedModel(teacher).eval()
+        self.engine = StepEngine(self.fm, self.opt, lambda p, m: cross_entropy(p, m, None, ignore_index),
+                                 teacher=t_fm, kd_fn=lambda s, t: kd_kl_div(s, t, kd_temperature),
+                                 kd_coef=kd_coef, use_graph=use_graph, warmup=1, static=(images, masks))
+        self.feed = feed
+        self.itrs = 0
+
+    @property
+    def graph(self):
+        return self.engine.graph
+
+    @property
+    def ex(self):
+        return self.fm.executor
+
+    def __call__(self):
+        if self.feed is not None:
+            self.feed(self.images, self.masks)
+        self.itrs += 1
+        return iteration(self.engine, self.sched, self.ema, self.itrs)
 
 
 @contextlib.contextmanager
@@ -142,7 +213,6 @@ def capture_mode():
     """hipGraph capture error mode: 'thread_local' under torch.distributed -- the process group's
     watchdog thread polls its work events while the step is being captured, which the default
     'global' mode turns into a capture error and a SIGABRT (seen intermittently with --graph-ddp)."""
-    import torch.distributed as dist
     return 'thread_local' if dist.is_available() and dist.is_initialized() else 'global'
 
 
@@ -159,13 +229,18 @@ def make_model(model_name, base_channel=17, num_class=2):
         return UNet(num_class=num_class, n_channel=3, base_channel=base_channel)
     if model_name.startswith('smp-'):
         parts = model_name.split('-')
-        if len(parts) == 3:   # smp-<decoder>-<encoder>, e.g. smp-fpn-resnet18 (fused encoder, eager decoder)
+        if len(parts) == 3:   # smp-<decoder>-<encoder>, e.g. smp-fpn-resnet18
             from ..models import smp
-            arch = {n.lower(): n for n in ('Unet', 'UnetPlusPlus', 'FPN', 'Linknet', 'MAnet', 'PAN', 'PSPNet',
-                                           'DeepLabV3', 'DeepLabV3Plus')}[parts[1]]
-            return getattr(smp, arch)(encoder_name=parts[2], encoder_weights=None, in_channels=3, classes=num_class)
+            return getattr(smp, smp_arch(parts[1]))(encoder_name=parts[2], encoder_weights=None, in_channels=3,
+                                                   classes=num_class)
         return Unet(encoder_name=model_name[4:], encoder_weights=None, in_channels=3, classes=num_class)
     raise ValueError(f'unknown model {model_name!r}')
+
+
+def smp_arch(name):
+    """smp class name of a lower-case decoder key ('fpn' -> 'FPN', 'deeplabv3plus' -> 'DeepLabV3Plus')."""
+    return {n.lower(): n for n in ('Unet', 'UnetPlusPlus', 'FPN', 'Linknet', 'MAnet', 'PAN', 'PSPNet',
+                                   'DeepLabV3', 'DeepLabV3Plus')}[name]
 
 
 def build_fused_step(batch, size, base_channel, device, use_graph=True, distributed=False, optimizer='adam',

@@ -63,6 +63,8 @@ def de_parallel(model):
 def set_device(config, rank):
     if config.DDP:
         use_gpu = torch.cuda.is_available()
+        if getattr(config, 'device_index', None) is not None:
+            rank = config.device_index   # every rank on one device (gloo rehearsal of the N-rank path)
         if use_gpu:
             torch.cuda.set_device(rank)
         if not dist.is_initialized():
@@ -75,6 +77,12 @@ def set_device(config, rank):
             dist.init_process_group(backend=backend, init_method='env://', **kw)
         device = torch.device('cuda', rank) if use_gpu else torch.device('cpu')
         config.gpu_num = group_size(config)
+    elif getattr(config, 'device_index', None) is not None:
+        # one explicit device, no DataParallel batch scaling (bench.py; tests)
+        device = torch.device('cuda', config.device_index) if torch.cuda.is_available() else torch.device('cpu')
+        if device.type == 'cuda':
+            torch.cuda.set_device(device)
+        config.gpu_num = 1
     else:
         device = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
         config.gpu_num = max(torch.cuda.device_count(), 1)
@@ -101,7 +109,7 @@ def parallel_model(config, model, rank, device, optimizer=None):
         group = get_group(config) if config.DDP else None
         arena = getattr(optimizer, 'arena', None)
         bucketer = None
-        if group is not None and dist.get_world_size(group) > 1 and arena is not None:
+        if group is not None and arena is not None:   # (world 1 too: the RCCL path stays exercised)
             from ..runtime.engine import GradBucketer
             bucketer = GradBucketer(arena, group, config.bucket_cap_mb,
                                     compress=getattr(config, 'grad_compress', None))
@@ -115,7 +123,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
                 setattr(model, name, nn.SyncBatchNorm.convert_sync_batchnorm(getattr(model, name), group))
         return FusedModel(model, group=stat_group(group) if config.synBN else None,
                           sinks=arena.sinks() if arena is not None else None,
-                          ready_hook=bucketer.ready if bucketer is not None else None)
+                          ready_hook=bucketer.ready if bucketer is not None else None,
+                          count_nbt=arena is None)   # with an arena: one counter add per step (StepEngine)
     if config.DDP:
         if config.synBN and device.type == 'cuda':
             model = nn.SyncBatchNorm.convert_sync_batchnorm(model)

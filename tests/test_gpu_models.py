@@ -36,7 +36,8 @@ def _smp(arch, encoder):
                                                  (lambda: _smp_unet('resnet50'), 64, 2),
                                                  # grouped 3x3 (MIOpen channels-last) between fused ops
                                                  (lambda: _smp_unet('resnext50_32x4d'), 64, 2),
-                                                 # fused encoder + eager decoder (hybrid)
+                                                 # fully fused decoders (runtime/fused_decoders.py)
+                                                 (lambda: _smp('UnetPlusPlus', 'resnet18'), 64, 4),
                                                  (lambda: _smp('FPN', 'resnet18'), 64, 4),
                                                  (lambda: _smp('DeepLabV3Plus', 'resnet18'), 64, 4),
                                                  # output stride 8: at 64 px the dilation-4 layer4 sees
@@ -46,7 +47,10 @@ def _smp(arch, encoder):
                                                  # branch's [2, C, 1, 1] channels-last bf16 input)
                                                  (lambda: _smp('DeepLabV3', 'resnet18'), 128, 4),
                                                  (lambda: _smp('PSPNet', 'resnet18'), 64, 4),
-                                                 (lambda: _smp('Linknet', 'resnet18'), 64, 4)])
+                                                 (lambda: _smp('Linknet', 'resnet18'), 64, 4),
+                                                 # hybrid: fused encoder + eager decoder
+                                                 # (PAN's FPA block pools the stride-32 map to 1/8: >= 128 px)
+                                                 (lambda: _smp('PAN', 'resnet18'), 128, 4)])
 def test_fused_matches_eager(gpu, model_fn, size, batch):
     """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is."""
     torch.manual_seed(0)
@@ -193,3 +197,12 @@ def test_duck_tail_fused_matches_separate_nodes(gpu, monkeypatch):
     assert min(cs) > 0.99 and sum(cs) / len(cs) > 0.999, (min(cs), sum(cs) / len(cs))
     for a, b in zip(res[0][2], res[1][2]):
         assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize('arch', ['UnetPlusPlus', 'Linknet', 'FPN', 'DeepLabV3', 'DeepLabV3Plus', 'PSPNet'])
+def test_decoders_fully_fused(arch):
+    """These smp decoders run on the HIP kernels end to end: no sub-module is left to the eager path."""
+    from medical_segmentation_pytorch_amd.runtime.fused_decoders import fused_decoder_kind
+    from medical_segmentation_pytorch_amd.runtime.fused_model import eager_parts
+    m = _smp(arch, 'resnet18')
+    assert fused_decoder_kind(m) is not None and eager_parts(m) == []

@@ -31,7 +31,7 @@ def test_trainer_runs(gpu, tmp_path, engine, ema):
     assert 0.0 <= float(score) <= 1.0
     assert torch.isfinite(torch.tensor(t.last_loss))
     if engine == 'fused':
-        assert t.graph_step is not None and t.graph_step.graph is not None   # hipGraph path really ran
+        assert t.engine is not None and t.engine.graph is not None   # hipGraph path really ran
     ck = torch.load(os.path.join(c.save_dir, 'last.pth'), weights_only=True)
     assert len(ck['state_dict']) == 1733
     # resume works on the fused optimizer (state_dict in torch's format)
@@ -75,7 +75,7 @@ def test_trainer_graph_with_ohem_and_kd(gpu, tmp_path, mode):
     c = _cfg(tmp_path, engine='fused', **kw)
     t = SegTrainer(c)
     t.run(c)
-    assert t.graph_step is not None and t.graph_step.graph is not None
+    assert t.engine is not None and t.engine.graph is not None
     assert torch.isfinite(torch.tensor(t.last_loss))
 
 
@@ -154,7 +154,7 @@ def test_trainer_fp16_amp_graph(gpu, tmp_path):
     t = SegTrainer(c)
     assert isinstance(t.scaler, FusedGradScaler) and t.scaler.is_enabled()
     t.run(c)
-    assert t.graph_step is not None and t.graph_step.graph is not None
+    assert t.engine is not None and t.engine.graph is not None
     assert torch.isfinite(torch.tensor(t.last_loss))
     assert t.scaler.get_scale() == 2.0 ** 16   # no overflow in a few bf16-computed steps
     ck = torch.load(os.path.join(c.save_dir, 'last.pth'), weights_only=True)
