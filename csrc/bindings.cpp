@@ -78,7 +78,7 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   TORCH_CHECK(wp.numel() == (int64_t)conv_rows_alloc(g.Go * g.Cgo) * g.Kp, "packed weight numel mismatch");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(g.Go == 1 && bias->numel() == g.Cgo_l, "bias: 1 group only");
   if (stat_part.has_value() && stat_part->defined())
-    TORCH_CHECK(stat_part->numel() == conv_stat_blocks(g) * 2 * g.Go * g.Cgo, "stat_part numel mismatch");
+    TORCH_CHECK(stat_part->numel() == conv_stat_blocks(g, trans) * 2 * g.Go * g.Cgo, "stat_part numel mismatch");
   a.w = bf(wp);
   a.bias = f32_opt(bias);
   a.stat_part = f32_opt_mut(stat_part);
@@ -151,8 +151,8 @@ bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::v
   return conv_uses_halo(make_geom(dims, dy, dx), trans);
 }
 
-int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
-  return conv_stat_blocks(make_geom(dims, dy, dx));
+int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  return conv_stat_blocks(make_geom(dims, dy, dx), trans);
 }
 
 void pack_weight_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
@@ -749,7 +749,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{}, py::arg("xrelu") = 0);
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);
-  m.def("conv_stat_blocks", &conv_stat_blocks_t);
+  m.def("conv_stat_blocks", &conv_stat_blocks_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans") = false);
   m.def("conv_uses_halo", &conv_uses_halo_t);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
   m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });

@@ -20,7 +20,11 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, 'medical_segmentation_pytorch_amd')
-BUILD = os.path.join(ROOT, 'build', 'csrc')
+# MSP_BUILD_VARIANT=ko: a profiling build with the halo kernels' perf knock-outs compiled in
+# (-DMSP_HALO_KNOCKOUTS=1; selected at run time by env MSP_HALO_DBG), written to
+# build/ko/_C.so and loaded instead of the product extension when env MSP_C_SO points at it
+VARIANT = os.environ.get('MSP_BUILD_VARIANT', '')
+BUILD = os.path.join(ROOT, 'build', 'csrc' + (f'_{VARIANT}' if VARIANT else ''))
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950').split(';')[0]
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 
@@ -40,6 +44,8 @@ def write_ninja(jobs):
     kernels = sorted(f for f in os.listdir(HERE) if f.endswith('.hip'))
     common = f'-O3 -fPIC -std=c++17 -D_GLIBCXX_USE_CXX11_ABI={abi} -I{HERE}'
     kflags = f'{common} --offload-arch={ARCH} -munsafe-fp-atomics -Wno-unused-result'
+    if VARIANT == 'ko':
+        kflags += ' -DMSP_HALO_KNOCKOUTS=1'
     bflags = (f'{common} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_C '
               f'-DTORCH_API_INCLUDE_EXTENSION_H -I{ROCM}/include -I{pyinc} -I{pybind11.get_include()} '
               + ' '.join(f'-isystem {p}' for p in tinc) + ' -Wno-deprecated-declarations')
@@ -48,7 +54,8 @@ def write_ninja(jobs):
     # libtorch_hip -> torch/lib/libamdhip64.so, i.e. the SAME runtime torch uses (never a 2nd copy).
     ldflags = (f'-shared -fPIC -L{tlib} -Wl,-rpath,{tlib} -Wl,--no-as-needed -lc10 -ltorch -ltorch_cpu '
                f'-ltorch_python -lc10_hip -ltorch_hip')
-    out = os.path.join(PKG, '_C.so')
+    out = os.path.join(PKG, '_C.so') if not VARIANT else os.path.join(ROOT, 'build', VARIANT, '_C.so')
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     lines = [
         f'hipcc = {hipcc}',
         f'kflags = {kflags}',

@@ -801,7 +801,7 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
 template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false>
-__global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+__global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
   __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
@@ -1226,7 +1226,11 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : 3) void co
       // No bias (every BN'd conv): the packed weights' padding rows are zero, so padding channels
       // accumulate exactly 0 and are stored as-is; the BN partials come from the fp32 accumulators
       // (the statistics of the stored bf16 values up to rounding noise) -- 11 instead of ~23 VALU ops
-      // per 4-channel quad in this issue-bound epilogue.
+      // per 4-channel quad in this issue-bound epilogue.  Parity note: the reference's autocast BN takes
+      // its statistics from the bf16 conv output itself; here they come from the fp32 values before
+      // that rounding (|diff| <= 2^-9 relative per element, unbiased), so the BN normalises the stored
+      // bf16 tensor with statistics of slightly different values -- a systematic, tolerance-level
+      // deviation (the bias path and the GEMM kernel use the rounded values).
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int p = (wave * NJ + j) * 16 + lr;
@@ -1394,7 +1398,14 @@ static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
 // MI <= 2, else 4); TW in {16, 32, 64} minimising (tiles) x (stores + halo loads).  The input is staged
 // whole (one chunk, LDS <= 64 KB) or -- single row group only -- in chunks of CC channels (CC | Cip, a
 // chunk's staging fits the kHaloLd registers per thread), widest CC first.
-static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe) ? 8 : 4; }
+// env MSP_HALO_NJ4=1: 256-pixel tiles (NJ = 4) for MI <= 2 too -- half the accumulators, 4 blocks / CU
+// instead of 3 (more blocks in different phases overlap staging, MFMAs and epilogue stores; A/B)
+static int g_nj4 = -1;
+static bool halo_nj4() {
+  if (g_nj4 < 0) { const char* e = getenv("MSP_HALO_NJ4"); g_nj4 = (e != nullptr && e[0] == '1') ? 1 : 0; }
+  return g_nj4 == 1;
+}
+static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe && !halo_nj4()) ? 8 : 4; }
 // env MSP_HALO_SMALL=1 enables the 128-pixel (NJ 2) halo tiles for inputs too wide for 256 pixels.  Off by
 // default: measured 1.3 % slower per step (L4 3x3 fwd -10 %, but dgrad +8 %, 1x7 fwd +26 %: at NJ 2 each
 // B fragment feeds only MI MFMAs and the halo ring is 40 % of the tile; profiles/r02/conv_bench_L4_small.log)
@@ -1536,10 +1547,14 @@ static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
   return hg.pipe ? std::min(nt, (long)kPipeGrid) : nt;   // PIPE: persistent grid
 }
 
-long conv_stat_blocks(const ConvGeom& g) {
+// Stat partial rows of a forward launch = its pixel-tile count, which depends on the kernel the launch
+// takes: ``trans`` (a strided transposed conv, conv_igemm's flag) never takes the GEMM or halo kernel --
+// sizing its rows by conv_gemm_ok(g, false) under-allocated the gather kernel's rows (out-of-bounds stat
+// writes: UNet / Linknet deconvs from 64 input channels up)
+long conv_stat_blocks(const ConvGeom& g, bool trans) {
   HaloGeom hg;
-  if (conv_gemm_ok(g, false)) return conv_gemm_stat_blocks(g);
-  if (halo_enabled() && conv_halo_ok(g, false, hg)) return halo_blocks(g, hg);
+  if (!trans && conv_gemm_ok(g, false)) return conv_gemm_stat_blocks(g);
+  if (!trans && halo_enabled() && conv_halo_ok(g, false, hg)) return halo_blocks(g, hg);
   const int mi = conv_pick_mi(g.Go * g.Cgo);
   const int nj = conv_pick_nj(g, mi);
   const int wpx = conv_pick_wpx(g, mi, nj);
@@ -1626,7 +1641,10 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     }
 #define HC_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe) {                                                                \
-      if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))                  \
+      if (MI_ <= 2 && hg.nj == 4) {                                                                          \
+        if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, 4, true, BNE_>))                                   \
+        else HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_>))                                             \
+      } else if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))            \
       else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>))                             \
       return 0;                                                                                              \
     }

@@ -72,7 +72,7 @@ void conv_set_halo(int on);
 void conv_set_small_halo(int on);   // opt-in 128-pixel halo tiles (tests / A-B)
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
 bool conv_uses_halo(const ConvGeom& g, bool trans);
-long conv_stat_blocks(const ConvGeom& g);
+long conv_stat_blocks(const ConvGeom& g, bool trans = false);   // trans: strided transposed (conv_igemm's flag)
 // returns 0, or an error code (conv_error_string) -- the bindings raise it as a Python error
 int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 const char* conv_error_string(int rc);

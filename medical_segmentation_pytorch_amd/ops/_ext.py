@@ -13,7 +13,15 @@ import torch
 _C = None
 _ERR = None
 try:
-    from .. import _C  # noqa: F401
+    if os.environ.get('MSP_C_SO'):   # a profiling variant of the extension (csrc/build.py MSP_BUILD_VARIANT)
+        import importlib.util
+        import sys
+        _spec = importlib.util.spec_from_file_location('medical_segmentation_pytorch_amd._C', os.environ['MSP_C_SO'])
+        _C = importlib.util.module_from_spec(_spec)
+        _spec.loader.exec_module(_C)
+        sys.modules['medical_segmentation_pytorch_amd._C'] = _C
+    else:
+        from .. import _C  # noqa: F401
 except Exception as e:  # pragma: no cover - depends on build state
     _ERR = e
 

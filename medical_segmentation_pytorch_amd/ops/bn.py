@@ -386,6 +386,25 @@ class _BNAct(torch.autograd.Function):
                 dbeta[:st.C] if dbeta is not None else None) + (dy,) * ctx.k
 
 
+# backward nodes whose data-gradient input may be a parked (not yet written) SyncBN dy: each calls
+# need_grads() before reading it (the parked-exchange invariant of _BNAct.backward)
+# (or that hands the gradient on unread to such nodes: _AddN, _Materialize)
+_FLUSHING_NODES = {'_ConvFnBackward', '_MultiConvFnBackward', '_BNActBackward', '_DuckTailBackward',
+                   '_Up2AddBackward', '_AddNBackward', '_MaterializeBackward', '_MaxPoolBackward',
+                   '_Up2CatBackward', '_AddActBackward'}
+
+
+def _check_deferrable(ts):
+    """Cheap guard of the ``defer_bwd`` invariant under multi-rank SyncBN: every input must come from one
+    of our autograd Functions (which flush the parked exchanges before reading a gradient) -- an input
+    produced by a stock torch op would let autograd read the parked dy before it is written."""
+    for t in ts:
+        gf = t.grad_fn
+        if gf is not None and type(gf).__name__ not in _FLUSHING_NODES:
+            raise RuntimeError(f'bn_act(defer_bwd=True): input produced by {type(gf).__name__}, which does not '
+                               'flush parked SyncBN exchanges; call with defer_bwd=False')
+
+
 def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None, deferred=False,
            defer_bwd=False):
     """act(BN(sum(xs))) for NHWC bf16 feature maps (``xs``: tensors and/or :class:`Deferred` BN
@@ -397,6 +416,8 @@ def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=Non
     if isinstance(xs, (torch.Tensor, Deferred)):
         xs = [xs]
     ts, coefs, mask = split_inputs(xs)
+    if defer_bwd and training and _world(st.group) > 1:
+        _check_deferrable(ts)
     out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd), (coefs, mask),
                               st.weight, st.bias, *ts)
     return Deferred(out, stats, relu) if deferred else out

@@ -102,7 +102,7 @@ class ConvPlan:
         oh, ow = self.out_hw(ih, iw)
         taps = self.taps_bwd if self.transposed else self.taps_fwd
         return require().conv_stat_blocks(self.fwd_dims(n, ih, iw, oh, ow), [t[0] for t in taps],
-                                          [t[1] for t in taps])
+                                          [t[1] for t in taps], self.transposed and self.stride > 1)
 
     # -- weight packing ---------------------------------------------------------------------------
     # A job = (src flat view, dst flat view, nrow, nch, T, Cpk, Kp, t_base, c_base, s_row, s_ch):
@@ -226,7 +226,7 @@ class _ConvFn(torch.autograd.Function):
             trans = False
         part = None
         if want_stats:
-            nblk = C.conv_stat_blocks(dims, dy, dx)
+            nblk = C.conv_stat_blocks(dims, dy, dx, trans)
             part = torch.empty(nblk, 2, plan.rows, dtype=torch.float32, device=dev)
         bias = plan.bias.detach().float().contiguous() if plan.bias is not None else None
         C.conv_fwd(xs, wp, ys, bias, part, dims, dy, dx, trans, coefs, rmask)

@@ -50,7 +50,15 @@ def cross_entropy(logits, target, weight=None, ignore_index=255):
 
 class _OHEM(torch.autograd.Function):
     """Per-pixel CE from the fused kernel; hard-pixel selection (threshold, else exact top-k) entirely on
-    the device (``loss.hip`` ohem_*): no host synchronisation, so the step stays graph-capturable."""
+    the device (``loss.hip`` ohem_*): no host synchronisation, so the step stays graph-capturable.
+
+    Two documented differences from the reference ``OhemCELoss`` (``core/loss.py:6-20``):
+      * no valid pixel at all (n_min = 0) and none above the threshold: the loss is 0 here, the
+        reference's ``torch.mean`` of an empty tensor is NaN;
+      * pixels tied at the k-th largest loss in the top-k fallback each get the fractional weight
+        (n_min - #greater) / #tied, where ``torch.topk`` gives the full 1/n_min to an arbitrary subset of
+        them: the loss VALUE is identical, the per-pixel gradients differ on the tied pixels only.
+        Tests that compare gradients bit-for-bit use tie-free inputs."""
 
     @staticmethod
     def forward(ctx, logits, target, thresh, ignore_index):

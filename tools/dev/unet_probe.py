@@ -27,11 +27,15 @@ def main():
     base = make_model(name, 32 if name == 'unet' else 17).to(dev).train()
     x = torch.randn(2, 3, size, size, device=dev)
     ref = copy.deepcopy(base)
+    print('ref forward ...', flush=True)
     with torch.backends.cudnn.flags(enabled=False):
         out_ref = ref(x)
+    print('ref forward done', flush=True)
     tgt = (F.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long()
     with torch.backends.cudnn.flags(enabled=False):
         F.cross_entropy(out_ref, tgt).backward()
+    torch.cuda.synchronize()
+    print('ref backward done', flush=True)
     for label, gemm, halo, phase, wg in [('default', 1, 1, 1, 1), ('gemm off', 0, 1, 1, 1), ('halo off', 1, 0, 1, 1),
                                          ('phase off', 1, 1, 0, 1), ('wgrad gemm off', 1, 1, 1, 0),
                                          ('all off', 0, 0, 0, 0)]:
@@ -39,10 +43,14 @@ def main():
         C.conv_set_halo(bool(halo))
         C.conv_set_phase(bool(phase))
         C.conv_set_wgrad_gemm(wg)
+        print(label, '...', flush=True)
         m = copy.deepcopy(base)
         ex = FusedExecutor(m)
         out = ex(x, training=True)
+        torch.cuda.synchronize()
+        print('  fwd ok', flush=True)
         F.cross_entropy(out, tgt).backward()
+        torch.cuda.synchronize()
         gc = [cos(p.grad, q.grad) for p, q in zip(m.parameters(), ref.parameters()) if q.grad is not None and q.grad.abs().sum() > 0]
         print(f'{label:16s} logits cos {cos(out, out_ref):.4f}  grad cos mean {sum(gc) / len(gc):.4f} min {min(gc):.4f}',
               flush=True)
