@@ -223,8 +223,11 @@ def main(argv=None):
         import torch.distributed as dist
         torch.cuda.set_device(dev_index)
         backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
-        # per-collective on-stream durations for the evidence pass (Work._get_duration)
-        os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
+        # per-collective on-stream durations for the evidence pass (Work._get_duration); not with a captured
+        # step: timing adds a start event per work, which the watchdog then queries while it belongs to the
+        # capturing stream (hipErrorCapturedEvent -> SIGABRT)
+        if not args.graph_ddp:
+            os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
         if args.graph_ddp:
             # RCCL inside a captured graph: the process group's shared event cache can hand an event that a
             # captured collective recorded to the watchdog's query (hipErrorCapturedEvent, seen as a

@@ -6,8 +6,10 @@ statistics in its epilogue and the BN(+ReLU) deferred into its consumers' stagin
 are the decoder kernels of ``csrc/decoder.hip`` (bilinear resize, GroupNorm, adaptive pooling,
 depthwise conv) and the existing elementwise ones (nearest up2 + add / concat, n-way add).  Concats
 that feed a conv are read as the conv's input channel groups where the widths allow it (ASPP's five
-branches, PSP's pyramid + input), so they are never built.  PAN and MAnet (attention / SE gating)
-keep the hybrid path: fused encoder, eager decoder (``FusedExecutor.smp_hybrid``).
+branches, PSP's pyramid + input, MAnet's gated high-level + skip), so they are never built.  PAN and
+MAnet: every conv / BN / pooling / resize on the HIP kernels; their attention glue (sigmoid gates,
+broadcast products, MAnet's position-attention matmuls + softmax) is torch tensor ops on the NHWC maps
+(the matmuls are plain library GEMMs on hipBLASLt).
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ from ..ops.bn import materialize
 from ..ops.conv import conv
 from ..ops.decoder import adaptive_avgpool, dwconv, group_norm_act, resize_bilinear
 from ..ops.elementwise import add_n, from_fm, up2_add
-from ..ops.pool import up2_cat
+from ..ops.pool import maxpool, up2_cat
 
 
 def _relu_of(m):
@@ -208,6 +210,96 @@ class SmpDecoders:
         return self.smp_head(model, y)
 
 
+    # -- PAN (FPA + GAU attention blocks) ---------------------------------------------------------------
+    def _cbr(self, m, x, training):
+        """smp ConvBnRelu: conv (+bias) -> BN -> optional ReLU -> optional bilinear x2 (align_corners)."""
+        y = materialize(self.conv_bn_act(m.conv, m.bn, m.activation if m.add_relu else nn.Identity(), x, training))
+        return resize_bilinear(y, scale_factor=2, align_corners=True) if m.interpolate else y
+
+    def _fpa(self, fpa, x, training):
+        x = materialize(x)
+        N, h, w, _ = x.shape
+        b1 = self._cbr(fpa.branch1[1], adaptive_avgpool(x, 1), training)
+        b1 = resize_bilinear(b1, size=(h, w), align_corners=True)
+        mid = self._cbr(fpa.mid[0], x, training)
+        x1 = self._cbr(fpa.down1[1], maxpool(x, 2, 2, 0), training)           # 1 channel (padded to 8)
+        x2 = self._cbr(fpa.down2[1], maxpool(x1, 2, 2, 0), training)
+        x3 = self._cbr(fpa.down3[2], self._cbr(fpa.down3[1], maxpool(x2, 2, 2, 0), training), training)
+        x3 = resize_bilinear(x3, size=(h // 4, w // 4), align_corners=True)
+        t = resize_bilinear(add_n(self._cbr(fpa.conv2, x2, training), x3), size=(h // 2, w // 2), align_corners=True)
+        t = resize_bilinear(add_n(t, self._cbr(fpa.conv1, x1, training)), size=(h, w), align_corners=True)
+        return t[..., :1] * mid + b1          # the 1-channel attention map broadcast over the channels
+
+    def _gau(self, gau, x, y, training):
+        """GAUBlock: up(y) + conv3x3-BN-ReLU(x) * sigmoid(BN(conv1x1(avgpool(y))))."""
+        y = materialize(y)
+        h, w = x.shape[1], x.shape[2]
+        y_up = resize_bilinear(y, size=(h, w), align_corners=True)
+        cb = gau.conv1[1]
+        g = torch.sigmoid(materialize(self.conv_bn_act(cb.conv, cb.bn, nn.Identity(), adaptive_avgpool(y, 1),
+                                                       training)))
+        return y_up + self._cbr(gau.conv2, x, training) * g
+
+    def smp_pan(self, model, images, training):
+        enc, dec = model.encoder, model.decoder
+        feats = self.resnet_encoder(enc, images, training)
+        x = self._fpa(dec.fpa, feats[-1], training)
+        x = self._gau(dec.gau3, feats[-2], x, training)
+        x = self._gau(dec.gau2, feats[-3], x, training)
+        x = self._gau(dec.gau1, feats[-4], x, training)
+        return self.smp_head(model, x)
+
+    # -- MAnet (position-attention center + multi-scale fusion attention blocks) -------------------------
+    def _pab(self, pab, x, training):
+        x = materialize(x)
+        b, h, w, Cp = x.shape
+        hw, P, C = h * w, pab.pab_channels, pab.in_channels
+        top = self.conv_plain(pab.top_conv, x, training).reshape(b, hw, -1)[..., :P]
+        center = self.conv_plain(pab.center_conv, x, training).reshape(b, hw, -1)[..., :P]
+        bottom = self.conv_plain(pab.bottom_conv, x, training).reshape(b, hw, -1)[..., :C]
+        sp = torch.softmax(torch.matmul(center, top.transpose(1, 2)).reshape(b, -1).float(), dim=1)
+        sp = torch.matmul(sp.to(x.dtype).reshape(b, hw, hw), bottom)          # [b, hw, C]
+        # the reference reshapes the [b, hw, C] product straight to [b, C, h, w] (no transpose): same here
+        sp = sp.reshape(b, C, h, w).permute(0, 2, 3, 1)
+        if Cp != C:
+            sp = F.pad(sp, (0, Cp - C))
+        return self.conv_plain(pab.out_conv, x + sp.contiguous(), training)
+
+    def _se(self, se, x, training):
+        """SE gate: avgpool -> 1x1 (+bias) -> ReLU -> 1x1 (+bias) -> sigmoid, [N, 1, 1, C]."""
+        g = self.conv_plain(se[1], adaptive_avgpool(materialize(x), 1), training)
+        g = self.conv_plain(se[3], torch.relu(g), training)
+        return torch.sigmoid(g)
+
+    def _mfab(self, blk, x, cx, skip, training):
+        y = self.cba(blk.hl_conv[0], x, training, single=True)
+        y = self.cba(blk.hl_conv[1], y, training)
+        cs = blk.hl_conv[1][0].out_channels
+        y = up2_cat(materialize(y), None, cs, 0)                               # nearest x2
+        att = self._se(blk.SE_hl, y, training)
+        if skip is None:
+            z = self.cba(blk.conv1, y, training, single=True)
+        else:
+            att = att + self._se(blk.SE_ll, skip, training)
+            z = self.cba(blk.conv1, [y * att, materialize(skip)], training, single=True)   # cat as 2 groups
+        return self.cba(blk.conv2, z, training), blk.conv2[0].out_channels
+
+    def smp_manet(self, model, images, training):
+        from ..models import smp
+        enc, dec = model.encoder, model.decoder
+        feats = self.resnet_encoder(enc, images, training)[::-1]
+        chans = list(enc.out_channels[1:])[::-1]
+        x, cx = self._pab(dec.center, feats[0], training), chans[0]
+        skips = feats[1:]
+        for i, blk in enumerate(dec.blocks):
+            skip = skips[i] if i < len(skips) else None
+            if isinstance(blk, smp.MFABBlock):
+                x, cx = self._mfab(blk, x, cx, skip, training)
+            else:
+                x, cx = self._unet_block(blk, x, cx, [(skip, chans[i + 1])] if skip is not None else [], training)
+        return self.smp_head(model, x)
+
+
 def fused_decoder_kind(model):
     """Name of the fused decoder method for an smp model (None: the hybrid eager-decoder path)."""
     from ..models import smp
@@ -227,4 +319,8 @@ def fused_decoder_kind(model):
         return 'smp_deeplabv3plus'
     if isinstance(dec, smp.PSPDecoder):
         return 'smp_pspnet' if isinstance(dec.conv[1], nn.BatchNorm2d) else None
+    if isinstance(dec, smp.PANDecoder):
+        return 'smp_pan' if dec.gau1.upscale_mode == 'bilinear' else None
+    if isinstance(dec, smp.MAnetDecoder):
+        return 'smp_manet' if all(isinstance(getattr(b, 'conv1')[1], nn.BatchNorm2d) for b in dec.blocks) else None
     return None

@@ -48,9 +48,9 @@ def _smp(arch, encoder):
                                                  (lambda: _smp('DeepLabV3', 'resnet18'), 128, 4),
                                                  (lambda: _smp('PSPNet', 'resnet18'), 64, 4),
                                                  (lambda: _smp('Linknet', 'resnet18'), 64, 4),
-                                                 # hybrid: fused encoder + eager decoder
-                                                 # (PAN's FPA block pools the stride-32 map to 1/8: >= 128 px)
-                                                 (lambda: _smp('PAN', 'resnet18'), 128, 4)])
+                                                 # (PAN's FPA block pools the stride-16 map to 1/8: >= 128 px)
+                                                 (lambda: _smp('PAN', 'resnet18'), 128, 4),
+                                                 (lambda: _smp('MAnet', 'resnet18'), 64, 4)])
 def test_fused_matches_eager(gpu, model_fn, size, batch):
     """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is."""
     torch.manual_seed(0)
@@ -199,7 +199,8 @@ def test_duck_tail_fused_matches_separate_nodes(gpu, monkeypatch):
         assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize('arch', ['UnetPlusPlus', 'Linknet', 'FPN', 'DeepLabV3', 'DeepLabV3Plus', 'PSPNet'])
+@pytest.mark.parametrize('arch', ['UnetPlusPlus', 'Linknet', 'FPN', 'DeepLabV3', 'DeepLabV3Plus', 'PSPNet', 'PAN',
+                                  'MAnet'])
 def test_decoders_fully_fused(arch):
     """These smp decoders run on the HIP kernels end to end: no sub-module is left to the eager path."""
     from medical_segmentation_pytorch_amd.runtime.fused_decoders import fused_decoder_kind

@@ -105,8 +105,7 @@ def test_backbones_and_modules_alias():
 
 
 def test_fused_engine_coverage_of_smp_hub():
-    """Which smp models the fused engine takes: every decoder over a plain ResNet encoder (Unet, Unet++,
-    Linknet, FPN, PSPNet, DeepLabV3/V3+ fully fused; MAnet and PAN as fused encoder + eager decoder),
+    """Which smp models the fused engine takes: every decoder over a plain ResNet encoder, fully fused,
     ResNeXt included (its grouped 3x3 runs on MIOpen inside the fused graph); MobileNetV2 (depthwise +
     ReLU6) stays eager.  Also the dilated MobileNetV2 encoder (DeepLabV3/V3+ output stride 8/16, smp
     ``replace_strides_with_dilation``)."""
@@ -115,7 +114,7 @@ def test_fused_engine_coverage_of_smp_hub():
     for arch in ['Unet', 'UnetPlusPlus', 'FPN', 'Linknet', 'MAnet', 'PAN', 'PSPNet', 'DeepLabV3', 'DeepLabV3Plus']:
         m = getattr(smp, arch)(encoder_name='resnet18', encoder_weights=None, classes=2)
         assert supports(m), arch
-        assert eager_parts(m) == (['decoder', 'segmentation_head'] if arch in ('MAnet', 'PAN') else []), arch
+        assert eager_parts(m) == [], arch   # every decoder runs on the fused kernels (runtime/fused_decoders.py)
         assert supports(getattr(smp, arch)(encoder_name='resnext50_32x4d', encoder_weights=None, classes=2)), arch
         assert not supports(getattr(smp, arch)(encoder_name='mobilenet_v2', encoder_weights=None, classes=2)), arch
     x = torch.randn(1, 3, 64, 64)
