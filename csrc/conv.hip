@@ -763,22 +763,10 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const int64_t* __restri
 // table lookup replaces the per-lane tap/bounds arithmetic of the gather kernel, and the input is read
 // from HBM once per tile (halo overhead (TH+ey)(TW+ex)/(TH*TW)) instead of once per tap from L2.
 // Waves split the tile's pixels (NJ 16-pixel columns each) and loop over the 16*MI-row groups.
-// LDS-DMA of 16 B per lane (global_load_lds_dwordx4): LDS[lds + 16*lane] = *src, lds wave-uniform via M0.
-// Inline asm (as conv_gemm.hip): the builtin would make the compiler drain every DMA in flight before any
-// later ds_read; the DMAP halo mode orders its DMAs with its own vmcnt(0) + barrier per tile.
-__device__ __attribute__((aligned(64))) uint4 g_halo_zero_page[4];
-DEVI void halo_glds16(const void* src, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
-}
-typedef __attribute__((address_space(3))) uint8_t halo_lds_u8_t;
-
 struct HaloGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
   int xtab;                          // deferred-BN prologue present: LDS coefficient table (3 x Cip fp32)
   int mi, pipe, nj;                  // row-group size (16*mi rows), PIPE mode, pixel columns per wave
-  int dmap;                          // DMAP mode: LDS-DMA double-buffered persistent tiles
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
   int dbg;                           // perf knock-outs (env MSP_HALO_DBG; 0 in production): 1 no y stores,
@@ -812,14 +800,8 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
-// DMAP (persistent grid, whole-input tiles whose pixel pitch == channel slots): the halo tile is staged
-// by LDS-DMA into one of two LDS buffers; the DMA of the block's NEXT tile is issued right after the
-// current tile's last MFMA loop, so it runs under the epilogue (stores, statistics) instead of as a
-// serial phase (the knock-outs show staging, MFMA loop and epilogue costing about a third each, unoverlapped).
-// It is issued after the last A-operand load on purpose: vector-memory loads complete in order, so an
-// A load issued behind an in-flight DMA would wait for it.
-template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool DMAP = false>
-__global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE || DMAP) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false>
+__global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
   __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
@@ -830,10 +812,8 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE || DMAP) ? 2 : ((
   const int Cip = g.Gi * g.Cgi, C8c = hg.CC >> 3;
   const int rows = g.Go * g.Cgo;
   const int hpx = hg.HH * hg.HWD;
-  // DMAP: two tile buffers of dma_elems (whole 64-vector chunks: the DMA tail lands inside the buffer)
-  const int dma_elems = DMAP ? ((hpx * C8c + 63) / 64) * 64 * 8 : 0;
-  // per-wave (sum, sum^2) rows after the tile(s): [kHaloWaves][2][rows] fp32
-  float* s_stat = reinterpret_cast<float*>(DMAP ? tile + 2 * dma_elems : tile + hpx * hg.pitch);
+  // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
+  float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
   // deferred-BN prologue table after them (hg.xtab): per input channel scale, shift and the ReLU floor
   // (0 or -inf); groups without a prologue get the identity (exact on bf16 values)
   float* s_coef = s_stat + kHaloWaves * 2 * rows;
@@ -1029,44 +1009,11 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE || DMAP) ? 2 : ((
   }
 
   const int n_rg = CHUNKED ? 1 : (rows + 16 * MI - 1) / (16 * MI);
-  const int t_end = (PIPE || DMAP) ? ntiles : wgid + 1;   // one tile per block unless persistent
-  // DMAP: DMA one whole halo tile (vectors idx = (halo pixel, 8-channel slot), contiguous in LDS since
-  // pitch == C8c slots) into buffer `dst`; out-of-image vectors and the chunk tail read the zero page
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(halo_lds_u8_t*)halo_smem;
-  auto dma_tile = [&](int t, int buf) {
-    int y0, x0;
-    long im;
-    set_tile(t, y0, x0, im);
-    const uint16_t* xb = a.x[0] + im * g.Cgi;
-    const int nchunk = (total + 63) / 64;
-    for (int ch = wave; ch < nchunk; ch += kHaloWaves) {
-      const int idx = ch * 64 + lane;
-      const void* src = g_halo_zero_page;
-      if (idx < total) {
-        const int hp = fdiv(idx, C8c, hg.inv_c8), c8 = idx - __mul24(hp, C8c);
-        const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
-        const int iy = y0 + hg.ey0 + hy, ix = x0 + hg.ex0 + hx;
-        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) src = xb + (iy * g.IW + ix) * g.Cgi + c8 * 8;
-      }
-      halo_glds16(src, __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(buf * dma_elems * 2 + ch * 1024)));
-    }
-  };
-  int it = 0;
-  if (DMAP) dma_tile(wgid, 0);
-  for (int tt = wgid; tt < t_end; tt += ((PIPE || DMAP) ? nwg : 1)) {
+  const int t_end = PIPE ? ntiles : wgid + 1;      // one tile per block unless PIPE (persistent grid)
+  for (int tt = wgid; tt < t_end; tt += (PIPE ? nwg : 1)) {
   set_tile(tt, ty0, tx0, img);
   xim0 = a.x[0] + img * g.Cgi;
-  if (DMAP) {
-    // this tile's DMA (issued one tile ago) and every store of the previous tile have landed; every
-    // wave is done reading the other buffer
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    tile = reinterpret_cast<uint16_t*>(halo_smem) + (it & 1) * dma_elems;
-    if (!BNE && hg.xtab) {   // deferred-BN prologue in place over the in-image vectors
-      xform_pass(0);
-      __syncthreads();
-    }
-  } else if (CHUNKED) {
+  if (CHUNKED) {
     load_batch(0, tid, pv, pd);   // host guarantees total <= 64*kHaloWaves*kHaloLd
   } else if (PIPE) {
     if (tt != wgid) __syncthreads();   // every wave is done reading the previous tile
@@ -1207,8 +1154,6 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE || DMAP) ? 2 : ((
         }
       }
     }
-    if (DMAP && rg == n_rg - 1 && tt + nwg < ntiles)
-      dma_tile(tt + nwg, (it + 1) & 1);   // next tile: in flight under this epilogue
     if (HALO_KO(hg, 16)) {   // knock-out: no epilogue (keep the accumulators alive)
       float t = 0.f;
 #pragma unroll
@@ -1352,7 +1297,6 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE || DMAP) ? 2 : ((
       }
     }
   }
-  ++it;
   }   // tile loop
   if (a.stat_part != nullptr) {
     __syncthreads();
@@ -1423,11 +1367,6 @@ int conv_rows_alloc(int rows) {
   return r;
 }
 
-static int g_dma_mode = -1;    // env MSP_HALO_DMA=1 enables the LDS-DMA double-buffered halo mode (DMAP)
-static bool halo_dma_enabled() {
-  if (g_dma_mode < 0) { const char* e = getenv("MSP_HALO_DMA"); g_dma_mode = (e != nullptr && e[0] == '1') ? 1 : 0; }
-  return g_dma_mode == 1;
-}
 static int g_pipe_mode = -1;   // env MSP_HALO_PIPE=0 disables the persistent pipelined halo kernels
 static bool pipe_enabled() {
   if (g_pipe_mode < 0) { const char* e = getenv("MSP_HALO_PIPE"); g_pipe_mode = (e == nullptr || e[0] != '0') ? 1 : 0; }
@@ -1515,39 +1454,6 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
   const int C8 = Cip / 8;
-  hg.dmap = 0;
-  // DMAP (env MSP_HALO_DMA=1, A/B): one input group, whole input (odd slot count -> pitch == slots, the
-  // tile is contiguous for the DMA), the standard tile (NJ per halo_nj), two tile buffers within ~78 KB
-  if (halo_dma_enabled() && g.Gi == 1 && (C8 & 1)) {
-    const int mi = conv_pick_mi(rows), nj = mi <= 2 ? 8 : 4, tp = kHaloWaves * nj * 16;
-    const int ks = cdiv(g.T * C8, 4);
-    double best = 1e30;
-    bool found = false;
-    for (int tw = 16; tw <= 64 && ks <= kHaloMaxKS; tw *= 2) {
-      const int th = tp / tw;
-      const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
-      const size_t buf = (size_t)((HH * HWD * C8 + 63) / 64) * 64 * 16;
-      if (2 * buf + (size_t)kHaloWaves * 2 * rows * 4 + 12 * (size_t)Cip > (size_t)kPipeMaxLds) continue;
-      const double tiles = (double)cdiv(g.OH, th) * cdiv(g.OW, tw);
-      const double cost = tiles * ((double)tp * rows / 8.0 + 0.5 * (double)HH * HWD * C8);
-      if (cost < best) { best = cost; found = true; hg.TH = th; hg.TW = tw; hg.HH = HH; hg.HWD = HWD; }
-    }
-    if (found) {
-      hg.ey0 = ey0; hg.ex0 = ex0;
-      hg.tiles_y = cdiv(g.OH, hg.TH);
-      hg.tiles_x = cdiv(g.OW, hg.TW);
-      hg.pitch = 8 * C8; hg.CC = 8 * C8; hg.nch = 1; hg.KS = ks;
-      hg.mi = mi; hg.nj = nj; hg.pipe = 0; hg.dmap = 1;
-      hg.tw_shift = hg.TW == 16 ? 4 : (hg.TW == 32 ? 5 : 6);
-      hg.inv_c8 = 1.0f / (float)C8;
-      const int step = 64 * kHaloWaves;
-      hg.st_q = step / C8; hg.st_r = step % C8;
-      hg.st_a = hg.st_q / hg.HWD; hg.st_b = hg.st_q % hg.HWD;
-      hg.inv_hwd = 1.0f / (float)hg.HWD;
-      hg.inv_cgi = 1.0f / (float)g.Cgi;
-      return true;
-    }
-  }
   // try 0: PIPE (whole input, halo tile within the prefetch registers); try 1: the standard kernels
   // PIPE pays where its 256-pixel tile is also the standard kernel's (MI 3) and the 3x3 halo is thin;
   // measured slower for the MI<=2 layers (which lose their 512-pixel tile) and the 1x7 / dilated halos
@@ -1619,11 +1525,7 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   return false;
 }
 
-static size_t halo_lds(const HaloGeom& hg, int rows) {
-  if (hg.dmap)   // two DMA tile buffers (whole 64-vector chunks) + the statistics rows
-    return 2 * (size_t)((hg.HH * hg.HWD * (hg.CC / 8) + 63) / 64) * 64 * 16 + (size_t)kHaloWaves * 2 * rows * 4;
-  return halo_lds_bytes(hg.HH, hg.HWD, hg.pitch, rows);
-}
+static size_t halo_lds(const HaloGeom& hg, int rows) { return halo_lds_bytes(hg.HH, hg.HWD, hg.pitch, rows); }
 
 static int g_halo_mode = -1;   // -1: from MSP_CONV_HALO (default on), 0: off, 1: on
 
@@ -1642,7 +1544,7 @@ bool conv_uses_halo(const ConvGeom& g, bool trans) {
 
 static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
   const long nt = (long)g.N * hg.tiles_y * hg.tiles_x;
-  return (hg.pipe || hg.dmap) ? std::min(nt, (long)kPipeGrid) : nt;   // PIPE / DMAP: persistent grid
+  return hg.pipe ? std::min(nt, (long)kPipeGrid) : nt;   // PIPE: persistent grid
 }
 
 // Stat partial rows of a forward launch = its pixel-tile count, which depends on the kernel the launch
@@ -1752,16 +1654,6 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       return 0;                                                                                              \
     }
     const bool bne = a.bn_y != nullptr;
-    if (hg.dmap) {
-#define HD_(MI_, BNE_)                                                                                       \
-      if (hmi == MI_ && bne == BNE_) {                                                                       \
-        HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, true>))                    \
-        return 0;                                                                                            \
-      }
-      HD_(1, false) HD_(2, false) HD_(3, false) HD_(4, false) HD_(1, true) HD_(2, true) HD_(3, true) HD_(4, true)
-#undef HD_
-      return 4;
-    }
     HS_(3, false) HS_(4, false) HS_(3, true) HS_(4, true)
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
     HP_(2, false) HP_(3, false) HP_(2, true) HP_(3, true)
