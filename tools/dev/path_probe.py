@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Dev probe: fused-vs-fp32 logits / grad cosine of a model under kernel-path switches (which conv path
-breaks a model?).  python tools/dev/unet_probe.py [unet|linknet|...]"""
+breaks a model?).  python tools/dev/path_probe.py <model> [size]   (model: tools/conv_bench-style names, e.g. unet, smp-linknet-resnet18)"""
 import copy
 import os
 import sys
