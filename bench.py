@@ -201,9 +201,10 @@ def model_label(args):
 
 
 # In-house reference speed: the reference's training step in eager PyTorch-ROCm on one
-# MI355X at its best measured config, DUCKNet-17 352x352 (profiles/eager_reference_speed.json; kept here
-# too because the profiles directory does not travel to the GPU boxes).
-EAGER_REFERENCE_IMG_S_PER_GPU = 120.27
+# MI355X at its best measured config, DUCKNet-17 352x352 -- channels-last bs64, 152.25 img/s (round-3
+# sweep over bs 16/32/64: 120.3 / 141.6 / 152.3; profiles/eager_reference_speed.json, kept here too
+# because the profiles directory does not travel to the GPU boxes).
+EAGER_REFERENCE_IMG_S_PER_GPU = 152.25
 
 
 def main(argv=None):

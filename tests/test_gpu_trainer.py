@@ -159,3 +159,20 @@ def test_trainer_fp16_amp_graph(gpu, tmp_path):
     assert t.scaler.get_scale() == 2.0 ** 16   # no overflow in a few bf16-computed steps
     ck = torch.load(os.path.join(c.save_dir, 'last.pth'), weights_only=True)
     assert ck['scaler']['scale'] == 2.0 ** 16
+
+
+def test_bench_step_is_the_trainer_step(gpu, tmp_path):
+    """bench.py's timed step is SegTrainer.train_step: one StepEngine (hipGraph-captured) driven by a real
+    trainer over its own DeviceAugLoader, with the trainer's scheduler and EMA -- and it trains."""
+    from medical_segmentation_pytorch_amd.runtime.bench_step import TrainerStep, bench_config
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import StepEngine
+    cfg = bench_config('ducknet', 8, 4, 64, 1e-3, 12, 16, 4, str(tmp_path / 'b'), device_index=0)
+    step = TrainerStep(cfg)
+    losses = [float(step()) for _ in range(10)]
+    tr = step.trainer
+    assert isinstance(tr.engine, StepEngine) and tr.engine.graph is not None
+    assert step.engine is tr.engine and tr.train_itrs == 10
+    assert tr.scheduler.last_epoch == 10                      # the trainer's own OneCycleLR stepped per iteration
+    assert all(l == l for l in losses) and min(losses[5:]) < losses[0]
+    dice, fg = step.validate()
+    assert 0.0 <= dice <= 1.0 and 0.0 <= fg <= 1.0
