@@ -201,10 +201,10 @@ def model_label(args):
 
 
 # In-house reference speed: the reference's training step in eager PyTorch-ROCm on one
-# MI355X at its best measured config, DUCKNet-17 352x352 -- channels-last bs64, 152.25 img/s (round-3
-# sweep over bs 16/32/64: 120.3 / 141.6 / 152.3; profiles/eager_reference_speed.json, kept here too
-# because the profiles directory does not travel to the GPU boxes).
-EAGER_REFERENCE_IMG_S_PER_GPU = 152.25
+# MI355X at its best measured config, DUCKNet-17 352x352 -- channels-last bs128, 158.37 img/s (round-3
+# sweep over bs 16/32/64/128: 120.3 / 141.6 / 152.3 / 158.4; profiles/eager_reference_speed.json, kept
+# here too because the profiles directory does not travel to the GPU boxes).
+EAGER_REFERENCE_IMG_S_PER_GPU = 158.37
 
 
 def main(argv=None):
