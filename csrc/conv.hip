@@ -770,7 +770,8 @@ struct HaloGeom {
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
   int dbg;                           // perf knock-outs (env MSP_HALO_DBG; 0 in production): 1 no y stores,
-                                     // 2 no staging loads, 4 no MFMAs, 8 no staging, 16 no epilogue
+                                     // 2 no staging loads, 4 no MFMAs, 8 no staging, 16 no epilogue,
+                                     // 32 no weight (A) loads
   float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
 };
 
@@ -1116,7 +1117,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         }
       }
       auto load_a = [&](uint4* A, int ks) {
-        if (CHUNKED) {
+        if (HALO_KO(hg, 32)) {   // knock-out: no weight loads (register-made A fragments)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) A[i] = make_uint4(ks, lr, i, 0);
+        } else if (CHUNKED) {
           const int ua = s_ua[4 * ks + lg];
 #pragma unroll
           for (int i = 0; i < MI; ++i)

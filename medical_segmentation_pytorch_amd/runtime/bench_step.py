@@ -160,6 +160,7 @@ class TrainerStep:
                 torch.manual_seed(1)
                 t = decoder_hub[cfg.teacher_decoder](encoder_name=cfg.teacher_encoder, encoder_weights=None,
                                                      in_channels=3, classes=cfg.num_class)
+                os.makedirs(os.path.dirname(cfg.teacher_ckpt), exist_ok=True)
                 tmp = cfg.teacher_ckpt + '.tmp'
                 torch.save({'state_dict': t.state_dict()}, tmp)
                 os.replace(tmp, cfg.teacher_ckpt)

@@ -130,6 +130,9 @@ def iteration(engine, scheduler, ema, itrs, images=None, masks=None):
     """One training iteration exactly as ``SegTrainer.train_one_epoch`` runs it: device step, then the
     per-iteration scheduler step and EMA update (reference core/seg_trainer.py:82-87)."""
     loss = engine(images, masks)
+    # the optimizer step ran inside the engine (launched, not via optimizer.step()): tell the LR
+    # scheduler's call-order check so, which it otherwise warns about on the first step
+    engine.optimizer._opt_called = True
     scheduler.step()
     ema.update(engine.model, itrs)
     return loss

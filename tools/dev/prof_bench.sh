@@ -12,3 +12,4 @@ db=$(python3 -c "import glob,sys; f=sorted(glob.glob(sys.argv[1]+'/**/*results.d
 cd "$root"
 python3 tools/rocpd_summary.py "$db" --steps 7 > "$root/gpurun_out/prof_$tag.txt" 2>&1
 python3 tools/rocpd_summary.py "$db" --steps 7 --group >> "$root/gpurun_out/prof_$tag.txt" 2>&1
+python3 tools/rocpd_timeline.py "$db" --steps 4 > "$root/gpurun_out/prof_${tag}_timeline.txt" 2>&1
