@@ -480,7 +480,11 @@ struct DwTile { int TH, TW, tw_shift, ey0, ex0, HH, HWd, HWv, tiles_y, tiles_x; 
 constexpr int kDwWaves = 8;      // waves per block: each owns <= 3 (tap, ci16) pairs of a 3x3
 constexpr int kDwMaxHalo = 640;  // halo pixels the staging registers cover (every T <= 9 tap set)
 constexpr long kDwSplitTarget = 256;
-constexpr int kDwMaxNcb = 3;     // 32-row dY sub-tiles per block, all sharing ONE staged input halo
+constexpr int kDwMaxNcb = 3;
+// two fragment sets (pipelined slice reads) where the registers allow it
+#ifndef DWB
+#define DWB(npw, ncb) ((ncb) * 2 + (npw) <= 5)
+#endif     // 32-row dY sub-tiles per block, all sharing ONE staged input halo
 constexpr int kDwMaxLds = 120 * 1024;
 constexpr double kDwHaloCost = 0.5;   // input-halo staging per tile, in units of one co sub-tile's work
 // staging elements per thread: NCB dY sub-tiles (2 slots of 128 pixels each) + the halo
@@ -493,8 +497,11 @@ DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 1
 // NCB > 1 (wide dY: horizontally fused convs, wide layers): the block owns NCB consecutive 32-row co
 // sub-tiles.  The input halo is staged, and every B fragment read from LDS, ONCE per slice for all of
 // them: one input pass per NCB sub-tiles instead of per sub-tile, and fewer LDS reads/writes per MFMA.
+#ifndef DW_MIN_WAVES
+#define DW_MIN_WAVES 1
+#endif
 template <int NPW, int NCB>
-__global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
+__global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
                                                               DwTile tl, int KT, long ntiles) {
   constexpr int NST = dw_stage(NCB);
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
@@ -546,11 +553,8 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
   for (int i = 0; i < 2; ++i) { offA[i][0] = dw_elem(plo, i, p4); offA[i][1] = dw_elem(phi, i, p4); }
   // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32.
   // Only the 16-channel halves that hold real channels are paired (a 40-channel input's second chunk
-  // has one), and co halves past `rows` are skipped: no MFMA runs on all-padding tiles.
+  // has one); pair slots past npairs read a valid address and are never stored.
   const int nhv = min(2, (Cip - ci0 + 15) >> 4);
-  int nco[NCB];
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) nco[cb] = max(0, min(2, (rows - co0 - DW_CH * cb + 15) >> 4));
   const int npairs = nhv * g.T;
   int offB[NPW][2];
 #pragma unroll
@@ -622,32 +626,52 @@ __global__ __launch_bounds__(64 * kDwWaves) void conv_wgrad_halo_kernel(WgradPtr
     }
     __syncthreads();
     if (tix + gridDim.x < ntiles) stage_load(tix + gridDim.x);   // in flight during the MFMAs
-    for (int sl = 0; sl < NSL; ++sl) {
+    // Slice loop: branch-free and software-pipelined -- slice s+1's transposed reads are issued before
+    // slice s's MFMAs (two fragment sets when the registers allow, DWB), so LDS latency hides under the
+    // MFMAs of the same wave.  MFMAs run unconditionally: a pair slot past npairs (or a co half past
+    // `rows`, whose staged dY is zero) accumulates into registers that are never stored.  Measured: the
+    // per-pair / per-half branches split every read -> wait -> MFMA into its own basic block, so nothing
+    // overlapped inside a wave (2 waves/SIMD: 53 % of wave cycles waiting, MFMA busy 0.19).
+    auto frags = [&](int sl, uint4 (&fa)[NCB][2], uint4 (&fb)[NPW]) {
       const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
-      uint4 fa[NCB][2];
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          fa[cb][i] = make_uint4(0, 0, 0, 0);
-          if (i < nco[cb]) {   // block-uniform: EXEC stays all ones for the transposed reads
-            const uint2 lo = tr_read(&sY[cb * SUB + sa + offA[i][0]]);
-            const uint2 hi = tr_read(&sY[cb * SUB + sa + offA[i][1]]);
-            fa[cb][i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          }
+          const uint2 lo = tr_read(&sY[cb * SUB + sa + offA[i][0]]);
+          const uint2 hi = tr_read(&sY[cb * SUB + sa + offA[i][1]]);
+          fa[cb][i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
         }
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
-        if (wave + kDwWaves * j < npairs) {
-          const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
-          const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
-          const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
+        const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
+        fb[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    };
+    auto mma = [&](const uint4 (&fa)[NCB][2], const uint4 (&fb)[NPW]) {
 #pragma unroll
-          for (int cb = 0; cb < NCB; ++cb)
+      for (int j = 0; j < NPW; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-              if (i < nco[cb]) acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb, acc[cb][i][j]);
-        }
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb[j], acc[cb][i][j]);
+    };
+    constexpr int NB = DWB(NPW, NCB) ? 2 : 1;
+    uint4 fa[NB][NCB][2], fb[NB][NPW];
+    if constexpr (NB == 2) {
+      frags(0, fa[0], fb[0]);
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) {
+        if (sl + 1 < NSL) frags(sl + 1, fa[(sl + 1) & 1], fb[(sl + 1) & 1]);
+        mma(fa[sl & 1], fb[sl & 1]);
+      }
+    } else {   // register-bound variants: one set (the scheduler still hoists reads across slices)
+      constexpr int UNR = NPW * NCB >= 9 ? 1 : NSL;   // <3,3> spills when unrolled
+#pragma unroll UNR
+      for (int sl = 0; sl < NSL; ++sl) {
+        frags(sl, fa[0], fb[0]);
+        mma(fa[0], fb[0]);
       }
     }
   }
@@ -1136,11 +1160,19 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       };
       uint4 A[MI];
       load_a(A, 0);
+      // the next k-step's B offset is read with its A prefetch: the table lookup is off the LDS
+      // read -> MFMA dependency chain of the current step (not in PIPE: its register budget is spent)
+      constexpr bool UBP = !PIPE;
+      int ub = UBP ? s_ub[lg] : 0;
       for (int ks = 0; ks < hg.KS; ++ks) {
         uint4 An[MI];
+        int ubn = 0;
         const bool more = ks + 1 < hg.KS;
-        if (more) load_a(An, ks + 1);
-        const int ub = s_ub[4 * ks + lg];
+        if (more) {
+          load_a(An, ks + 1);
+          if (UBP) ubn = s_ub[4 * (ks + 1) + lg];
+        }
+        if (!UBP) ub = s_ub[4 * ks + lg];
         uint4 B[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
@@ -1155,6 +1187,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         if (more) {
 #pragma unroll
           for (int i = 0; i < MI; ++i) A[i] = An[i];
+          if (UBP) ub = ubn;
         }
       }
     }
@@ -1756,13 +1789,17 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
     P.ncb = ncb;
     P.gy = cdiv(rows, DW_CH * ncb);
     P.gz = cdiv(g.Gi * g.Cgi, DW_CH);
-    // one 8-wave block per CU that software-pipelines its ~8 tiles beats more, shorter-lived blocks
+    // one 8-wave block per CU that software-pipelines its tiles beats more, shorter-lived blocks for a
+    // single ci sub-tile (L1: 256 vs 512 blocks 0.642 vs 0.648 ms); with two ci sub-tiles (L2, 40 ch)
+    // 512 blocks win (3x3 0.442 -> 0.417 ms, fused-8 2.59 -> 2.43 ms at bs128;
+    // profiles/r03/conv_bench_v9_dw_split_bs128.log)
     static long split_target = -1;   // blocks in the grid; env MSP_DW_SPLIT overrides (tuning)
     if (split_target < 0) {
       const char* e = getenv("MSP_DW_SPLIT");
-      split_target = (e != nullptr && atol(e) > 0) ? atol(e) : kDwSplitTarget;
+      split_target = (e != nullptr && atol(e) > 0) ? atol(e) : 0;
     }
-    P.nsplit = std::max(1L, std::min(split_target / ((long)P.gy * P.gz), P.ntiles));
+    const long target = split_target > 0 ? split_target : (P.gz >= 2 ? 2 : 1) * kDwSplitTarget;
+    P.nsplit = std::max(1L, std::min(target / ((long)P.gy * P.gz), P.ntiles));
     return P;
   }
   P.halo = false;
