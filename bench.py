@@ -205,6 +205,13 @@ def model_label(args):
 # sweep over bs 16/32/64/128: 120.3 / 141.6 / 152.3 / 158.4; profiles/eager_reference_speed.json, kept
 # here too because the profiles directory does not travel to the GPU boxes).
 EAGER_REFERENCE_IMG_S_PER_GPU = 158.37
+# The same protocol for the other BASELINE configs at 352x352 (eager channels-last, one measured batch each,
+# round 3: profiles/r03/eager_{r101_cl_bs64,kd_cl_bs32}.json): (model, base channel, teacher) -> img/s/GPU
+EAGER_REFERENCE_CONFIGS = {
+    ('ducknet', 17, None): EAGER_REFERENCE_IMG_S_PER_GPU,
+    ('smp-resnet101', None, None): 877.91,        # config #3: smp-Unet(ResNet-101), bs64
+    ('ducknet', 34, 'smp-resnet101'): 54.09,      # config #4: DUCKNet-34 + ResNet-101-Unet KD teacher, bs32
+}
 
 
 def main(argv=None):
@@ -321,14 +328,15 @@ def main(argv=None):
             baseline = (json.load(f).get('published') or {}).get('images_per_sec')
     except Exception:
         pass
-    if baseline is None and args.model == 'ducknet' and args.base_channel == 17 and args.size == 352 \
-            and not args.teacher:
-        per_gpu = EAGER_REFERENCE_IMG_S_PER_GPU
-        try:   # a re-measured value, where the profiles directory is present
-            with open(os.path.join(here, 'profiles', 'eager_reference_speed.json')) as f:
-                per_gpu = json.load(f)['images_per_sec_per_gpu']
-        except Exception:
-            pass
+    ref_key = (args.model, args.base_channel if args.model == 'ducknet' else None, args.teacher or None)
+    if baseline is None and args.size == 352 and ref_key in EAGER_REFERENCE_CONFIGS:
+        per_gpu = EAGER_REFERENCE_CONFIGS[ref_key]
+        if ref_key == ('ducknet', 17, None):
+            try:   # a re-measured value, where the profiles directory is present
+                with open(os.path.join(here, 'profiles', 'eager_reference_speed.json')) as f:
+                    per_gpu = json.load(f)['images_per_sec_per_gpu']
+            except Exception:
+                pass
         baseline = per_gpu * world
     if rank == 0:
         print(json.dumps({

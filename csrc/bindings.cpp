@@ -765,6 +765,7 @@ PYBIND11_MODULE(_C, m) {
     return conv_gemm_ok(make_geom(dims, dy, dx), trans);
   });
   m.def("conv_set_small_halo", [](bool on) { conv_set_small_halo(on ? 1 : 0); });
+  m.def("conv_set_wlds", [](bool on) { conv_set_wlds(on ? 1 : 0); });
   m.def("conv_set_phase", [](bool on) { conv_set_phase(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);
   m.def("unpack_wgrad", &unpack_wgrad_t, py::arg("src"), py::arg("dst"), py::arg("nrow"), py::arg("nch"),

@@ -791,6 +791,7 @@ struct HaloGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
   int xtab;                          // deferred-BN prologue present: LDS coefficient table (3 x Cip fp32)
   int mi, pipe, nj;                  // row-group size (16*mi rows), PIPE mode, pixel columns per wave
+  int wl;                            // non-PIPE: the packed weights staged in LDS (WL instantiation)
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
   int dbg;                           // perf knock-outs (env MSP_HALO_DBG; 0 in production): 1 no y stores,
@@ -825,7 +826,11 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
-template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false>
+// WL (whole-input, non-PIPE): the block's packed weight rows are staged in LDS next to the input tile, so
+// the k-loop reads A from LDS instead of one global (L2) load per k-step with a one-step prefetch --
+// the L2 latency was exposed in every k-step (knock-outs: the k-loop alone 0.198 ms of the L1 3x3
+// forward's 0.515 ms at bs128, ~4x its MFMA time)
+template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool WL = false>
 __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
@@ -857,7 +862,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   // the next tile).  Row pitch = an odd number of 16-B slots.
   uint16_t* sA = reinterpret_cast<uint16_t*>(s_coef + (hg.xtab ? 3 * Cip : 0));
   const int pitchA = (4 * hg.KS + 1) * 8;
-  if (PIPE) {
+  if (PIPE || WL) {
     const int rowsA = ((rows + 16 * MI - 1) / (16 * MI)) * 16 * MI;
     const int per_row = 4 * hg.KS;
     for (int e = tid; e < rowsA * per_row; e += 64 * kHaloWaves) {
@@ -1149,7 +1154,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             A[i] = ua >= 0 ? *reinterpret_cast<const uint4*>(wrow[i] + ua + c0) : make_uint4(0, 0, 0, 0);
-        } else if (PIPE) {
+        } else if (PIPE || WL) {
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             A[i] = *reinterpret_cast<const uint4*>(sA + (co0 + 16 * i + lr) * pitchA + 32 * ks + 8 * lg);
@@ -1452,6 +1457,12 @@ static bool halo_small_tile_enabled() {
   return g_small_tile == 1;
 }
 
+static int g_wlds = -1;   // env MSP_HALO_WLDS=0: weights stay in global memory (A/B of the WL kernels)
+static bool halo_wlds_enabled() {
+  if (g_wlds < 0) { const char* e = getenv("MSP_HALO_WLDS"); g_wlds = (e != nullptr && e[0] == '0') ? 0 : 1; }
+  return g_wlds == 1;
+}
+
 static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
   return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
 }
@@ -1546,6 +1557,17 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
       hg.mi = mi;
       hg.nj = nj;
       hg.pipe = pipe ? 1 : 0;
+      hg.wl = 0;
+      if (!pipe && pass == 0 && halo_wlds_enabled()) {
+        // weights in LDS when the block still fits next to its tile and no block per CU is lost: the
+        // non-PIPE kernels run (MI <= 2 && NJ <= 4) ? 4 : 3 blocks per CU by registers
+        const size_t lds0 = halo_lds_bytes(hg.HH, hg.HWD, pitch, rows) + 12 * (size_t)Cip;
+        const size_t lds1 = lds0 + pipe_a_bytes(rows, mi, ks);
+        const size_t stat = 4 * 4 * kHaloMaxKS + 512;   // static tap tables + slack
+        auto by_lds = [&](size_t b) { return (int)((160 * 1024) / (b + stat)); };
+        const int by_vgpr = (mi <= 2 && nj <= 4) ? 4 : 3;
+        if (lds1 <= halo_tile_cap() && std::min(by_vgpr, by_lds(lds1)) >= std::min(by_vgpr, by_lds(lds0))) hg.wl = 1;
+      }
       hg.tw_shift = hg.TW == 16 ? 4 : (hg.TW == 32 ? 5 : 6);
       hg.inv_c8 = 1.0f / (float)d;
       {
@@ -1573,6 +1595,7 @@ static bool halo_enabled() {
 
 void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
 void conv_set_small_halo(int on) { g_small_tile = on ? 1 : 0; }
+void conv_set_wlds(int on) { g_wlds = on ? 1 : 0; }
 bool conv_uses_halo(const ConvGeom& g, bool trans) {
   HaloGeom hg;
   if (conv_gemm_ok(g, trans)) return false;   // wide inputs: the LDS-tiled GEMM kernel (conv_gemm.hip)
@@ -1657,7 +1680,7 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     hg.dbg = dbg;
     if (hg.xtab && a.bn_y != nullptr) return 3;   // BN prologue (forward) and BN epilogue (dgrad) never meet
     const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) + (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0) +
-                       (hg.pipe ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
+                       ((hg.pipe || hg.wl) ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
     // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers.
     // The prologue table may take the dynamic LDS past 64 KB: opted into once per instantiation,
     // before any graph capture (the first call of every shape runs eagerly).
@@ -1682,6 +1705,7 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
         if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, 4, true, BNE_>))                                   \
         else HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_>))                                             \
       } else if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))            \
+      else if (hg.wl) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, true>))      \
       else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>))                             \
       return 0;                                                                                              \
     }
@@ -1962,6 +1986,11 @@ int conv_plan_selfcheck(int verbose) {
                   if (halo_lds(hg, rows) + 12 * (size_t)cin + pipe_a_bytes(rows, hg.mi, hg.KS) > (size_t)kPipeMaxLds)
                     fail("PIPE LDS budget", g);
                   if (hg.nch != 1 || C8 != d) fail("PIPE with channel chunks", g);
+                }
+                if (hg.wl) {
+                  if (hg.pipe || hg.nch != 1) fail("WL outside the whole-input non-PIPE kernel", g);
+                  if (halo_lds(hg, rows) + 12 * (size_t)cin + pipe_a_bytes(rows, hg.mi, hg.KS) > halo_tile_cap())
+                    fail("WL LDS budget", g);
                 }
                 if (cdiv(rows, 16 * hg.mi) * 16 * hg.mi > conv_rows_alloc(rows)) fail("weight rows under-allocated", g);
                 const long blocks = halo_blocks(g, hg);

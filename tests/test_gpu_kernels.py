@@ -54,6 +54,19 @@ def test_conv_small_halo_tile(gpu, case, monkeypatch):
         C.conv_set_small_halo(False)
 
 
+@pytest.mark.parametrize('case', CONV_CASES[:6])
+def test_conv_halo_weights_in_global(gpu, case):
+    """The halo kernels with the packed weights read from global memory (MSP_HALO_WLDS=0) instead of
+    staged in LDS (the default WL instantiations) -- both paths stay covered."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    C = _ext.require()
+    C.conv_set_wlds(False)
+    try:
+        test_conv_fwd_bwd(gpu, case)
+    finally:
+        C.conv_set_wlds(True)
+
+
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_fwd_bwd(gpu, case):
     n, h, w, ci, co, (kh, kw), s, pad, dil = case
