@@ -826,10 +826,9 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
-// WL (whole-input, non-PIPE): the block's packed weight rows are staged in LDS next to the input tile, so
-// the k-loop reads A from LDS instead of one global (L2) load per k-step with a one-step prefetch --
-// the L2 latency was exposed in every k-step (knock-outs: the k-loop alone 0.198 ms of the L1 3x3
-// forward's 0.515 ms at bs128, ~4x its MFMA time)
+// WL (whole-input, non-PIPE; opt-in, env MSP_HALO_WLDS=1): the block's packed weight rows are staged in
+// LDS next to the input tile, so the k-loop reads A from LDS instead of one global (L2) load per k-step
+// with a one-step prefetch (measured neutral: see halo_wlds_enabled)
 template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool WL = false>
 __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   extern __shared__ uint4 halo_smem[];
@@ -1165,19 +1164,11 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       };
       uint4 A[MI];
       load_a(A, 0);
-      // the next k-step's B offset is read with its A prefetch: the table lookup is off the LDS
-      // read -> MFMA dependency chain of the current step (not in PIPE: its register budget is spent)
-      constexpr bool UBP = !PIPE;
-      int ub = UBP ? s_ub[lg] : 0;
       for (int ks = 0; ks < hg.KS; ++ks) {
         uint4 An[MI];
-        int ubn = 0;
         const bool more = ks + 1 < hg.KS;
-        if (more) {
-          load_a(An, ks + 1);
-          if (UBP) ubn = s_ub[4 * (ks + 1) + lg];
-        }
-        if (!UBP) ub = s_ub[4 * ks + lg];
+        if (more) load_a(An, ks + 1);
+        const int ub = s_ub[4 * ks + lg];
         uint4 B[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
@@ -1192,7 +1183,6 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         if (more) {
 #pragma unroll
           for (int i = 0; i < MI; ++i) A[i] = An[i];
-          if (UBP) ub = ubn;
         }
       }
     }
@@ -1457,9 +1447,13 @@ static bool halo_small_tile_enabled() {
   return g_small_tile == 1;
 }
 
-static int g_wlds = -1;   // env MSP_HALO_WLDS=0: weights stay in global memory (A/B of the WL kernels)
+// env MSP_HALO_WLDS=1: the WL instantiations (weights in LDS).  Off by default: measured neutral to
+// slower (L1 3x3 fwd 0.535 -> 0.562 ms, 1x7 0.459 -> 0.435, the rest within noise; bench 505.7 img/s
+// either way; profiles/r03/conv_bench_v10_wl_{on,off}_bs128.log) -- the one-step global prefetch of A
+// already hides the L2 latency in the short (7-k-step) L1/L2 loops.
+static int g_wlds = -1;
 static bool halo_wlds_enabled() {
-  if (g_wlds < 0) { const char* e = getenv("MSP_HALO_WLDS"); g_wlds = (e != nullptr && e[0] == '0') ? 0 : 1; }
+  if (g_wlds < 0) { const char* e = getenv("MSP_HALO_WLDS"); g_wlds = (e != nullptr && e[0] == '1') ? 1 : 0; }
   return g_wlds == 1;
 }
 

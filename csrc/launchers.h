@@ -70,7 +70,7 @@ int conv_pick_mi(int rows);
 int conv_rows_alloc(int rows);
 void conv_set_halo(int on);
 void conv_set_small_halo(int on);   // opt-in 128-pixel halo tiles (tests / A-B)
-void conv_set_wlds(int on);         // halo kernels' weights in LDS (default) or global memory (tests / A-B)
+void conv_set_wlds(int on);         // halo kernels' weights in LDS (opt-in WL) or global memory (default)
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
 bool conv_uses_halo(const ConvGeom& g, bool trans);
 long conv_stat_blocks(const ConvGeom& g, bool trans = false);   // trans: strided transposed (conv_igemm's flag)

@@ -374,8 +374,11 @@ class _BNAct(torch.autograd.Function):
                 g_t[:st.C] += (tot[1] * stats[3])[:st.C]
             if b_t is not None:
                 b_t[:st.C] += tot[0][:st.C]
-        dy = torch.empty_like(y)
-        C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+        # no input needs a data-gradient (the first DUCK's in_bn over the image): only dgamma/dbeta
+        need_dy = any(ctx.needs_input_grad[9:])
+        dy = torch.empty_like(y) if need_dy else None
+        if need_dy:
+            C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
         if h is not None:   # break the output -> node -> ctx -> handle -> output cycle now
             h.y = h.stats = h.part = None
             ctx.handle = None

@@ -55,16 +55,16 @@ def test_conv_small_halo_tile(gpu, case, monkeypatch):
 
 
 @pytest.mark.parametrize('case', CONV_CASES[:6])
-def test_conv_halo_weights_in_global(gpu, case):
-    """The halo kernels with the packed weights read from global memory (MSP_HALO_WLDS=0) instead of
-    staged in LDS (the default WL instantiations) -- both paths stay covered."""
+def test_conv_halo_weights_in_lds(gpu, case):
+    """The opt-in WL halo kernels (packed weights staged in LDS, MSP_HALO_WLDS=1) -- both paths stay
+    covered."""
     from medical_segmentation_pytorch_amd.ops import _ext
     C = _ext.require()
-    C.conv_set_wlds(False)
+    C.conv_set_wlds(True)
     try:
         test_conv_fwd_bwd(gpu, case)
     finally:
-        C.conv_set_wlds(True)
+        C.conv_set_wlds(False)
 
 
 @pytest.mark.parametrize('case', CONV_CASES)
