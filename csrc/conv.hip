@@ -74,6 +74,23 @@ DEVI int in_pixel(int pn, int ph, int pw, int2 d, const ConvGeom& g) {
 // the Tv valid taps (a 3x3 s2 data-gradient does 2.25 of 9 taps' work on average, not 9).
 struct PhaseArgs { int s, py, px, OHp, OWp, Kloop; int tA[kMaxTaps]; };
 
+// 16-B load through a pointer the compiler cannot prove global (read back from LDS, or a
+// by-value struct member): a global_load,
+// not a FLAT load (FLAT also counts in lgkmcnt, so LDS waits would drain it)
+// (through an integer: an addrspacecast of the generic pointer is folded back into a FLAT load)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+DEVI uint4 ldg4(const uint16_t* p) {
+  const u32x4_t v =
+      *reinterpret_cast<const __attribute__((address_space(1))) u32x4_t*>(reinterpret_cast<uintptr_t>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// load8f through a global-memory pointer read back from LDS (the s_xc table)
+DEVI void load8f_g(const float* p, float* d) {
+  const uint4 a = ldg4(reinterpret_cast<const uint16_t*>(p)), b = ldg4(reinterpret_cast<const uint16_t*>(p + 4));
+  d[0] = __uint_as_float(a.x); d[1] = __uint_as_float(a.y); d[2] = __uint_as_float(a.z); d[3] = __uint_as_float(a.w);
+  d[4] = __uint_as_float(b.x); d[5] = __uint_as_float(b.y); d[6] = __uint_as_float(b.z); d[7] = __uint_as_float(b.w);
+}
+
 template <int MI, int NJ, int WPX, bool TRANS, bool PH = false, bool BNE = false>
 __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseArgs pa) {
   const ConvGeom& g = a.g;
@@ -141,7 +158,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
       uint4 v = make_uint4(0, 0, 0, 0);
       if (pn[j] >= 0 && kval) {
         const int pix = in_pixel<TRANS>(pn[j], ph[j], pw[j], d, g);
-        if (pix >= 0) { v = *reinterpret_cast<const uint4*>(xb + (long)pix * g.Cgi); ok |= 1u << j; }
+        if (pix >= 0) { v = ldg4(xb + (long)pix * g.Cgi); ok |= 1u << j; }
       }
       B[j] = v;
     }
@@ -153,8 +170,8 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
     if (PH || p.t >= g.T) return 0;
     const float* cf = s_xc[p.gi];
     if (cf == nullptr) return 0;
-    load8f(cf + p.cl, sc);
-    load8f(cf + g.Cgi + p.cl, sh);
+    load8f_g(cf + p.cl, sc);
+    load8f_g(cf + g.Cgi + p.cl, sh);
     return 1 | (int)(((a.xrelu >> p.gi) & 1u) << 1);
   };
   auto xform_b = [&](uint4* B, unsigned ok, int mode, const float* sc, const float* sh) {
@@ -168,10 +185,10 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
       const int off = p.t < g.T ? s_ta[p.t] * (g.Gi * g.Cgi) + p.gi * g.Cgi + p.cl : -1;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
-        A[i] = off >= 0 ? *reinterpret_cast<const uint4*>(wrow[i] + off) : make_uint4(0, 0, 0, 0);
+        A[i] = off >= 0 ? ldg4(wrow[i] + off) : make_uint4(0, 0, 0, 0);
     } else {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + k0);
+      for (int i = 0; i < MI; ++i) A[i] = ldg4(wrow[i] + k0);
     }
   };
 
@@ -826,6 +843,7 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // convs reads 8 dY groups), padding units zero A, the next chunk's global loads are in flight in
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
+
 // WL (whole-input, non-PIPE; opt-in, env MSP_HALO_WLDS=1): the block's packed weight rows are staged in
 // LDS next to the input tile, so the k-loop reads A from LDS instead of one global (L2) load per k-step
 // with a one-step prefetch (measured neutral: see halo_wlds_enabled)
@@ -835,12 +853,21 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
   __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
   __shared__ int s_ub[kHaloMaxKS * 4];
+  // input-group pointers in LDS: staging indexes them per lane.  a.x[gi] with a lane-varying gi compiles
+  // to a global load of the pointer from the kernarg segment + s_waitcnt vmcnt(0) before the data load,
+  // which drains every staging load in flight -- the staging loop then ran one round trip at a time (a
+  // select chain over a.x[] is folded back into that load); an LDS read waits on lgkmcnt only.
+  __shared__ const uint16_t* s_xp[kMaxGroups];
+  // (pointers read back from LDS are generic: loads through them would be FLAT, counted in lgkmcnt too,
+  // so the next pointer read's lgkmcnt wait would drain them again -- load through global pointers)
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int Cip = g.Gi * g.Cgi, C8c = hg.CC >> 3;
   const int rows = g.Go * g.Cgo;
   const int hpx = hg.HH * hg.HWD;
+  if (tid < kMaxGroups) s_xp[tid] = a.x[tid];
+  if (g.Gi > 1) __syncthreads();   // block-uniform; Gi == 1 staging never reads s_xp
   // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
   float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
   // deferred-BN prologue table after them (hg.xtab): per input channel scale, shift and the ReLU floor
@@ -911,10 +938,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
           const int ci = c0 + c8 * 8;
           const int pix = iy * g.IW + ix;
           if (g.Gi == 1) {
-            v[u] = *reinterpret_cast<const uint4*>(xim0 + pix * g.Cgi + ci);
+            v[u] = ldg4(xim0 + pix * g.Cgi + ci);
           } else {
             const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
-            v[u] = *reinterpret_cast<const uint4*>(a.x[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+            v[u] = ldg4(s_xp[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
           }
         }
       }
@@ -988,10 +1015,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
           const int pix = iy * g.IW + ix;
           pd[u] |= (c8 + 1) << 16;
           if (g.Gi == 1) {
-            pv[u] = *reinterpret_cast<const uint4*>(xb + pix * g.Cgi + ci);
+            pv[u] = ldg4(xb + pix * g.Cgi + ci);
           } else {
             const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
-            pv[u] = *reinterpret_cast<const uint4*>(a.x[gi] + im * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+            pv[u] = ldg4(s_xp[gi] + im * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
           }
         }
       }
@@ -1074,10 +1101,10 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
             const int pix = iy * g.IW + ix;
             cc[u] = c8;
             if (g.Gi == 1) {
-              v[u] = *reinterpret_cast<const uint4*>(xim0 + pix * g.Cgi + ci);
+              v[u] = ldg4(xim0 + pix * g.Cgi + ci);
             } else {
               const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
-              v[u] = *reinterpret_cast<const uint4*>(a.x[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+              v[u] = ldg4(s_xp[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
             }
           }
         }
