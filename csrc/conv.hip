@@ -84,6 +84,18 @@ DEVI uint4 ldg4(const uint16_t* p) {
       *reinterpret_cast<const __attribute__((address_space(1))) u32x4_t*>(reinterpret_cast<uintptr_t>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+// 8-B global load / store through a pointer read back from LDS (the igemm epilogue's s_y table)
+DEVI uint2 ldg2(const uint16_t* p) {
+  const u32x2_t v =
+      *reinterpret_cast<const __attribute__((address_space(1))) u32x2_t*>(reinterpret_cast<uintptr_t>(p));
+  return make_uint2(v.x, v.y);
+}
+DEVI void stg2(uint16_t* p, uint2 v) {
+  u32x2_t w;
+  w.x = v.x; w.y = v.y;
+  *reinterpret_cast<__attribute__((address_space(1))) u32x2_t*>(reinterpret_cast<uintptr_t>(p)) = w;
+}
 // load8f through a global-memory pointer read back from LDS (the s_xc table)
 DEVI void load8f_g(const float* p, float* d) {
   const uint4 a = ldg4(reinterpret_cast<const uint16_t*>(p)), b = ldg4(reinterpret_cast<const uint16_t*>(p + 4));
@@ -266,7 +278,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
         float v[4];
         float old[4] = {0.f, 0.f, 0.f, 0.f};
         if (!BNE && a.accum) {   // y += conv(x): add the stored bf16 output (sibling launches' dgrads)
-          const uint2 ov = *reinterpret_cast<const uint2*>(yb + mo * g.Cgo);
+          const uint2 ov = ldg2(yb + mo * g.Cgo);
           old[0] = __uint_as_float(ov.x << 16); old[1] = __uint_as_float(ov.x & 0xffff0000u);
           old[2] = __uint_as_float(ov.y << 16); old[3] = __uint_as_float(ov.y & 0xffff0000u);
         }
@@ -296,7 +308,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
             csq[i][r] += v[r] * v[r];
           }
         }
-        *reinterpret_cast<uint2*>(yb + mo * g.Cgo) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        stg2(yb + mo * g.Cgo, make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])));
       }
     }
   }
