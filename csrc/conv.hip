@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * WPX) void conv_igemm_kernel(ConvArgs a, PhaseA
 // layout and feeds the MFMA with ds_read_b64_tr_b16 (hardware transpose read, CDNA4).  The next
 // chunk's global loads are issued into registers before the current chunk's MFMAs (register
 // double-buffering).  Each of the 4 waves reduces 32 pixels of a chunk; the waves' partial tiles are
-// summed through LDS, then across pixel splits with fp32 atomics into dW (zeroed by the caller).
+// summed through LDS; each pixel split writes its own fp32 slab, summed in fixed order by unpack_wgrad.
 constexpr int WG_M = 128;
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
     __syncthreads();
   }
 
-  // sequential cross-wave accumulation in LDS (fp32 tile), then one atomic per element
+  // sequential cross-wave accumulation in LDS (fp32 tile), then one slab store per element
   float* red = reinterpret_cast<float*>(smem);
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradPtrs P, float* __r
 // in LDS ONCE, and every tap reads its shifted window of the halo with ds_read_b64_tr_b16 (each lane
 // supplies its own pixel row address, so the shift is free).  Block output = dW[32 co][T taps][32 ci];
 // the 4 waves own disjoint (tap, ci16) pairs, so no cross-wave reduction.  Blocks loop over pixel
-// tiles (accumulating in registers) and finish with one fp32 atomic per output element.
+// tiles (accumulating in registers) and finish by writing the block's fp32 slab (deterministic split-K).
 // LDS layout: one 64-B row per pixel (32 channels, no padding); the two 32-B halves are XOR-swizzled
 // by bit 3 of the pixel index.  A transposed read of 32 lanes touches pixels {b..b+3, b+8..b+11}
 // (+ a tap shift): pixels p and p+8 share a bank quadrant and always sit in opposite halves, so both
