@@ -47,7 +47,6 @@ def parse_args(argv=None):
                    help="ducknet | unet | smp-<resnet encoder> (e.g. smp-resnet101, BASELINE config #3)")
     p.add_argument('--teacher', default=None,
                    help='KD teacher (e.g. smp-resnet101; BASELINE config #4 = --base-channel 34 --teacher smp-resnet101)')
-    p.add_argument('--graph-ddp', action='store_true', help='also capture the multi-GPU step in a hipGraph')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
     p.add_argument('--ddp', action='store_true',
@@ -118,7 +117,7 @@ def val_dice(model, args, device, seed):
     return float(dice.mean()), float(dice[1])
 
 
-def comm_evidence(step, args, dist, step_ms):
+def comm_evidence(step, args, dist, step_ms, device):
     """Multi-GPU evidence, measured AFTER the timed region (and after the Dice): (1) ``comm_steps``
     instrumented steps -- per gradient bucket its size, RCCL on-stream time, how long before the end of
     backward it was issued (the compute it can hide under) and whether it only left at finish(); every
@@ -130,21 +129,25 @@ def comm_evidence(step, args, dist, step_ms):
     bk = getattr(step, 'bucketer', None)
     n = args.comm_steps
     world = dist.get_world_size()
-    dev = torch.cuda.current_device()
+    cuda = device.type == 'cuda'
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(device)
     out = {'world_size': world, 'backend': dist.get_backend(),
-           'rccl_version': '.'.join(str(v) for v in torch.cuda.nccl.version()) if torch.cuda.is_available() else None,
+           'rccl_version': '.'.join(str(v) for v in torch.cuda.nccl.version()) if cuda else None,
            'timed_step_ms': round(step_ms, 3)}
     if bk is not None:
         bk.instrument = True
     bnmod.COMM['instrument'] = True
     bnmod.COMM['works'] = []
     ex0 = bnmod.EXCHANGES[0]
-    torch.cuda.synchronize(dev)
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(n):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     out['instrumented_step_ms'] = round((time.perf_counter() - t0) / n * 1e3, 3)
     out['syncbn_exchanges_per_step'] = (bnmod.EXCHANGES[0] - ex0) / n
     durs = []
@@ -168,18 +171,20 @@ def comm_evidence(step, args, dist, step_ms):
                                        if any(r['rccl_ms'] is not None for r in rs) else None),
                            'issue_to_bwd_end_ms': round(statistics.median([r['issue_to_bwd_end_ms'] for r in rs]), 3),
                            'late': any(r['late'] for r in rs)} for b, rs in sorted(per.items())]
-        out['grad_ready_order_monotone'] = bk.ready_order == sorted(bk.ready_order, reverse=True)
+        ro = list(dict.fromkeys(bk.ready_order))
+        out['buckets_rebuilt_in_ready_order'] = bool(bk.rebuilt) and bk.bucket_order()[:len(ro)] == ro
+        out['grad_ready_order_is_reverse_registration'] = ro == sorted(ro, reverse=True)
     # knock-out pass
     if bk is not None:
         bk.enabled = False
     bnmod.COMM['enabled'] = False
-    torch.cuda.synchronize(dev)
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(n):
         step()
-    torch.cuda.synchronize(dev)
-    t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], device=torch.device('cuda', dev), dtype=torch.float64)
+    sync()
+    t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], device=device, dtype=torch.float64)
     bnmod.COMM['enabled'] = True
     if bk is not None:
         bk.enabled = True
@@ -214,40 +219,60 @@ EAGER_REFERENCE_CONFIGS = {
 }
 
 
+def self_launch(args, argv=None):
+    """``python bench.py --gpus N`` (N > 1) without a launcher: start N rank processes (torchrun
+    environment, one per GPU) BEFORE this process makes any GPU call, supervise them (the first failing
+    rank stops the rest) and return the job's exit code.  Returns None when this process is a rank."""
+    if args.gpus <= 1 or os.environ.get('WORLD_SIZE') is not None:
+        return None
+    from medical_segmentation_pytorch_amd.utils.launch import spawn_ranks
+    rest = list(sys.argv[1:] if argv is None else argv)
+    print(f'[bench] no WORLD_SIZE in the environment: starting {args.gpus} ranks (one per GPU)', file=sys.stderr,
+          flush=True)
+    return spawn_ranks(args.gpus, [os.path.abspath(__file__)] + rest)
+
+
 def main(argv=None):
     args = parse_args(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus and rank == 0:
-        print(f'[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
 
     dist = None
+    cuda = torch.cuda.is_available()   # (first GPU call of this process: after the self-launch decision)
     # test hooks: BENCH_DIST_BACKEND=gloo + BENCH_SAME_DEVICE=1 rehearse the N-rank path on one GPU
-    # (RCCL refuses two ranks per device); the driver's runs use RCCL, one rank per GPU
+    # (RCCL refuses two ranks per device); the driver's runs use RCCL, one rank per GPU.  Without a GPU the
+    # whole contract runs on the CPU over gloo (the trainer's eager engine): the CPU test tier's rehearsal.
     dev_index = 0 if os.environ.get('BENCH_SAME_DEVICE') == '1' else local_rank
     ddp = world > 1 or args.ddp
     if ddp:
         import torch.distributed as dist
-        torch.cuda.set_device(dev_index)
-        backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl')
-        # per-collective on-stream durations for the evidence pass (Work._get_duration); not with a captured
-        # step: timing adds a start event per work, which the watchdog then queries while it belongs to the
-        # capturing stream (hipErrorCapturedEvent -> SIGABRT)
-        if not args.graph_ddp:
-            os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
-        if args.graph_ddp:
-            # RCCL inside a captured graph: the process group's shared event cache can hand an event that a
-            # captured collective recorded to the watchdog's query (hipErrorCapturedEvent, seen as a
-            # sporadic SIGABRT); per-work events keep captured and watched events apart
-            os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
+        if cuda:
+            torch.cuda.set_device(dev_index)
+        backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl' if cuda else 'gloo')
+        # per-collective on-stream durations for the evidence pass (Work._get_duration)
+        os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
         kw = {'device_id': torch.device('cuda', dev_index)} if backend == 'nccl' else {}
         dist.init_process_group(backend, **kw)
         world, rank = dist.get_world_size(), dist.get_rank()   # the process group's own view (n_gpus)
-    device = torch.device('cuda', dev_index)
+    if world != args.gpus:
+        # a bench that silently ran a different job size would report a wrong n_gpus / scaling point
+        print(f'[bench] error: --gpus {args.gpus} but the job has {world} rank(s)', file=sys.stderr, flush=True)
+        sys.exit(3)
+    device = torch.device('cuda', dev_index) if cuda else torch.device('cpu')
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
 
     impl = args.impl
-    use_graph = not args.no_graph and (not ddp or args.graph_ddp)
+    # multi-GPU steps run uncaptured (RCCL collectives outside any hipGraph); at the bench batch the step
+    # is GPU-bound, so the ~2k host launches per step are hidden behind the GPU (round 2: graph vs no
+    # graph within 1 %)
+    use_graph = cuda and not args.no_graph and not ddp
     total_steps = args.warmup + args.steps + 2 * args.comm_steps + 2
     save_dir = None
     if impl == 'fused':
@@ -261,7 +286,9 @@ def main(argv=None):
                            args.train_images, args.val_images, save_dir,
                            device_index=dev_index if (not ddp or same_dev) else None, teacher_name=args.teacher,
                            use_graph=use_graph, dist_backend=os.environ.get('BENCH_DIST_BACKEND') if ddp else None,
-                           world=world)
+                           world=world, dist_world1_bucketer=ddp)
+        if not cuda:
+            cfg.base_workers = 0   # CPU rehearsal: batches built in-process
         step = TrainerStep(cfg, fixed=args.data == 'fixed')
     else:
         from medical_segmentation_pytorch_amd.runtime.bench_step import build_bench_step
@@ -284,20 +311,20 @@ def main(argv=None):
     for i in range(args.warmup):
         step()
         if rank == 0:   # progress on stderr (first eager steps can spend minutes in MIOpen's kernel search)
-            torch.cuda.synchronize()
+            sync()
             print(f'[bench] warmup {i + 1}/{args.warmup} done at {time.perf_counter() - t_w:.1f}s', file=sys.stderr,
                   flush=True)
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -320,7 +347,7 @@ def main(argv=None):
     # eager side, whose DDP+SyncBN would scale sub-linearly).
     comm = None
     if dist is not None and args.comm_steps > 0 and impl == 'fused' and not use_graph:
-        comm = comm_evidence(step, args, dist, ms)
+        comm = comm_evidence(step, args, dist, ms, device)
     baseline = None
     here = os.path.dirname(os.path.abspath(__file__))
     try:
@@ -346,9 +373,10 @@ def main(argv=None):
             'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': round(value / baseline, 3) if baseline else None,
-            'dtype': 'bf16',
+            'dtype': 'bf16' if cuda else 'fp32',
             'data': (f'synthetic {args.size}x{args.size} polyp images/masks, random-init weights; ' +
-                     (('fresh batch per step from the trainer\'s DeviceAugLoader (HBM-resident split, MyConfig '
+                     ('CPU rehearsal (no GPU): host DataLoader, eager engine over gloo' if not cuda else
+                      ('fresh batch per step from the trainer\'s DeviceAugLoader (HBM-resident split, MyConfig '
                        'augmentation on the GPU) inside the timed loop' if impl == 'fused' else
                        'fresh GPU-augmented batch per step (MyConfig aug) inside the timed loop')
                       if args.data == 'augment' else 'one resident batch replayed')),

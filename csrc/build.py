@@ -82,18 +82,56 @@ def write_ninja(jobs):
     return path, out
 
 
-def build(jobs=None, verbose=False):
+def _mtimes(paths):
+    return {p: (os.path.getmtime(p) if os.path.exists(p) else None) for p in paths}
+
+
+def sha256(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, 'rb') as f:
+        for chunk in iter(lambda: f.read(1 << 20), b''):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def build(jobs=None, verbose=False, force=None):
+    """Incremental ninja build; prints which objects were (re)compiled this call and the sha256 of the
+    linked extension, and records both in ``build/BUILD_INFO.json`` (provenance: the same digest is
+    printed by ``__graft_entry__.smoke()`` from the .so the GPU process actually loaded).
+    ``force`` (or env MSP_FORCE_REBUILD=1): clean first, so every kernel is recompiled."""
+    import json
+    import time
     path, out = write_ninja(jobs)
     ninja = shutil.which('ninja')
     if ninja is None:
         import ninja as _nj  # pip package ships the binary
         ninja = os.path.join(_nj.BIN_DIR, 'ninja')
+    force = os.environ.get('MSP_FORCE_REBUILD') == '1' if force is None else force
+    if force:
+        subprocess.run([ninja, '-f', path, '-t', 'clean'], check=True, cwd=BUILD, stdout=subprocess.DEVNULL)
+    objs = sorted(os.path.join(BUILD, f.replace('.hip', '.o')) for f in os.listdir(HERE) if f.endswith('.hip'))
+    objs.append(os.path.join(BUILD, 'bindings.o'))
+    before = _mtimes(objs + [out])
     cmd = [ninja, '-f', path]
     if jobs:
         cmd += ['-j', str(jobs)]
     if verbose:
         cmd.append('-v')
     subprocess.run(cmd, check=True, cwd=BUILD)
+    after = _mtimes(objs + [out])
+    compiled = [os.path.basename(p) for p in objs if after[p] != before[p]]
+    info = {'arch': ARCH, 'extension': os.path.relpath(out, ROOT), 'sha256': sha256(out),
+            'compiled_this_call': compiled, 'relinked': after[out] != before[out],
+            'objects': [os.path.basename(p) for p in objs], 'time': time.strftime('%Y-%m-%d %H:%M:%S')}
+    os.makedirs(os.path.join(ROOT, 'build'), exist_ok=True)
+    with open(os.path.join(ROOT, 'build', 'BUILD_INFO.json' if not VARIANT else f'BUILD_INFO_{VARIANT}.json'),
+              'w') as f:
+        json.dump(info, f, indent=1)
+    print(f'[build] {ARCH}: compiled {len(compiled)}/{len(objs)} objects this call '
+          f'({", ".join(compiled) if compiled else "all up to date"}); '
+          f'{"relinked" if info["relinked"] else "unchanged"} {info["extension"]} sha256={info["sha256"][:16]}',
+          flush=True)
     return out
 
 

@@ -133,7 +133,8 @@ class BaseConfig:
         self.cap_workers = True        # cap DataLoader workers at the host CPU count (ref: gpu_num*base_workers)
         self.teacher_base_channel = None
         self.graph_warmup = 3          # eager iterations before the hipGraph capture
-        self.graph_ddp = False         # also capture multi-GPU steps (RCCL inside the graph)
+        self.bucketer_world1 = False   # attach the RCCL gradient bucketer at world size 1 too (bench --ddp
+                                       # evidence run); a step with a bucketer is never graph-captured
         self.val_fp32 = False          # validate the EMA model in fp32 eager PyTorch exactly as the reference
                                        # (core/seg_trainer.py:114); False: the bf16 fused executor (fast)
         self.progress_bar = True

@@ -90,10 +90,14 @@ class SegTrainer(BaseTrainer):
 
     def _use_graph(self, config):
         # every loss (CE, device-side OHEM, BCE+Dice), the KD term and the fused fp16 GradScaler are
-        # capture-safe; the eager teacher fallback is not
+        # capture-safe; the eager teacher fallback is not.  A step that issues torch.distributed
+        # collectives (gradient buckets, SyncBN over RCCL) is never captured: the process group's watchdog
+        # polls the events of its works, and events recorded inside a capture abort it
+        # (hipErrorCapturedEvent).  At world size 1 no collective is attached, so the step is captured.
         kd_ok = not config.kd_training or isinstance(self.teacher_model, FusedModel)
-        return (self.fused and config.use_graph and kd_ok and not config.use_aux
-                and (not config.DDP or config.gpu_num == 1 or config.graph_ddp))
+        collectives = getattr(self.optimizer, 'bucketer', None) is not None or \
+            (config.DDP and config.gpu_num > 1)
+        return self.fused and config.use_graph and kd_ok and not config.use_aux and not collectives
 
     def step_engine(self, config):
         """The fused engine's device step (:class:`runtime.trainer_engine.StepEngine`) -- the same object
@@ -104,6 +108,10 @@ class SegTrainer(BaseTrainer):
                                      teacher=self.teacher_model if config.kd_training else None, kd_fn=kd_fn,
                                      kd_coef=config.kd_loss_coefficient, use_graph=self._use_graph(config),
                                      warmup=config.graph_warmup)
+            if self.main_rank and self.logger:
+                self.logger.info(f'step engine: hipGraph capture {"on" if self.engine.use_graph else "off"} '
+                                 f'(world {config.gpu_num if config.DDP else 1}, gradient bucketer '
+                                 f'{"on" if getattr(self.optimizer, "bucketer", None) is not None else "off"})')
         return self.engine
 
     def train_step(self, images, masks):
@@ -116,7 +124,7 @@ class SegTrainer(BaseTrainer):
         engine = self.step_engine(config)
         if engine is not None:
             loss = iteration(engine, self.scheduler, self.ema_model, self.train_itrs, images, masks)
-            self._last_kd = engine.kd.clone() if engine.kd is not None else None
+            self._last_kd = engine.last_kd.clone() if engine.last_kd is not None else None
             return loss
         loss = self.eager_step(images, masks)
         self.scheduler.step()

@@ -207,6 +207,12 @@ def dwconv(x, conv: torch.nn.Conv2d):
     """Depthwise ``conv`` (groups == in == out channels, stride 1) on an NHWC bf16 map."""
     kh, kw = conv.kernel_size
     assert conv.groups == conv.in_channels == conv.out_channels and tuple(conv.stride) == (1, 1)
+    # the kernel writes a 'same'-sized map (y = empty_like(x)): any other padding would be silently
+    # shifted / cropped, so it is refused here
+    (ph, pw), (dh, dw) = tuple(conv.padding), tuple(conv.dilation)
+    if 2 * ph != dh * (kh - 1) or 2 * pw != dw * (kw - 1):
+        raise ValueError(f'dwconv: only same-size depthwise convs are fused (kernel {kh}x{kw}, padding '
+                         f'{(ph, pw)}, dilation {(dh, dw)})')
     return _DwConv.apply(x, conv.weight, conv.bias, kh, kw, tuple(conv.padding), tuple(conv.dilation))
 
 

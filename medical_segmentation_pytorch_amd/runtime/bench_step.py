@@ -93,7 +93,8 @@ def build_eager_step(batch, size, base_channel, device, channels_last=False, dis
 
 
 def bench_config(model_name, base_channel, batch, size, lr, total_steps, train_images, val_images, save_dir,
-                 device_index=None, teacher_name=None, use_graph=True, dist_backend=None, world=1):
+                 device_index=None, teacher_name=None, use_graph=True, dist_backend=None, world=1,
+                 dist_world1_bucketer=False):
     """The MyConfig a bench / tool run trains with: reference defaults (adam, CE, OneCycle 'cos_warmup',
     MyConfig augmentation, use_ema False) on a synthetic polyp split of ``train_images``/``val_images``
     images at ``size``, one OneCycle over ``total_steps`` iterations, lr = ``lr`` per GPU
@@ -125,6 +126,7 @@ def bench_config(model_name, base_channel, batch, size, lr, total_steps, train_i
     cfg.device_index = device_index
     cfg.dist_backend = dist_backend
     cfg.use_graph = use_graph
+    cfg.bucketer_world1 = dist_world1_bucketer
     cfg.graph_warmup = 1
     cfg.use_tb = False
     cfg.progress_bar = False
@@ -172,11 +174,22 @@ class TrainerStep:
         self.trainer.config_ref = cfg
         self.trainer.model.train()
         self.loader = self.trainer.train_loader
-        self.order = self.loader.stream()
+        # the GPU run draws from the HBM-resident DeviceAugLoader; without a GPU (the CPU rehearsal of the
+        # bench contract) the trainer's host DataLoader is cycled epoch after epoch
+        self.order = self.loader.stream() if hasattr(self.loader, 'stream') else self._host_batches()
         self.bucketer = getattr(self.trainer.optimizer, 'bucketer', None)
         self.images = self.masks = None
         self.fixed = fixed   # replay the first batch (isolates the model step from the data pipeline)
         self._drawn = False
+
+    def _host_batches(self):
+        epoch = 0
+        while True:
+            if hasattr(self.loader.sampler, 'set_epoch'):
+                self.loader.sampler.set_epoch(epoch)
+            for images, masks in self.loader:
+                yield images, masks
+            epoch += 1
 
     @property
     def ema_model(self):
@@ -187,6 +200,10 @@ class TrainerStep:
         return self.trainer.engine
 
     def __call__(self):
+        if not hasattr(self.loader, 'stream'):   # host loader (CPU rehearsal)
+            images, masks = next(self.order)
+            dev = self.trainer.device
+            return self.trainer.train_step(images.to(dev, torch.float32), masks.to(dev))
         eng = self.trainer.engine
         if eng is not None and eng.images is not None:   # the loader writes into the graph inputs
             out = (eng.images, eng.masks)

@@ -100,43 +100,54 @@ def stat_group(group):
     return group
 
 
+class _Bucket:
+    """One all-reduce unit: ``members`` (arena parameter indices, in the order their gradients land).
+    ``span`` = (lo, hi) when the members tile one contiguous arena slice (the all-reduce runs in place);
+    otherwise the bucket is *packed*: its gradients are gathered into a staging slice (one multi-tensor
+    copy), all-reduced there and scattered back in ``finish``."""
+
+    def __init__(self, arena, members):
+        self.members = list(members)
+        self.set = set(self.members)
+        self.numel = sum(arena.params[i].numel() for i in self.members)
+        lo = min(arena.offsets[i] for i in self.members)
+        hi = max(arena.offsets[i] + arena.params[i].numel() for i in self.members)
+        inside = {i for i, o in enumerate(arena.offsets) if lo <= o < hi}
+        self.span = (lo, hi) if inside == self.set else None
+        self.stage = None   # (lo, hi) in the staging buffer of a packed bucket
+
+
 class GradBucketer:
-    """DDP-equivalent gradient averaging over RCCL: buckets are contiguous slices of the grad arena
-    in REVERSE parameter order (backward produces the last layers first); a bucket is all-reduced
-    as soon as all of its parameters reported ready (SUM; the 1/world factor is folded into the
-    optimizer's grad scale).
+    """DDP-equivalent gradient averaging over RCCL: a bucket is all-reduced as soon as all of its
+    parameters reported ready (SUM; the 1/world factor is folded into the optimizer's grad scale).
+
+    Bucket order: the first step's buckets follow reverse registration order (backward produces the
+    last layers first -- torch DDP's initial guess) as contiguous slices of the grad arena.  During that
+    step every gradient's arrival is recorded (``ready_order``); at its ``finish`` rank 0's observed
+    order is broadcast and the buckets are REBUILT in that order (torch DDP's rebuild-after-first-
+    iteration), so every bucket's gradients land together and it leaves as early as possible.  A rebuilt
+    bucket whose members are not one contiguous arena slice is packed through a staging buffer.
 
     ``compress='bf16'`` (config ``grad_compress``; torch DDP's ``bf16_compress_hook``): a ready bucket
-    is rounded into a persistent bf16 shadow of the arena, all-reduced at half the xGMI bytes, and
-    widened back into the fp32 arena in :meth:`finish`."""
+    is rounded into a persistent bf16 shadow, all-reduced at half the xGMI bytes, and widened back into
+    the fp32 arena in :meth:`finish`."""
 
-    def __init__(self, arena: Arena, group=None, bucket_cap_mb=64.0, first_bucket_mb=4.0, compress=None):
+    def __init__(self, arena: Arena, group=None, bucket_cap_mb=64.0, first_bucket_mb=4.0, compress=None,
+                 rebuild=True):
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group)
         if compress not in (None, 'bf16'):
             raise ValueError(f'grad_compress must be None or "bf16", got {compress!r}')
+        self.compress = compress
+        self.cap_mb, self.first_mb = bucket_cap_mb, first_bucket_mb
         self.shadow = torch.empty(arena.numel, dtype=torch.bfloat16, device=arena.grad.device) \
             if compress == 'bf16' else None
-        idx = list(range(len(arena.params)))[::-1]
-        buckets, cur, cur_bytes, cap = [], [], 0, first_bucket_mb * 2 ** 20
-        for i in idx:
-            cur.append(i)
-            cur_bytes += arena.params[i].numel() * 4
-            if cur_bytes >= cap:
-                buckets.append(cur)
-                cur, cur_bytes, cap = [], 0, bucket_cap_mb * 2 ** 20
-        if cur:
-            buckets.append(cur)
-        self.buckets = []
-        self.owner = {}
-        for b, members in enumerate(buckets):
-            lo = min(arena.offsets[i] for i in members)
-            hi = max(arena.offsets[i] + arena.params[i].numel() for i in members)
-            self.buckets.append((lo, hi, set(members)))
-            for i in members:
-                self.owner[i] = b
+        self.stage = None
         self.pidx = arena.param_index()
+        self._assign(list(range(len(arena.params)))[::-1])
+        self.rebuild_pending = rebuild
+        self.rebuilt = False
         # evidence knobs (bench.py's multi-GPU pass): enabled=False skips the all-reduces (timing probe);
         # instrument=True records, per bucket, an event at issue time and the RCCL work (its on-stream
         # duration needs TORCH_NCCL_ENABLE_TIMING=1), read back by collect() after the step
@@ -146,8 +157,55 @@ class GradBucketer:
         self.ready_order = []   # parameter indices in the order their gradients landed (first step)
         self.reset()
 
+    def _assign(self, order):
+        """Cut ``order`` into buckets (first one small: it leaves early; then ``cap_mb`` each)."""
+        a = self.arena
+        groups, cur, cur_bytes, cap = [], [], 0, self.first_mb * 2 ** 20
+        for i in order:
+            cur.append(i)
+            cur_bytes += a.params[i].numel() * 4
+            if cur_bytes >= cap:
+                groups.append(cur)
+                cur, cur_bytes, cap = [], 0, self.cap_mb * 2 ** 20
+        if cur:
+            groups.append(cur)
+        self.buckets = [_Bucket(a, g) for g in groups]
+        self.owner = {i: b for b, bk in enumerate(self.buckets) for i in bk.members}
+        n, dev = 0, a.grad.device
+        for bk in self.buckets:
+            if bk.span is None:
+                bk.stage = (n, n + bk.numel)
+                n += bk.numel
+        dtype = torch.bfloat16 if self.compress == 'bf16' else torch.float32
+        self.stage = torch.empty(n, dtype=dtype, device=dev) if n else None
+        for bk in self.buckets:
+            if bk.span is None:
+                lo = bk.stage[0]
+                bk.grads = [a.params[i].grad.view(-1) for i in bk.members]
+                bk.views = []
+                for g in bk.grads:
+                    bk.views.append(self.stage[lo:lo + g.numel()])
+                    lo += g.numel()
+
+    def rebuild(self):
+        """Re-bucket along the grad-ready order observed in the first step (identical on every rank:
+        rank 0's order is broadcast).  Parameters that never reported come last."""
+        n = len(self.arena.params)
+        seen = set(self.ready_order)
+        order = list(dict.fromkeys(self.ready_order)) + [i for i in range(n - 1, -1, -1) if i not in seen]
+        t = torch.tensor(order, dtype=torch.int64, device=self.arena.grad.device)
+        if self.world > 1:
+            dist.broadcast(t, dist.get_global_rank(self.group, 0) if self.group is not None and
+                           self.group is not dist.group.WORLD else 0, group=self.group)
+        self._assign(t.cpu().tolist())
+        self.rebuilt = True
+
+    def bucket_order(self):
+        """Parameter indices in bucket order (bucket 0's members first)."""
+        return [i for bk in self.buckets for i in bk.members]
+
     def reset(self):
-        self.pending = [set(m) for _, _, m in self.buckets]
+        self.pending = [set(bk.set) for bk in self.buckets]
         self.works = []
         self.launched = [False] * len(self.buckets)
         self.launch_order = []
@@ -165,13 +223,18 @@ class GradBucketer:
                 self._launch(b)
 
     def _launch(self, b, late=False):
-        lo, hi, _ = self.buckets[b]
+        bk = self.buckets[b]
         self.launched[b] = True
         self.launch_order.append((b, late))
-        buf = self.arena.grad[lo:hi]
-        if self.shadow is not None:
-            buf = self.shadow[lo:hi]
-            buf.copy_(self.arena.grad[lo:hi])
+        if bk.span is not None:
+            lo, hi = bk.span
+            buf = self.arena.grad[lo:hi]
+            if self.shadow is not None:
+                buf = self.shadow[lo:hi]
+                buf.copy_(self.arena.grad[lo:hi])
+        else:   # packed: gather the members' gradients into the staging slice (one multi-tensor copy)
+            torch._foreach_copy_(bk.views, bk.grads)
+            buf = self.stage[bk.stage[0]:bk.stage[1]]
         ev = None
         if self.instrument:
             ev = torch.cuda.Event(enable_timing=True)
@@ -192,12 +255,19 @@ class GradBucketer:
         for b, w, ev in self.works:
             if w is not None:
                 w.wait()
-            if self.shadow is not None:
-                lo, hi, _ = self.buckets[b]
+            bk = self.buckets[b]
+            if bk.span is None:
+                torch._foreach_copy_(bk.grads, bk.views)
+            elif self.shadow is not None:
+                lo, hi = bk.span
                 self.arena.grad[lo:hi].copy_(self.shadow[lo:hi])
         if self.instrument:
             self.records.append((list(self.works), end, list(self.launch_order)))
         self.reset()
+        if self.rebuild_pending:   # after the first step: re-bucket in the observed grad-ready order
+            self.rebuild_pending = False
+            self.rebuild()
+            self.reset()
 
     def collect(self):
         """Per-bucket evidence of the instrumented steps (host-syncs; call after the timed region):
@@ -208,14 +278,15 @@ class GradBucketer:
         for works, end, order in self.records:
             late = {b: lt for b, lt in order}
             for b, w, ev in works:
-                lo, hi, _ = self.buckets[b]
+                bk = self.buckets[b]
                 dur = None
                 if w is not None:
                     try:
                         dur = float(w._get_duration())
                     except Exception:
                         dur = None
-                out.append({'bucket': b, 'mib': round((hi - lo) * 4 / 2 ** 20, 2), 'rccl_ms': dur,
+                out.append({'bucket': b, 'mib': round(bk.numel * 4 / 2 ** 20, 2), 'packed': bk.span is None,
+                            'rccl_ms': dur,
                             'issue_to_bwd_end_ms': round(ev.elapsed_time(end), 3) if ev is not None and end is not None
                             else None, 'late': bool(late.get(b, False))})
         self.records = []

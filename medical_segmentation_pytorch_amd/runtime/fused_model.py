@@ -504,10 +504,11 @@ class FusedExecutor(SmpDecoders):
         return feats
 
     def smp_hybrid(self, model, images, training):
-        """smp decoders without a fused implementation (PAN, MAnet; any decoder with MSP_FUSED_DECODERS=0)
-        over a ResNet encoder: the encoder -- the bulk of the FLOPs -- runs on the fused kernels, the decoder
-        and head eagerly under bf16 autocast on the NCHW features (reference ``models/__init__.py:8-10,23-25``).
-        Unet++ / Linknet / FPN / DeepLabV3(+) / PSPNet run fully fused (``runtime.fused_decoders``)."""
+        """smp decoders over a ResNet encoder with the decoder run eagerly (only with MSP_FUSED_DECODERS=0:
+        every decoder of the hub -- Unet++, Linknet, FPN, DeepLabV3(+), PSPNet, PAN, MAnet -- has a fused
+        implementation in ``runtime.fused_decoders``): the encoder -- the bulk of the FLOPs -- runs on the
+        fused kernels, the decoder and head eagerly under bf16 autocast on the NCHW features (reference
+        ``models/__init__.py:8-10,23-25``)."""
         enc = model.encoder
         feats = self.resnet_encoder(enc, images, training)
         chans = list(enc.out_channels[1:])

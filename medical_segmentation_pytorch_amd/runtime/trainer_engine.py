@@ -42,6 +42,7 @@ class StepEngine:
         self.images, self.masks = static if static is not None else (None, None)
         self.graph = None
         self.loss = self.kd = None
+        self.last_kd = None    # KD term of the latest step (the graph's static output or a ragged eager step)
         self.calls = 0
         self._nbt_inc = None   # 0/1 per arena BN counter: BNs the executor runs (one add per step)
 
@@ -98,9 +99,12 @@ class StepEngine:
             self.images, self.masks = torch.empty_like(images), torch.empty_like(masks)
         if images is not None and images is not self.images:
             if images.shape != self.images.shape or masks.shape != self.masks.shape:
-                self.optimizer.prepare()     # ragged batch: not capturable, run eagerly
-                self.loss, self.kd = self.body(images, masks)
-                return self.loss
+                # ragged batch: not capturable, run eagerly.  Its loss / KD term are returned through
+                # last_kd, never stored over self.loss / self.kd: those are the captured graph's static
+                # outputs, which every later replay refreshes
+                self.optimizer.prepare()
+                loss, self.last_kd = self.body(images, masks)
+                return loss
             self.images.copy_(images, non_blocking=True)
             self.masks.copy_(masks, non_blocking=True)
         self.optimizer.prepare()
@@ -116,6 +120,7 @@ class StepEngine:
                 self.loss, self.kd = self.body(self.images, self.masks)
             if ex.pack_program is None and (not self.use_graph or self.calls == self.warmup):
                 ex.build_pack_program(self.images.device)
+            self.last_kd = self.kd
             return self.loss
         if self.graph is None:
             torch.cuda.synchronize()
@@ -123,6 +128,7 @@ class StepEngine:
             with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
                 self.loss, self.kd = self.body(self.images, self.masks)
         self.graph.replay()
+        self.last_kd = self.kd
         return self.loss
 
 
@@ -214,8 +220,8 @@ def no_gc():
 
 def capture_mode():
     """hipGraph capture error mode: 'thread_local' under torch.distributed -- the process group's
-    watchdog thread polls its work events while the step is being captured, which the default
-    'global' mode turns into a capture error and a SIGABRT (seen intermittently with --graph-ddp)."""
+    watchdog thread polls its (uncaptured) work events while a world-size-1 step is being captured, which
+    the default 'global' mode turns into a capture error."""
     return 'thread_local' if dist.is_available() and dist.is_initialized() else 'global'
 
 

@@ -45,6 +45,55 @@ def worker_count(env=None):
     return n if n > 1 else 0
 
 
+def spawn_ranks(n, argv, extra_env=None, poll_s=0.2, grace_s=20.0):
+    """Start ``n`` rank processes of ``[python] + argv`` with the torchrun environment (127.0.0.1
+    rendezvous, one rank per local GPU) and supervise them the way torchrun does: all handles are
+    polled, and the first rank that exits non-zero tears the others down (SIGTERM, then SIGKILL after
+    ``grace_s``), so a dead rank never leaves its peers blocked in a collective until the process-group
+    timeout.  Must be called before this process touches a GPU (the children are fresh interpreters).
+    Returns the job's exit code (0, or the first failing rank's code)."""
+    import signal
+    import time
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), **(extra_env or {}))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f'[launch] rank {r} exited with {code}; stopping the other ranks', file=sys.stderr,
+                          flush=True)
+                    for q in live:
+                        procs[q].send_signal(signal.SIGTERM)
+                    deadline = time.monotonic() + grace_s
+                    for q in sorted(live):
+                        try:
+                            procs[q].wait(timeout=max(deadline - time.monotonic(), 0.1))
+                        except subprocess.TimeoutExpired:
+                            procs[q].kill()
+                            procs[q].wait()
+                    live.clear()
+                    break
+            if live:
+                time.sleep(poll_s)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        rc = 130
+    return rc
+
+
 def maybe_spawn_workers(argv=None):
     """In the launcher-less multi-GPU case start one worker per GPU (this same script and arguments,
     with the torchrun environment) and exit with the workers' status; otherwise return."""
@@ -52,21 +101,7 @@ def maybe_spawn_workers(argv=None):
     if n == 0:
         return
     argv = list(sys.argv if argv is None else argv)
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), **{DP_ENV: '1'})
-        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
-    rc = 0
-    try:
-        for p in procs:
-            rc = max(rc, p.wait())
-    except KeyboardInterrupt:
-        for p in procs:
-            p.terminate()
-        rc = 130
-    sys.exit(rc)
+    sys.exit(spawn_ranks(n, argv, {DP_ENV: '1'}))
 
 
 def apply_dp_semantics(config):

@@ -109,7 +109,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
         group = get_group(config) if config.DDP else None
         arena = getattr(optimizer, 'arena', None)
         bucketer = None
-        if group is not None and arena is not None:   # (world 1 too: the RCCL path stays exercised)
+        if group is not None and arena is not None and (dist.get_world_size(group) > 1 or
+                                                        getattr(config, 'bucketer_world1', False)):
             from ..runtime.engine import GradBucketer
             bucketer = GradBucketer(arena, group, config.bucket_cap_mb,
                                     compress=getattr(config, 'grad_compress', None))

@@ -41,6 +41,52 @@ def _bucketer_worker(rank, world, port, q, compress=None):
     dist.destroy_process_group()
 
 
+def _rebuild_worker(rank, world, port, q, compress=None):
+    """Gradients land in a scrambled (non-registration) order; step 1 uses the initial reverse-registration
+    buckets, then the bucketer re-buckets along the observed order; step 2 must still sum exactly and every
+    bucket must launch right when its last gradient lands (never deferred to finish())."""
+    _init(rank, world, port)
+    import random
+    from medical_segmentation_pytorch_amd.runtime.engine import Arena, GradBucketer
+    torch.manual_seed(0)
+    model = nn.Sequential(*[nn.Linear(64, 64) for _ in range(6)])
+    arena = Arena(model, torch.device('cpu'))
+    b = GradBucketer(arena, None, bucket_cap_mb=0.03, first_bucket_mb=0.02, compress=compress)
+    n = len(arena.params)
+    order = list(range(n))
+    random.Random(5).shuffle(order)   # same on every rank (as the executor's backward order is)
+    before = [list(bk.members) for bk in b.buckets]
+    res = []
+    for step in range(2):
+        for i, p in enumerate(arena.params):
+            p.grad.fill_(float(rank + 1) * (i + 1) + step)
+        launched_at = []
+        for k, i in enumerate(order):
+            b.ready([arena.params[i]])
+            launched_at.append(len(b.launch_order))
+        late = [lt for _, lt in b.launch_order]
+        b.finish()
+        ok = all(torch.allclose(p.grad, torch.full_like(p.grad, 3.0 * (i + 1) + 2 * step))
+                 for i, p in enumerate(arena.params))
+        res.append((ok, any(late)))
+    q.put((rank, res, before, [list(bk.members) for bk in b.buckets], order, b.bucket_order(),
+           [bk.span is None for bk in b.buckets]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('compress', [None, 'bf16'])
+def test_grad_bucketer_rebuilds_in_ready_order(compress):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    mp.spawn(_rebuild_worker, args=(2, _port(), q, compress), nprocs=2, join=True)
+    for rank, res, before, after, order, border, packed in [q.get() for _ in range(2)]:
+        assert all(ok for ok, _ in res), res
+        assert before != after and len(after) > 1
+        assert border == order                     # buckets follow the observed grad-ready order
+        assert res[1][1] is False                  # after the rebuild no bucket waits for finish()
+        assert any(packed)                         # scrambled order: some buckets go through the staging buffer
+
+
 @pytest.mark.parametrize('compress', [None, 'bf16'])
 def test_grad_bucketer_allreduce(compress):
     """Bucketed all-reduce (SUM) of the grad arena; values 1*(i+1) + 2*(i+1) are exact in bf16 too."""
@@ -141,3 +187,53 @@ def test_main_spawns_dataparallel_workers(tmp_path):
     assert cfg['synBN'] is False          # DataParallel: per-replica BatchNorm statistics
     assert abs(cfg['lr'] - cfg['base_lr'] * 0.1 * 2) < 1e-12   # adam: 0.1 * base_lr * gpu_num
     assert os.path.isfile(tmp_path / 'save' / 'last.pth')
+
+
+@pytest.mark.slow
+def test_bench_self_launches_ranks(tmp_path):
+    """``python bench.py --gpus 2`` WITHOUT torchrun starts 2 ranks itself (before any GPU call) and the
+    JSON line is the 2-rank job's: n_gpus 2, dp2, the evidence pass sees a 2-rank process group.  Without a
+    GPU the contract runs on the CPU over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('LOCAL_RANK', 'RANK', 'WORLD_SIZE', 'MASTER_PORT')}
+    env.update(OMP_NUM_THREADS='2', BENCH_SAVE_DIR=str(tmp_path / 'save'))
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '2', '--warmup', '1',
+           '--batch', '2', '--size', '64', '--model', 'unet', '--base-channel', '8', '--train-images', '8',
+           '--val-images', '2', '--comm-steps', '1']
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'dp2' and d['config']['global_batch'] == 4
+    assert d['comm']['world_size'] == 2 and d['value'] > 0
+
+
+def test_bench_refuses_mismatched_world(tmp_path):
+    """A rank whose process group does not have --gpus ranks exits non-zero instead of benching a
+    different job size."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(_port()))
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '1', '--warmup', '0']
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and 'job has 1 rank' in out.stderr, out.stderr[-2000:]
+
+
+def test_spawn_ranks_tears_down_on_failure(tmp_path):
+    """The launcher-less supervisor (bench / main.py DP mode) stops the surviving ranks as soon as one rank
+    fails instead of waiting on rank 0 forever (torchrun semantics)."""
+    import time
+    from medical_segmentation_pytorch_amd.utils.launch import spawn_ranks
+    script = tmp_path / 'r.py'
+    script.write_text('import os, sys, time\n'
+                      'if os.environ["RANK"] == "1":\n    sys.exit(7)\n'
+                      'time.sleep(120)\n')
+    t0 = time.monotonic()
+    rc = spawn_ranks(3, [str(script)], grace_s=5.0)
+    assert rc == 7 and time.monotonic() - t0 < 60

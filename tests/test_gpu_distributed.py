@@ -135,30 +135,44 @@ def test_bench_ddp_path_two_ranks(gpu, tmp_path):
     assert c['step_ms_comm_off'] > 0 and c['instrumented_step_ms'] > 0
 
 
-@pytest.mark.parametrize('graph', [False, pytest.param(True, marks=pytest.mark.xfail(
-    reason='opt-in --graph-ddp: with the trainer-built step the process-group watchdog queries an event of '
-           'a collective recorded inside the hipGraph capture (hipErrorCapturedEvent, SIGABRT) on this ROCm '
-           '7 / torch 2.10 stack; the default multi-GPU path (uncaptured RCCL) is the graph=False case',
-    strict=False))])
-def test_bench_rccl_path_world1(gpu, tmp_path, graph):
+def test_bench_rccl_path_world1(gpu, tmp_path):
     """The RCCL code path on the real backend: one rank over `nccl` (RCCL) with --ddp, so the process
-    group, the bucketed gradient all-reduce of the arena and the step's RCCL calls all run on the GPU
-    (one device -> world size 1; more ranks are the driver's 8-GPU runs).  graph=True also captures
-    the RCCL all-reduces inside the hipGraph (the opt-in --graph-ddp mode)."""
+    group, the bucketed gradient all-reduce of the arena (rebuilt in grad-ready order after step 1) and the
+    step's RCCL calls all run on the GPU (one device -> world size 1; more ranks are the driver's 8-GPU
+    runs).  A step with collectives is never graph-captured."""
     import json
     s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
            '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '1', '--ddp',
            '--steps', '3', '--warmup', '2', '--batch', '4', '--size', '64', '--train-images', '8',
-           '--val-images', '4'] + (['--graph-ddp'] if graph else [])
+           '--val-images', '4']
     r = subprocess.run(cmd, env=dict(os.environ), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     errs = [ln for ln in r.stderr.splitlines() if 'rror' in ln or 'what()' in ln or 'Exception' in ln][:20]
     assert r.returncode == 0, '\n'.join(errs) + '\n...\n' + r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert len(line) == 1, r.stdout
     d = json.loads(line[0])
-    assert d['n_gpus'] == 1 and d['value'] > 0 and d['config']['hipgraph'] == graph
-    if not graph:   # RCCL on-stream durations of every gradient bucket (TORCH_NCCL_ENABLE_TIMING)
-        c = d['comm']
-        assert c['world_size'] == 1 and c['rccl_version'] and c['buckets']
-        assert all(b['rccl_ms'] is not None and b['rccl_ms'] >= 0 for b in c['buckets']), c['buckets']
+    assert d['n_gpus'] == 1 and d['value'] > 0 and d['config']['hipgraph'] is False
+    c = d['comm']   # RCCL on-stream durations of every gradient bucket (TORCH_NCCL_ENABLE_TIMING)
+    assert c['world_size'] == 1 and c['rccl_version'] and c['buckets']
+    assert all(b['rccl_ms'] is not None and b['rccl_ms'] >= 0 for b in c['buckets']), c['buckets']
+    assert c['buckets_rebuilt_in_ready_order'], c
+
+
+def test_main_torchrun_world1_graph(gpu, tmp_path):
+    """``torchrun --nproc_per_node=1 main.py`` on the fused engine: world size 1 attaches no collective, so
+    the step IS graph-captured (use_graph on) and the run exits cleanly (round-3 advisor: a world-1
+    bucketer inside the capture aborted in the process-group watchdog)."""
+    s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'main.py'), '--dataset', 'synthetic',
+           '--synthetic_num', '16', '4', '4', '--synthetic_size', '64', '--crop_size', '64', '--total_epoch', '2',
+           '--warmup_epochs', '0', '--train_bs', '4', '--val_bs', '4', '--base_workers', '0', '--model', 'ducknet',
+           '--base_channel', '8', '--no_progress_bar', '--save_dir', str(tmp_path / 'save'),
+           '--data_root', str(tmp_path / 'data'), '--graph_warmup', '1']
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    log = open(tmp_path / 'save' / 'seg_trainer.log').read()
+    assert 'hipGraph capture on' in log and 'gradient bucketer off' in log, log[-2000:]
+    assert os.path.isfile(tmp_path / 'save' / 'last.pth')
