@@ -150,13 +150,15 @@ def comm_evidence(step, args, dist, step_ms, device):
     sync()
     out['instrumented_step_ms'] = round((time.perf_counter() - t0) / n * 1e3, 3)
     out['syncbn_exchanges_per_step'] = (bnmod.EXCHANGES[0] - ex0) / n
+    from medical_segmentation_pytorch_amd.runtime import comm as ipc_comm
+    out['syncbn_exchange_path'] = ipc_comm.describe()
     durs = []
     for _, w in bnmod.COMM['works']:
         try:
             durs.append(float(w._get_duration()))
         except Exception:
             pass
-    out['syncbn_rccl_ms_per_step'] = round(sum(durs) / n, 3) if durs else None
+    out['syncbn_exchange_ms_per_step'] = round(sum(durs) / n, 3) if durs else None
     out['syncbn_bytes_per_step'] = sum(b for b, _ in bnmod.COMM['works']) / n
     bnmod.COMM['instrument'] = False
     bnmod.COMM['works'] = []

@@ -737,6 +737,48 @@ void colsum_t(const at::Tensor& part, const at::Tensor& out, bool accum) {
   TORCH_CHECK(part.numel() % ncol == 0, "colsum: part [nrow][ncol]");
   colsum(f32(part), part.numel() / ncol, ncol, f32(out), accum ? 1 : 0, cur_stream());
 }
+// ---- comm.hip: IPC peer-memory all-reduce -------------------------------------------------------
+py::tuple comm_alloc_t(int64_t bytes) {
+  void* p = nullptr;
+  char h[kCommHandleBytes] = {0};
+  const int rc = comm_alloc(bytes, &p, h);
+  TORCH_CHECK(rc == 0, "comm_alloc: uncached allocation / IPC export failed (step ", rc, ")");
+  return py::make_tuple(reinterpret_cast<int64_t>(p), py::bytes(h, kCommHandleBytes));
+}
+
+int64_t comm_open_t(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == kCommHandleBytes, "comm_open: bad IPC handle");
+  void* p = nullptr;
+  TORCH_CHECK(comm_open(h.data(), &p) == 0, "comm_open: hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+// in/out: fp64 rows (out may alias in); peers: every rank's mapped exchange buffer (own one included);
+// epoch: int64 device counter (advanced by the kernel); err: int32 device error counter
+void comm_allreduce_t(const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& peers, int64_t rank,
+                      int64_t cap, const at::Tensor& epoch, const at::Tensor& err, double timeout_s) {
+  CHECK_DEV(in); CHECK_DEV(out); CHECK_I64(epoch); CHECK_DEV(err);
+  TORCH_CHECK(in.scalar_type() == at::kDouble && out.scalar_type() == at::kDouble, "comm_allreduce: fp64 rows");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1 && epoch.numel() >= 1, "comm_allreduce: state");
+  const int world = (int)peers.size();
+  TORCH_CHECK(world >= 1 && world <= kCommMaxRanks && rank >= 0 && rank < world, "comm_allreduce: bad rank/world");
+  TORCH_CHECK(in.numel() == out.numel() && in.numel() <= cap, "comm_allreduce: ", in.numel(),
+              " values exceed the exchange capacity ", cap);
+  CommPeers pt{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(peers[i] != 0, "comm_allreduce: unmapped peer buffer");
+    pt.buf[i] = reinterpret_cast<char*>(peers[i]);
+  }
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  const long long ticks = (long long)(timeout_s * (khz > 0 ? khz : 100000) * 1000.0);
+  oneshot_allreduce(in.data_ptr<double>(), out.data_ptr<double>(), in.numel(), pt, (int)rank, world, cap,
+                    reinterpret_cast<unsigned long long*>(epoch.data_ptr<int64_t>()), err.data_ptr<int>(), ticks,
+                    cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -843,4 +885,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_wgrad_blocks", &dwconv_wgrad_blocks_t);
   m.def("dwconv_wgrad", &dwconv_wgrad_t);
   m.def("colsum", &colsum_t);
+  m.def("comm_buffer_bytes", &comm_buffer_bytes);
+  m.def("comm_alloc", &comm_alloc_t);
+  m.def("comm_open", &comm_open_t);
+  m.def("comm_close", [](int64_t p) { comm_close(reinterpret_cast<void*>(p)); });
+  m.def("comm_free", [](int64_t p) { comm_free(reinterpret_cast<void*>(p)); });
+  m.def("comm_allreduce", &comm_allreduce_t);
+  m.def("comm_max_ranks", []() { return kCommMaxRanks; });
 }

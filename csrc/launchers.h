@@ -241,3 +241,18 @@ int dwconv_wgrad_blocks(long P, int Cp);
 int dwconv_wgrad(const uint16_t* x, const uint16_t* dyv, float* part, int nblk, int N, int H, int W, int Cp, int T,
                  const int* dy, const int* dx, hipStream_t s);
 void colsum(const float* part, int nrow, int ncol, float* out, int accum, hipStream_t s);
+
+// comm.hip: one-shot intra-node all-reduce over IPC-mapped peer buffers (SyncBN statistic exchanges)
+constexpr int kCommMaxRanks = 16;
+constexpr long kCommDataOff = 4096;       // flags first, then data[2][world][cap] fp64
+constexpr int kCommHandleBytes = 64;
+struct CommPeers {
+  char* buf[kCommMaxRanks];               // every rank's exchange buffer, mapped in this process
+};
+long comm_buffer_bytes(long cap, int world);
+int comm_alloc(long bytes, void** ptr, void* handle64);
+int comm_open(const void* handle64, void** ptr);
+void comm_close(void* ptr);
+void comm_free(void* ptr);
+void oneshot_allreduce(const double* in, double* out, long n, const CommPeers& peers, int rank, int world, long cap,
+                       unsigned long long* epoch, int* err, long long timeout, hipStream_t s);

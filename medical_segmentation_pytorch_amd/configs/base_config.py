@@ -123,6 +123,8 @@ class BaseConfig:
                                           # kernels; 1.8x the NCHW step on MI355X, profiles/r02/eager_sweep)
         self.bucket_cap_mb = 64        # gradient bucket size for the RCCL all-reduce
         self.grad_compress = None      # None | 'bf16' all-reduce compression
+        self.syncbn_comm = 'auto'      # SyncBN statistic exchange: 'auto' (IPC peer-memory kernel on one node,
+                                       # RCCL otherwise) | 'ipc' | 'rccl'  (env MSP_SYNCBN_COMM overrides)
         self.gpu_augment = True        # run augmentation on the GPU over an HBM-resident dataset
         self.dist_backend = None       # None -> 'nccl' (RCCL) on GPU, 'gloo' on CPU
         self.log_interval = 50         # device-side loss accumulation, host sync every N iters

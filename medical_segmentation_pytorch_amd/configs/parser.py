@@ -114,6 +114,7 @@ def get_parser():
     _flag(p, 'synthetic_num', type=int, nargs=3)
     _flag(p, 'synthetic_size', type=int)
     _flag(p, 'bucketer_world1', action='store_true')
+    _flag(p, 'syncbn_comm', type=str, choices=['auto', 'ipc', 'rccl'])
     _flag(p, 'val_fp32', action='store_true')
     _flag(p, 'gpu_augment', action='store_false')
     _flag(p, 'trace', action='store_true')

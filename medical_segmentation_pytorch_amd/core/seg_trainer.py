@@ -135,6 +135,9 @@ class SegTrainer(BaseTrainer):
         if not self._loss_hist:
             return
         vals = torch.stack([v for _, v, _ in self._loss_hist]).float().cpu().tolist()
+        if config.DDP:
+            from ..runtime import comm as ipc_comm
+            ipc_comm.check()   # a timed-out peer-memory exchange poisons the step with NaN: name the cause
         check_finite(vals, self._loss_hist[-1][0])
         kds = [k for _, _, k in self._loss_hist]
         kdv = torch.stack(kds).float().cpu().tolist() if all(k is not None for k in kds) else None

@@ -171,10 +171,34 @@ EXCHANGES = [0]   # SyncBN collectives issued by this process (tests count them)
 COMM = {'enabled': True, 'instrument': False, 'works': []}
 
 
+class _EventSpan:
+    """Duration of one IPC exchange kernel (the ``Work._get_duration`` shape of an RCCL work)."""
+    __slots__ = ('a', 'b')
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    def _get_duration(self):
+        return self.a.elapsed_time(self.b)
+
+
 def _exchange(buf, group):
-    """One SyncBN statistic all-reduce (SUM, in place)."""
+    """One SyncBN statistic all-reduce (SUM, in place): the IPC peer-memory kernel when the group has
+    one (``runtime.comm``), RCCL otherwise."""
     EXCHANGES[0] += 1
     if not COMM['enabled']:
+        return
+    from ..runtime import comm as ipc
+    c = ipc.lookup(group)
+    if c is not None and c.fits(buf):
+        if COMM['instrument']:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            c.all_reduce(buf)
+            b.record()
+            COMM['works'].append((buf.numel() * buf.element_size(), _EventSpan(a, b)))
+        else:
+            c.all_reduce(buf)
         return
     if COMM['instrument']:
         w = dist.all_reduce(buf, group=group, async_op=True)

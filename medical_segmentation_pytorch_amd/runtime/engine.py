@@ -81,23 +81,29 @@ def register_stat_group(group, stat_group):
     _STAT_GROUPS[group] = stat_group
 
 
-def stat_group(group):
+def stat_group(group, device=None):
     """Communicator for the SyncBN statistic exchanges of a run on ``group``.
 
     Each RCCL communicator runs its collectives in order on its own stream, so tiny BN all-reduces
     that share the gradient buckets' communicator queue behind multi-MB bucket all-reduces during
     backward.  For WORLD a duplicate communicator is created here (every rank of the job reaches this
     point together); a sub-group uses the partner registered by ``register_stat_group`` or, failing
-    that, itself.
+    that, itself.  On a single-node GPU job the exchanges themselves then run on the IPC peer-memory
+    kernel (:mod:`runtime.comm`), attached here collectively; the RCCL communicator stays the fallback.
     """
     if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return group
     if group in _STAT_GROUPS:
-        return _STAT_GROUPS[group]
-    if group is dist.group.WORLD or dist.get_world_size(group) == dist.get_world_size():
-        _STAT_GROUPS[group] = dist.new_group(list(range(dist.get_world_size())))
-        return _STAT_GROUPS[group]
-    return group
+        sg = _STAT_GROUPS[group]
+    elif group is dist.group.WORLD or dist.get_world_size(group) == dist.get_world_size():
+        sg = _STAT_GROUPS[group] = dist.new_group(list(range(dist.get_world_size())))
+    else:
+        sg = group
+    if device is None and torch.cuda.is_available():
+        device = torch.device('cuda', torch.cuda.current_device())
+    from . import comm
+    comm.attach(sg, device)
+    return sg
 
 
 class _Bucket:

@@ -115,7 +115,9 @@ def parallel_model(config, model, rank, device, optimizer=None):
             bucketer = GradBucketer(arena, group, config.bucket_cap_mb,
                                     compress=getattr(config, 'grad_compress', None))
             optimizer.attach_bucketer(bucketer)
+        from ..runtime import comm as ipc_comm
         from ..runtime.engine import stat_group
+        ipc_comm.POLICY['mode'] = os.environ.get('MSP_SYNCBN_COMM', getattr(config, 'syncbn_comm', 'auto'))
         from ..runtime.fused_model import eager_parts
         if group is not None and config.synBN:
             # modules that run eagerly inside the fused model (smp decoders over a fused encoder): torch

@@ -51,18 +51,19 @@ if rank == 0:
     upd = [p.detach().float().cpu() - a for p, a in zip(model.parameters(), w0)]   # the SGD update
     w = torch.cat([u.flatten() for u in upd])
     rms = [b.detach().float().cpu() for n, b in model.named_buffers() if 'running_mean' in n]
+    from medical_segmentation_pytorch_amd.runtime import comm
     torch.save({'w': w, 'upd': upd, 'names': names, 'rm': torch.cat(rms), 'rms': rms, 'loss': float(loss),
-                'exchanges': exchanges, 'n_bn': n_bn}, os.environ['OUT'])
+                'exchanges': exchanges, 'n_bn': n_bn, 'path': comm.describe()}, os.environ['OUT'])
 dist.destroy_process_group()
 '''
 
 
-def _run(world, out, tmp, dup=False, perturb=False):
+def _run(world, out, tmp, dup=False, perturb=False, syncbn_comm='auto'):
     s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
     script = tmp / 'w.py'
     script.write_text(WORKER)
     env = dict(os.environ, ROOT=ROOT, OUT=str(out), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
-               DUP='1' if dup else '0', PERTURB='1' if perturb else '0')
+               DUP='1' if dup else '0', PERTURB='1' if perturb else '0', MSP_SYNCBN_COMM=syncbn_comm)
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={world}',
            '--master-addr', '127.0.0.1', '--master-port', str(port), str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
@@ -83,6 +84,18 @@ def test_replicated_batch_is_exact(gpu, tmp_path):
     print('replicated: max running_mean rel diff', max(rel))
     assert max(rel) < 1e-4, rel
     assert per[0][0] < 1e-2, per[:8]
+
+
+def test_syncbn_ipc_exchange_bitwise_equals_collective(gpu, tmp_path):
+    """The SyncBN exchange on the IPC peer-memory kernel vs the process group's collective (gloo here: RCCL
+    refuses two ranks on one GPU): with two ranks both sum x0 + x1 in fp64, so the whole training step --
+    statistics, data-gradients, the averaged update -- must be BITWISE identical."""
+    ipc = _run(2, tmp_path / 'ipc.pt', tmp_path, syncbn_comm='ipc')
+    col = _run(2, tmp_path / 'col.pt', tmp_path, syncbn_comm='rccl')
+    assert ipc['path'] == ['ipc'] and col['path'] == ['rccl'], (ipc['path'], col['path'])
+    assert ipc['exchanges'] == col['exchanges'] > 0
+    assert torch.equal(ipc['rm'], col['rm'])
+    assert torch.equal(ipc['w'], col['w'])
 
 
 def _upd_rel(a, b):
@@ -173,6 +186,6 @@ def test_main_torchrun_world1_graph(gpu, tmp_path):
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
-    log = open(tmp_path / 'save' / 'seg_trainer.log').read()
+    log = open(tmp_path / 'save' / 'medseg_trainer.log').read()   # MyConfig.logger_name
     assert 'hipGraph capture on' in log and 'gradient bucketer off' in log, log[-2000:]
     assert os.path.isfile(tmp_path / 'save' / 'last.pth')
