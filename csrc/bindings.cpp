@@ -41,6 +41,27 @@ void fill_coefs(const OptTensors& cs, int n, const std::vector<int64_t>& ld, con
   }
 }
 
+// deferred BN-backward prologue of the data-gradient groups (ConvArgs::gy): per group the BN input y (bf16,
+// the group's shape), its stats [4][C] and backward coef [3][C] (fp32), or None for a plain gradient group
+bool fill_bwd(const OptTensors& ys, const OptTensors& ss, const OptTensors& ks, int n, int64_t numel, int64_t C,
+              const uint16_t** gy, const float** gs, const float** gk) {
+  TORCH_CHECK(ys.empty() || ((int)ys.size() == n && (int)ss.size() == n && (int)ks.size() == n),
+              "BN-backward prologue: one (y, stats, coef) entry per gradient group");
+  bool any = false;
+  for (int i = 0; i < n; ++i) {
+    gy[i] = nullptr; gs[i] = nullptr; gk[i] = nullptr;
+    if (ys.empty() || !ys[i].has_value() || !ys[i]->defined()) continue;
+    CHECK_BF16(*ys[i]);
+    TORCH_CHECK(ys[i]->numel() == numel, "BN-backward prologue: y must have the gradient's shape");
+    TORCH_CHECK(ss[i].has_value() && ks[i].has_value(), "BN-backward prologue: stats and coef required");
+    CHECK_F32(*ss[i]); CHECK_F32(*ks[i]);
+    TORCH_CHECK(ss[i]->numel() >= 2 * C && ks[i]->numel() >= 3 * C, "BN-backward prologue: [4][C] stats, [3][C] coef");
+    gy[i] = bf(*ys[i]); gs[i] = ss[i]->data_ptr<float>(); gk[i] = ks[i]->data_ptr<float>();
+    any = true;
+  }
+  return any;
+}
+
 ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>& dy, const std::vector<int64_t>& dx) {
   TORCH_CHECK(dims.size() == 13, "geom dims = [N, IH, IW, Gi, Cgi, OH, OW, Go, Cgo, Cgo_l, T, Kp, stride]");
   ConvGeom g{};
@@ -59,7 +80,8 @@ ConvGeom make_geom(const std::vector<int64_t>& dims, const std::vector<int64_t>&
 void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys,
               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& stat_part,
               std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
-              OptTensors xc, int64_t xrelu, bool accumulate) {
+              OptTensors xc, int64_t xrelu, bool accumulate, OptTensors gy, OptTensors gs, OptTensors gk,
+              int64_t grelu) {
   ConvGeom g = make_geom(dims, dy, dx);
   TORCH_CHECK(!accumulate || !(stat_part.has_value() && stat_part->defined()), "accumulate: no stats epilogue");
   TORCH_CHECK((int)xs.size() == g.Gi && (int)ys.size() == g.Go, "group count mismatch");
@@ -77,8 +99,10 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
   CHECK_BF16(wp);
   TORCH_CHECK(wp.numel() == (int64_t)conv_rows_alloc(g.Go * g.Cgo) * g.Kp, "packed weight numel mismatch");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(g.Go == 1 && bias->numel() == g.Cgo_l, "bias: 1 group only");
+  const bool bwd = fill_bwd(gy, gs, gk, g.Gi, (int64_t)g.N * g.IH * g.IW * g.Cgi, g.Cgi, a.gy, a.gs, a.gk);
+  a.grelu = (unsigned)grelu;
   if (stat_part.has_value() && stat_part->defined())
-    TORCH_CHECK(stat_part->numel() == conv_stat_blocks(g, trans) * 2 * g.Go * g.Cgo, "stat_part numel mismatch");
+    TORCH_CHECK(stat_part->numel() == conv_stat_blocks(g, trans, bwd) * 2 * g.Go * g.Cgo, "stat_part numel mismatch");
   a.w = bf(wp);
   a.bias = f32_opt(bias);
   a.stat_part = f32_opt_mut(stat_part);
@@ -94,7 +118,7 @@ void conv_fwd(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::
 // channel partials of the BatchNorm whose output z was this conv's only input.
 void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<at::Tensor> ys, const at::Tensor& stat_part,
                  std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, const at::Tensor& bn_y,
-                 const at::Tensor& bn_coef, bool relu) {
+                 const at::Tensor& bn_coef, bool relu, OptTensors gy, OptTensors gs, OptTensors gk, int64_t grelu) {
   ConvGeom g = make_geom(dims, dy, dx);
   TORCH_CHECK(g.Go == 1 && (int)ys.size() == 1 && (int)xs.size() == g.Gi, "BN epilogue: one output group");
   ConvArgs a{};
@@ -108,8 +132,10 @@ void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<a
   a.y[0] = bf(ys[0]);
   CHECK_BF16(wp);
   TORCH_CHECK(wp.numel() == (int64_t)conv_rows_alloc(g.Go * g.Cgo) * g.Kp, "packed weight numel mismatch");
+  const bool bwd = fill_bwd(gy, gs, gk, g.Gi, (int64_t)g.N * g.IH * g.IW * g.Cgi, g.Cgi, a.gy, a.gs, a.gk);
+  a.grelu = (unsigned)grelu;
   CHECK_F32(stat_part);
-  TORCH_CHECK(stat_part.numel() == conv_stat_blocks(g) * 2 * g.Cgo, "stat_part numel mismatch");
+  TORCH_CHECK(stat_part.numel() == conv_stat_blocks(g, false, bwd) * 2 * g.Cgo, "stat_part numel mismatch");
   CHECK_BF16(bn_y);
   TORCH_CHECK(bn_y.numel() == ys[0].numel(), "bn_y must have the data-gradient's shape");
   CHECK_F32(bn_coef);
@@ -127,7 +153,7 @@ void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<a
 
 void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const at::Tensor& dw,
                   std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
-                  OptTensors xc, int64_t xrelu) {
+                  OptTensors xc, int64_t xrelu, OptTensors gy, OptTensors gs, OptTensors gk, int64_t grelu) {
   ConvGeom g = make_geom(dims, dy, dx);
   TORCH_CHECK((int)xs.size() == g.Gi && (int)dys.size() == g.Go, "group count mismatch");
   std::vector<const uint16_t*> px, pd;
@@ -135,24 +161,35 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   for (auto& t : dys) { CHECK_BF16(t); TORCH_CHECK(t.numel() == (int64_t)g.N * g.OH * g.OW * g.Cgo); pd.push_back(bf(t)); }
   CHECK_F32(dw);
   const int64_t one = (int64_t)g.Go * g.Cgo * g.T * g.Gi * g.Cgi;
-  TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans), "dw numel mismatch (replicas)");
+  const uint16_t* gyp[kMaxGroups];
+  const float* gsp[kMaxGroups];
+  const float* gkp[kMaxGroups];
+  const bool bwd = fill_bwd(gy, gs, gk, g.Go, (int64_t)g.N * g.OH * g.OW * g.Cgo, g.Cgo, gyp, gsp, gkp);
+  TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans, bwd), "dw numel mismatch (replicas)");
   const float* cf[kMaxGroups];
   fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), cf);
   TORCH_CHECK(!trans || xc.empty(), "no BN prologue on transposed weight-gradients");
-  const int rc = conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream());
+  const int rc = conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream(), gyp, gsp, gkp,
+                            (unsigned)grelu);
   TORCH_CHECK(rc == 0, conv_error_string(rc));
 }
 
-int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
-  return conv_wgrad_replicas(make_geom(dims, dy, dx), trans);
+int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
+                              bool bwd) {
+  return conv_wgrad_replicas(make_geom(dims, dy, dx), trans, bwd);
 }
 
-bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
-  return conv_uses_halo(make_geom(dims, dy, dx), trans);
+bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans, bool bwd) {
+  return conv_uses_halo(make_geom(dims, dy, dx), trans, bwd);
 }
 
-int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
-  return conv_stat_blocks(make_geom(dims, dy, dx), trans);
+bool conv_wgrad_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
+  return conv_wgrad_uses_halo(make_geom(dims, dy, dx), trans);
+}
+
+int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
+                           bool bwd) {
+  return conv_stat_blocks(make_geom(dims, dy, dx), trans, bwd);
 }
 
 void pack_weight_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
@@ -785,14 +822,21 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
   m.def("conv_fwd", &conv_fwd, py::arg("xs"), py::arg("wp"), py::arg("ys"), py::arg("bias"), py::arg("stat_part"),
         py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{},
-        py::arg("xrelu") = 0, py::arg("accumulate") = false);
-  m.def("conv_fwd_bn", &conv_fwd_bn);
+        py::arg("xrelu") = 0, py::arg("accumulate") = false, py::arg("gy") = OptTensors{},
+        py::arg("gs") = OptTensors{}, py::arg("gk") = OptTensors{}, py::arg("grelu") = 0);
+  m.def("conv_fwd_bn", &conv_fwd_bn, py::arg("xs"), py::arg("wp"), py::arg("ys"), py::arg("stat_part"), py::arg("dims"),
+        py::arg("dy"), py::arg("dx"), py::arg("bn_y"), py::arg("bn_coef"), py::arg("relu"), py::arg("gy") = OptTensors{},
+        py::arg("gs") = OptTensors{}, py::arg("gk") = OptTensors{}, py::arg("grelu") = 0);
   m.def("conv_wgrad", &conv_wgrad_t, py::arg("dys"), py::arg("xs"), py::arg("dw"), py::arg("dims"), py::arg("dy"),
-        py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{}, py::arg("xrelu") = 0);
+        py::arg("dx"), py::arg("trans"), py::arg("xc") = OptTensors{}, py::arg("xrelu") = 0,
+        py::arg("gy") = OptTensors{}, py::arg("gs") = OptTensors{}, py::arg("gk") = OptTensors{}, py::arg("grelu") = 0);
+  m.def("conv_wgrad_uses_halo", &conv_wgrad_uses_halo_t);
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);
-  m.def("conv_stat_blocks", &conv_stat_blocks_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans") = false);
-  m.def("conv_uses_halo", &conv_uses_halo_t);
+  m.def("conv_stat_blocks", &conv_stat_blocks_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans") = false,
+        py::arg("bwd") = false);
+  m.def("conv_uses_halo", &conv_uses_halo_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"),
+        py::arg("bwd") = false);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
   m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });
   m.def("conv_gemm_force_cfg", [](int64_t c) { conv_gemm_force_cfg((int)c); });
@@ -813,7 +857,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("unpack_wgrad", &unpack_wgrad_t, py::arg("src"), py::arg("dst"), py::arg("nrow"), py::arg("nch"),
         py::arg("T"), py::arg("Cpk"), py::arg("Ktot"), py::arg("t_base"), py::arg("c_base"), py::arg("s_row"),
         py::arg("s_ch"), py::arg("accumulate"), py::arg("nrep") = 1, py::arg("rep_stride") = 0);
-  m.def("conv_wgrad_replicas", &conv_wgrad_replicas_t);
+  m.def("conv_wgrad_replicas", &conv_wgrad_replicas_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"),
+        py::arg("bwd") = false);
   m.def("pack_batch", &pack_batch_t);
   m.def("pack_per_block", &pack_per_block);
   m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });

@@ -391,6 +391,9 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
   float a[8], b[8], k1[8], k2[8], k3[8];
   load8f(scale + c0, a); load8f(shift + c0, b);
   load8f(coef + c0, k1); load8f(coef + Cp + c0, k2); load8f(coef + 2 * Cp + c0, k3);
+  if (!relu)   // bwd1's ReLU test passes everywhere
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = INFINITY;
   const long stride = (long)gridDim.x * R;
   long p = (long)blockIdx.x * R + r;
   for (; p < P; p += kUnroll * stride) {
@@ -410,10 +413,7 @@ __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
       unpack8(gin[u], g);
       unpack8(yin[u], v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float gr = (!relu || fmaf(v[e], a[e], b[e]) > 0.f) ? g[e] : 0.f;
-        g[e] = k1[e] * gr + k2[e] * v[e] + k3[e];
-      }
+      for (int e = 0; e < 8; ++e) g[e] = bwd1(g[e], v[e], a[e], b[e], k1[e], k2[e], k3[e]);
       *reinterpret_cast<uint4*>(dy + q * Cp + c0) = pack8(g);
     }
   }

@@ -80,6 +80,24 @@ DEVI uint4 affine8(const uint4& v, const float* s, const float* h, bool relu) {
   return pack8(f);
 }
 
+// BatchNorm(+ReLU) backward apply on 8 channels: dy = k1 * dzr + k2 * y + k3 with dzr = dz where
+// scale*y + shift > 0 (or everywhere: shift = +inf for a BN without ReLU), else 0.  ONE definition for
+// bn_act_bwd_apply and the conv staging prologues, so the deferred and the materialised dy are
+// bit-identical.  t = [5][ld] table (scale, shift, k1, k2, k3) at the 8 channels.
+DEVI float bwd1(float d, float v, float sc, float sh, float k1, float k2, float k3) {
+  const float gr = fmaf(v, sc, sh) > 0.f ? d : 0.f;
+  return fmaf(k1, gr, fmaf(k2, v, k3));
+}
+
+DEVI uint4 bwd8(const uint4& dz, const uint4& yv, const float* t, int ld) {
+  float d[8], v[8];
+  unpack8(dz, d);
+  unpack8(yv, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) d[e] = bwd1(d[e], v[e], t[e], t[ld + e], t[2 * ld + e], t[3 * ld + e], t[4 * ld + e]);
+  return pack8(d);
+}
+
 DEVI float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -529,10 +529,14 @@ DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 1
 #ifndef DW_MIN_WAVES
 #define DW_MIN_WAVES 1
 #endif
-template <int NPW, int NCB>
+// BWD: the dY sub-tiles are rebuilt from (dz, y) at staging time (WgradPtrs::gy, the deferred
+// BN-backward prologue -- the same bwd8 as bn_act_bwd_apply, so dY is bit-identical)
+template <int NPW, int NCB, bool BWD = false>
 __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
                                                               DwTile tl, int KT, long ntiles) {
   constexpr int NST = dw_stage(NCB);
+  constexpr int LDT = DW_CH * NCB;                        // BWD table row length (the block's co rows)
+  __shared__ float s_bt[BWD ? 5 * LDT : 1];
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
   constexpr int NPX = 256, NSL = 8, SUB = NPX * DW_CH;
   uint16_t* sY = dsm;                       // [NCB][256][32]  swizzled
@@ -544,10 +548,23 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
   const int co0 = blockIdx.y * DW_CH * NCB, ci0 = blockIdx.z * DW_CH;
   const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
+  if constexpr (BWD) {   // [5][LDT]: scale, shift (+inf: no ReLU test), k1, k2, k3 of the block's co rows
+    for (int e = tid; e < LDT; e += 64 * kDwWaves) {
+      const int co = co0 + e;
+      const int gg = co < rows ? co / g.Cgo : 0, cl = co - gg * g.Cgo;
+      const bool on = co < rows && P.gy[gg] != nullptr;
+      s_bt[e] = on ? P.gs[gg][cl] : 0.f;
+      s_bt[LDT + e] = (on && ((P.grelu >> gg) & 1u)) ? P.gs[gg][g.Cgo + cl] : INFINITY;
+      s_bt[2 * LDT + e] = on ? P.gk[gg][cl] : 1.f;
+      s_bt[3 * LDT + e] = on ? P.gk[gg][g.Cgo + cl] : 0.f;
+      s_bt[4 * LDT + e] = on ? P.gk[gg][2 * g.Cgo + cl] : 0.f;
+    }
+  }
 
   // per-thread loader roles: vector vv = tid & 3 (8 channels), pixel lane vp = tid >> 2 (16 per wave)
   const int vv = tid & 3, vp = tid >> 2;
   const uint16_t* y_base[NCB];
+  const uint16_t* z_base[BWD ? NCB : 1];   // BWD: the BN input y of the dY group (nullptr: plain group)
   bool y_ok[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -555,6 +572,8 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
     y_ok[cb] = yco < rows;
     const int y_g = y_ok[cb] ? yco / g.Cgo : 0;
     y_base[cb] = P.dy[y_g] + (y_ok[cb] ? yco - y_g * g.Cgo : 0);
+    if constexpr (BWD)
+      z_base[cb] = (y_ok[cb] && P.gy[y_g] != nullptr) ? P.gy[y_g] + (yco - y_g * g.Cgo) : nullptr;
   }
   const int xci = ci0 + 8 * vv;
   const bool x_ok = xci < Cip;
@@ -609,8 +628,10 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
   // after it, so HBM latency hides under the MFMAs.  Slot u < 2*NCB is dY sub-tile u/2 (pixels
   // vp + 128*(u&1)); the other slots walk the halo.
   uint4 sv[NST];
+  uint4 sz[BWD ? 2 * NCB : 1];   // BWD: y of the dY slots
   int sd[NST];
   unsigned sx = 0;   // staged halo slots that hold in-image pixels (get the BN prologue)
+  unsigned syb = 0;  // BWD: dY slots with a loaded y (get the BN-backward prologue)
   auto stage_load = [&](long tix) {
     const int per_img = tl.tiles_y * tl.tiles_x;
     const int n = (int)(tix / per_img);
@@ -619,6 +640,7 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
     const long yoff = (long)n * g.OH * g.OW * g.Cgo;
     const uint16_t* xim = x_base + (long)n * g.IH * g.IW * g.Cgi;
     sx = 0;
+    syb = 0;
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
       sv[u] = make_uint4(0, 0, 0, 0);
@@ -627,8 +649,17 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
         const int cb = u >> 1, e = vp + 16 * kDwWaves * (u & 1);
         const int oy = y0 + (e >> tl.tw_shift), ox = x0 + (e & (tl.TW - 1));
         sd[u] = cb * SUB + dw_elem(e, vv >> 1, 2 * (vv & 1));
-        if (y_ok[cb] && oy < g.OH && ox < g.OW)
-          sv[u] = *reinterpret_cast<const uint4*>(y_base[cb] + yoff + (oy * g.OW + ox) * g.Cgo);
+        if constexpr (BWD) sz[u] = make_uint4(0, 0, 0, 0);
+        if (y_ok[cb] && oy < g.OH && ox < g.OW) {
+          const long po = yoff + (oy * g.OW + ox) * g.Cgo;
+          sv[u] = *reinterpret_cast<const uint4*>(y_base[cb] + po);
+          if constexpr (BWD) {
+            if (z_base[cb] != nullptr) {
+              sz[u] = *reinterpret_cast<const uint4*>(z_base[cb] + po);
+              syb |= 1u << u;
+            }
+          }
+        }
       } else {
         const int hp = vp + 16 * kDwWaves * (u - 2 * NCB);
         if (hp < nh) {
@@ -651,6 +682,9 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
       if (sd[u] < 0) continue;
       uint4 v = sv[u];
       if (x_cf != nullptr && ((sx >> u) & 1u)) v = affine8(v, x_sc, x_sh, x_relu);
+      if constexpr (BWD) {
+        if (u < 2 * NCB && ((syb >> u) & 1u)) v = bwd8(v, sz[u < 2 * NCB ? u : 0], s_bt + DW_CH * (u >> 1) + 8 * vv, LDT);
+      }
       *reinterpret_cast<uint4*>(&sY[sd[u]]) = v;
     }
     __syncthreads();
@@ -859,8 +893,11 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // WL (whole-input, non-PIPE; opt-in, env MSP_HALO_WLDS=1): the block's packed weight rows are staged in
 // LDS next to the input tile, so the k-loop reads A from LDS instead of one global (L2) load per k-step
 // with a one-step prefetch (measured neutral: see halo_wlds_enabled)
-template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool WL = false>
+// BWD: the data-gradient staging rebuilds dY from (dz, y) per input group (ConvArgs::gy, the deferred
+// BN-backward prologue: no bn_act_bwd_apply pass writes dY); never with PIPE / WL
+template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool WL = false, bool BWD = false>
 __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+  static_assert(!(BWD && (PIPE || WL)), "BN-backward prologue: standard / chunked staging only");
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
   __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
@@ -870,6 +907,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   // which drains every staging load in flight -- the staging loop then ran one round trip at a time (a
   // select chain over a.x[] is folded back into that load); an LDS read waits on lgkmcnt only.
   __shared__ const uint16_t* s_xp[kMaxGroups];
+  __shared__ const uint16_t* s_yp[BWD ? kMaxGroups : 1];   // BWD: the groups' BN inputs y (nullable)
   // (pointers read back from LDS are generic: loads through them would be FLAT, counted in lgkmcnt too,
   // so the next pointer read's lgkmcnt wait would drain them again -- load through global pointers)
   const ConvGeom& g = a.g;
@@ -878,14 +916,32 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   const int Cip = g.Gi * g.Cgi, C8c = hg.CC >> 3;
   const int rows = g.Go * g.Cgo;
   const int hpx = hg.HH * hg.HWD;
-  if (tid < kMaxGroups) s_xp[tid] = a.x[tid];
-  if (g.Gi > 1) __syncthreads();   // block-uniform; Gi == 1 staging never reads s_xp
+  if (tid < kMaxGroups) {
+    s_xp[tid] = a.x[tid];
+    if constexpr (BWD) s_yp[tid] = a.gy[tid];
+  }
+  if (g.Gi > 1) __syncthreads();   // block-uniform; Gi == 1 staging never reads s_xp / s_yp
   // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
   float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
   // deferred-BN prologue table after them (hg.xtab): per input channel scale, shift and the ReLU floor
   // (0 or -inf); groups without a prologue get the identity (exact on bf16 values)
   float* s_coef = s_stat + kHaloWaves * 2 * rows;
-  if (!BNE && hg.xtab) {
+  if constexpr (BWD) {
+    // BN-backward table [5][Cip]: scale, shift (+inf: no ReLU test), k1, k2, k3; plain groups get the
+    // identity (dy = dz exactly: y is never loaded for them)
+    for (int c = tid; c < Cip; c += 64 * kHaloWaves) {
+      const int gi = c / g.Cgi, cl = c - gi * g.Cgi;
+      const bool on = a.gy[gi] != nullptr;
+      const float* st = a.gs[gi];
+      const float* k = a.gk[gi];
+      s_coef[c] = on ? st[cl] : 0.f;
+      s_coef[Cip + c] = (on && ((a.grelu >> gi) & 1u)) ? st[g.Cgi + cl] : INFINITY;
+      s_coef[2 * Cip + c] = on ? k[cl] : 1.f;
+      s_coef[3 * Cip + c] = on ? k[g.Cgi + cl] : 0.f;
+      s_coef[4 * Cip + c] = on ? k[2 * g.Cgi + cl] : 0.f;
+    }
+    __syncthreads();
+  } else if (!BNE && hg.xtab) {
     for (int c = tid; c < Cip; c += 64 * kHaloWaves) {
       const int gi = c / g.Cgi, cl = c - gi * g.Cgi;
       const float* cf = a.xc[gi];
@@ -924,6 +980,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   int ty0 = 0, tx0 = 0;
   long img = 0;
   const uint16_t* xim0 = a.x[0];
+  const uint16_t* yim0 = BWD ? a.gy[0] : nullptr;   // BWD, Gi == 1: the BN input of the one group
   auto set_tile = [&](int t, int& y0, int& x0, long& im) {
     const int n = t / per_img;
     const int trem = t - n * per_img;
@@ -935,12 +992,18 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
 
   // staging: element idx -> (halo pixel, 8-channel slot of the chunk); zero outside the image.
   // 32-bit per-image offsets (one image's activations < 2^31 elements) from per-image base pointers.
-  auto load_batch = [&](int c0, int base, uint4* v, int* dst) {
+  // (BWD: yv[u] = the BN input y at the same element, cc[u] = its channel in [0, Cip) or -1 outside
+  // the image / for a plain group -- the zero padding and plain groups stay dz)
+  auto load_batch = [&](int c0, int base, uint4* v, int* dst, uint4* yv, int* cc) {
 #pragma unroll
     for (int u = 0; u < kHaloLd; ++u) {
       const int idx = base + u * 64 * kHaloWaves;
       v[u] = make_uint4(0, 0, 0, 0);
       dst[u] = -1;
+      if constexpr (BWD) {
+        yv[u] = make_uint4(0, 0, 0, 0);
+        cc[u] = -1;
+      }
       if (idx < total) {
         const int hp = fdiv(idx, C8c, hg.inv_c8), c8 = idx - __mul24(hp, C8c);
         const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
@@ -951,18 +1014,36 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
           const int pix = iy * g.IW + ix;
           if (g.Gi == 1) {
             v[u] = ldg4(xim0 + pix * g.Cgi + ci);
+            if constexpr (BWD) {
+              yv[u] = ldg4(yim0 + pix * g.Cgi + ci);
+              cc[u] = ci;
+            }
           } else {
             const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
-            v[u] = ldg4(s_xp[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+            const int off = img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi));
+            v[u] = ldg4(s_xp[gi] + off);
+            if constexpr (BWD) {
+              const uint16_t* yp = s_yp[gi];
+              if (yp != nullptr) {
+                yv[u] = ldg4(yp + off);
+                cc[u] = ci;
+              }
+            }
           }
         }
       }
     }
   };
-  auto store_batch = [&](const uint4* v, const int* dst) {
+  auto store_batch = [&](const uint4* v, const int* dst, const uint4* yv, const int* cc) {
 #pragma unroll
-    for (int u = 0; u < kHaloLd; ++u)
-      if (dst[u] >= 0) *reinterpret_cast<uint4*>(tile + dst[u]) = v[u];
+    for (int u = 0; u < kHaloLd; ++u) {
+      if (dst[u] < 0) continue;
+      uint4 val = v[u];
+      if constexpr (BWD) {
+        if (cc[u] >= 0) val = bwd8(val, yv[u], s_coef + cc[u], Cip);
+      }
+      *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+    }
   };
   // Deferred-BN prologue as its own pass over the staged chunk (after the barrier that published it):
   // every in-image vector is normalised (+ReLU) in place from the LDS table, the zero padding is left
@@ -1003,6 +1084,8 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   constexpr int PF = CHUNKED ? kHaloLd : (PIPE ? kPipeLd : 1);
   uint4 pv[PF];
   int pd[PF];
+  uint4 pyv[(BWD && CHUNKED) ? PF : 1];
+  int pcc[(BWD && CHUNKED) ? PF : 1];
   // PIPE: the whole halo tile of tile t (total <= 256*kPipeLd vectors, host-checked) is fetched into
   // registers while the block computes the previous tile -- HBM reads overlap MFMA + epilogue work
   // instead of running as serial phases.  pd[u] = LDS offset | (slot + 1) << 16 for in-image vectors,
@@ -1081,8 +1164,11 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   for (int tt = wgid; tt < t_end; tt += (PIPE ? nwg : 1)) {
   set_tile(tt, ty0, tx0, img);
   xim0 = a.x[0] + img * g.Cgi;
+  if constexpr (BWD) {
+    if (g.Gi == 1) yim0 = a.gy[0] + img * g.Cgi;
+  }
   if (CHUNKED) {
-    load_batch(0, tid, pv, pd);   // host guarantees total <= 64*kHaloWaves*kHaloLd
+    load_batch(0, tid, pv, pd, pyv, pcc);   // host guarantees total <= 64*kHaloWaves*kHaloLd
   } else if (PIPE) {
     if (tt != wgid) __syncthreads();   // every wave is done reading the previous tile
     pipe_store();
@@ -1099,10 +1185,12 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
     const int iy0 = ty0 + hg.ey0, ix0 = tx0 + hg.ex0;
     for (int base = tid; base < ((HALO_KO(hg, 8)) ? 0 : total); base += 64 * kHaloWaves * kHaloLd) {
       uint4 v[kHaloLd];
+      uint4 yv[BWD ? kHaloLd : 1];
       int dst[kHaloLd], cc[kHaloLd];
 #pragma unroll
       for (int u = 0; u < kHaloLd; ++u) {
         v[u] = make_uint4(0, 0, 0, 0);
+        if constexpr (BWD) yv[u] = make_uint4(0, 0, 0, 0);
         dst[u] = -1;
         cc[u] = -1;
         if (base + u * 64 * kHaloWaves < total) {
@@ -1114,9 +1202,16 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
             cc[u] = c8;
             if (g.Gi == 1) {
               v[u] = ldg4(xim0 + pix * g.Cgi + ci);
+              if constexpr (BWD) yv[u] = ldg4(yim0 + pix * g.Cgi + ci);
             } else {
               const int gi = fdiv(ci, g.Cgi, hg.inv_cgi);
-              v[u] = ldg4(s_xp[gi] + img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi)));
+              const int off = img * g.Cgi + (pix * g.Cgi + ci - __mul24(gi, g.Cgi));
+              v[u] = ldg4(s_xp[gi] + off);
+              if constexpr (BWD) {
+                const uint16_t* yp = s_yp[gi];
+                if (yp != nullptr) yv[u] = ldg4(yp + off);
+                else cc[u] = -1;   // a plain gradient group: stored as loaded
+              }
             }
           }
         }
@@ -1129,7 +1224,15 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         hy += hg.st_a;
         if (hx >= hg.HWD) { hx -= hg.HWD; ++hy; }
       }
-      if (!BNE && hg.xtab) {
+      if constexpr (BWD) {
+#pragma unroll
+        for (int u = 0; u < kHaloLd; ++u) {
+          if (dst[u] < 0) continue;
+          uint4 val = v[u];
+          if (cc[u] >= 0) val = bwd8(val, yv[u], s_coef + cc[u] * 8, Cip);
+          *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+        }
+      } else if (!BNE && hg.xtab) {
 #pragma unroll
         for (int u = 0; u < kHaloLd; ++u) {
           if (dst[u] < 0) continue;
@@ -1175,9 +1278,9 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       const int c0 = ch * hg.CC;
       if (CHUNKED) {
         if (ch > 0) __syncthreads();           // every wave is done reading the previous chunk
-        store_batch(pv, pd);
+        store_batch(pv, pd, pyv, pcc);
         __syncthreads();
-        if (ch + 1 < hg.nch) load_batch(c0 + hg.CC, tid, pv, pd);   // in flight during the MFMAs
+        if (ch + 1 < hg.nch) load_batch(c0 + hg.CC, tid, pv, pd, pyv, pcc);   // in flight during the MFMAs
         if (!BNE && hg.xtab) {   // prologues are forward-only, BNE data-gradient-only
           xform_pass(c0);
           __syncthreads();
@@ -1523,7 +1626,8 @@ static int halo_fallback_mi(int rows) {
   return cdiv(rows, 48) * 48 <= cdiv(rows, 64) * 64 ? 3 : 4;
 }
 
-static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
+// bwd: a data-gradient launch with the BN-backward prologue: its [5][Cip] table instead of [3][Cip], no PIPE
+static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg, bool bwd = false) {
   if (trans || g.stride != 1 || g.OH != g.IH || g.OW != g.IW) return false;
   const int rows = g.Go * g.Cgo;
   if (rows > kHaloMaxRows || g.T > 16) return false;
@@ -1541,7 +1645,8 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi); try 3: a
   // 128-pixel tile (NJ = 2) for inputs too wide for a 256-pixel halo tile (136 channels at 44^2: the
   // gather kernel re-reads every input pixel once per tap from L2)
-  const bool pipe_ok = pipe_enabled() && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
+  const bool pipe_ok = !bwd && pipe_enabled() && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
+  const size_t tab = (bwd ? 20 : 12) * (size_t)Cip;   // prologue table bytes
   for (int attempt = pipe_ok ? 0 : 1; attempt < 4; ++attempt) {
   const bool pipe = attempt == 0;
   if (attempt == 2 && halo_fallback_mi(rows) == 0) continue;
@@ -1553,7 +1658,7 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
   const int nj = attempt == 3 ? 2 : halo_nj(mi, pipe);
   const int tp = kHaloWaves * nj * 16;
   for (int pass = 0; pass < (pipe || attempt == 3 ? 1 : 2); ++pass) {   // pass 0: whole input; 1: chunks
-    if (pass == 1 && n_rg != 1) break;
+    if (pass == 1 && (n_rg != 1 || bwd)) break;   // BWD: no chunked staging (its y registers would spill)
     for (int d = C8; d >= 1; --d) {
       if (C8 % d != 0) continue;
       if (pass == 0 && d != C8) break;
@@ -1567,10 +1672,10 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
         const int th = tp / tw;
         const int HH = th + ey1 - ey0, HWD = tw + ex1 - ex0;
         // (+ the prologue table a deferred-BN input adds: two blocks per CU must still fit)
-        if (halo_lds_bytes(HH, HWD, pitch, rows) + 12 * (size_t)Cip > halo_tile_cap()) continue;
+        if (halo_lds_bytes(HH, HWD, pitch, rows) + tab > halo_tile_cap()) continue;
         if (pass == 1 && HH * HWD * d > 64 * kHaloWaves * kHaloLd) continue;
         if (pipe && HH * HWD * d > 64 * kHaloWaves * kPipeLd) continue;
-        if (pipe && halo_lds_bytes(HH, HWD, pitch, rows) + 12 * (size_t)Cip + pipe_a_bytes(rows, mi, ks) >
+        if (pipe && halo_lds_bytes(HH, HWD, pitch, rows) + tab + pipe_a_bytes(rows, mi, ks) >
                         (size_t)kPipeMaxLds) continue;
         const double tiles = (double)cdiv(g.OH, th) * cdiv(g.OW, tw);
         const double cost = tiles * ((double)tp * rows / 8.0 + 0.5 * (double)HH * HWD * C8);
@@ -1591,7 +1696,7 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg) {
       hg.nj = nj;
       hg.pipe = pipe ? 1 : 0;
       hg.wl = 0;
-      if (!pipe && pass == 0 && halo_wlds_enabled()) {
+      if (!pipe && !bwd && pass == 0 && halo_wlds_enabled()) {
         // weights in LDS when the block still fits next to its tile and no block per CU is lost: the
         // non-PIPE kernels run (MI <= 2 && NJ <= 4) ? 4 : 3 blocks per CU by registers
         const size_t lds0 = halo_lds_bytes(hg.HH, hg.HWD, pitch, rows) + 12 * (size_t)Cip;
@@ -1629,10 +1734,10 @@ static bool halo_enabled() {
 void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
 void conv_set_small_halo(int on) { g_small_tile = on ? 1 : 0; }
 void conv_set_wlds(int on) { g_wlds = on ? 1 : 0; }
-bool conv_uses_halo(const ConvGeom& g, bool trans) {
+bool conv_uses_halo(const ConvGeom& g, bool trans, bool bwd) {
   HaloGeom hg;
   if (conv_gemm_ok(g, trans)) return false;   // wide inputs: the LDS-tiled GEMM kernel (conv_gemm.hip)
-  return halo_enabled() && conv_halo_ok(g, trans, hg);
+  return halo_enabled() && conv_halo_ok(g, trans, hg, bwd);
 }
 
 static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
@@ -1644,10 +1749,10 @@ static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
 // takes: ``trans`` (a strided transposed conv, conv_igemm's flag) never takes the GEMM or halo kernel --
 // sizing its rows by conv_gemm_ok(g, false) under-allocated the gather kernel's rows (out-of-bounds stat
 // writes: UNet / Linknet deconvs from 64 input channels up)
-long conv_stat_blocks(const ConvGeom& g, bool trans) {
+long conv_stat_blocks(const ConvGeom& g, bool trans, bool bwd) {
   HaloGeom hg;
   if (!trans && conv_gemm_ok(g, false)) return conv_gemm_stat_blocks(g);
-  if (!trans && halo_enabled() && conv_halo_ok(g, false, hg)) return halo_blocks(g, hg);
+  if (!trans && halo_enabled() && conv_halo_ok(g, false, hg, bwd)) return halo_blocks(g, hg);
   const int mi = conv_pick_mi(g.Go * g.Cgo);
   const int nj = conv_pick_nj(g, mi);
   const int wpx = conv_pick_wpx(g, mi, nj);
@@ -1700,9 +1805,12 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     conv_igemm_phased(a, mi, s);
     return 0;
   }
+  bool bwd = false;
+  for (int i = 0; i < a.g.Gi; ++i) bwd |= a.gy[i] != nullptr;
+  if (bwd && (trans || conv_gemm_ok(a.g, trans))) return 7;
   if (conv_gemm_ok(a.g, trans)) return conv_gemm(a, s);
   HaloGeom hg;
-  if (halo_enabled() && conv_halo_ok(a.g, trans, hg)) {
+  if (halo_enabled() && conv_halo_ok(a.g, trans, hg, bwd)) {
     const unsigned blocks = (unsigned)halo_blocks(a.g, hg);
     const bool pipe = hg.pipe != 0;
     const int hmi = hg.mi;
@@ -1712,7 +1820,9 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     if (dbg < 0) { const char* e = getenv("MSP_HALO_DBG"); dbg = e != nullptr ? atoi(e) : 0; }
     hg.dbg = dbg;
     if (hg.xtab && a.bn_y != nullptr) return 3;   // BN prologue (forward) and BN epilogue (dgrad) never meet
-    const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) + (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0) +
+    if (bwd && hg.xtab) return 3;
+    const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) +
+                       (bwd ? 5 * 4 * (size_t)a.g.Gi * a.g.Cgi : (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0)) +
                        ((hg.pipe || hg.wl) ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
     // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers.
     // The prologue table may take the dynamic LDS past 64 KB: opted into once per instantiation,
@@ -1732,6 +1842,16 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       HC_LAUNCH_((conv_halo_kernel<MI_, 2, false, BNE_>))                                                    \
       return 0;                                                                                              \
     }
+#define HB_(MI_, BNE_)                                                                                       \
+    if (bwd && hmi == MI_ && bne == BNE_) {                                                                  \
+      const int nj_ = hg.nj;                                                                                 \
+      if (MI_ >= 3 && nj_ == 2) {                                                                            \
+        if constexpr (MI_ >= 3) HC_LAUNCH_((conv_halo_kernel<(MI_ >= 3 ? MI_ : 3), 2, false, BNE_, false, false, true>)) \
+      } else if (MI_ <= 2 && nj_ == 4) {                                                                     \
+        HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_, false, false, true>))                              \
+      } else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, false, true>))       \
+      return 0;                                                                                              \
+    }
 #define HC_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe) {                                                                \
       if (MI_ <= 2 && hg.nj == 4) {                                                                          \
@@ -1748,10 +1868,12 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       return 0;                                                                                              \
     }
     const bool bne = a.bn_y != nullptr;
+    HB_(1, false) HB_(2, false) HB_(3, false) HB_(4, false) HB_(1, true) HB_(2, true) HB_(3, true) HB_(4, true)
     HS_(3, false) HS_(4, false) HS_(3, true) HS_(4, true)
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
     HP_(2, false) HP_(3, false) HP_(2, true) HP_(3, true)
     return 4;   // no instantiation for this row-group size
+#undef HB_
 #undef HP_
 #undef HS_
 #undef HC_
@@ -1774,6 +1896,7 @@ const char* conv_error_string(int rc) {
     case 4: return "halo conv: no instantiation for this row-group size";
     case 5: return "wgrad: no instantiation for the chosen tile configuration";
     case 6: return "wgrad (halo / gather): no instantiation for this plan";
+    case 7: return "BN-backward prologue: only the stride-1 halo kernels rebuild dY (resolve the gradient first)";
   }
   return "conv: unknown error";
 }
@@ -1817,7 +1940,9 @@ struct WgradPlan {
   long nsplit, ntiles;
 };
 
-static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
+// bwd: the dY groups carry the BN-backward prologue (at most 2 co sub-tiles per block: the y staging
+// registers of a third spill)
+static WgradPlan wgrad_plan(const ConvGeom& g, bool trans, bool bwd = false) {
   WgradPlan P{};
   const int KT = g.T * g.Gi * g.Cgi;
   const int rows = g.Go * g.Cgo;
@@ -1837,7 +1962,7 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans) {
     const int nst = cdiv(rows, DW_CH);
     int ncb = 1;
     double best = 1e30;
-    for (int c = 1; c <= std::min(max_ncb, nst); ++c) {
+    for (int c = 1; c <= std::min(bwd ? 2 : max_ncb, nst); ++c) {
       if (c > 1 && wgrad_halo_lds(P.tl, c) > (size_t)kDwMaxLds) break;
       const int gy = cdiv(nst, c);
       const double cost = (double)gy * c + kDwHaloCost * gy;
@@ -1887,13 +2012,18 @@ static bool wgrad_use_gemm(const ConvGeom& g, bool trans) {
   return g.Cgi >= 64 || g.stride > 1 || g.T == 1 || trans || !wgrad_halo_ok(g, tl);
 }
 
-int conv_wgrad_replicas(const ConvGeom& g, bool trans) {
+int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd) {
   if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm_replicas(g);
-  return (int)wgrad_plan(g, trans).nsplit;
+  return (int)wgrad_plan(g, trans, bwd).nsplit;
+}
+
+bool conv_wgrad_uses_halo(const ConvGeom& g, bool trans) {
+  return !wgrad_use_gemm(g, trans) && wgrad_plan(g, trans).halo;
 }
 
 int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-               const float* const* xc, unsigned xrelu, hipStream_t s) {
+               const float* const* xc, unsigned xrelu, hipStream_t s, const uint16_t* const* gy,
+               const float* const* gs, const float* const* gk, unsigned grelu) {
   const int KT = g.T * g.Gi * g.Cgi;
   WgradPtrs P{};
   for (int i = 0; i < g.Go; ++i) P.dy[i] = dy[i];
@@ -1901,8 +2031,17 @@ int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, c
   bool pro = false;
   for (int i = 0; i < g.Gi; ++i) { P.xc[i] = xc != nullptr ? xc[i] : nullptr; pro |= P.xc[i] != nullptr; }
   P.xrelu = xrelu;
+  bool bwd = false;
+  for (int i = 0; i < g.Go; ++i) {
+    P.gy[i] = gy != nullptr ? gy[i] : nullptr;
+    P.gs[i] = gs != nullptr ? gs[i] : nullptr;
+    P.gk[i] = gk != nullptr ? gk[i] : nullptr;
+    bwd |= P.gy[i] != nullptr;
+  }
+  P.grelu = grelu;
+  if (bwd && !conv_wgrad_uses_halo(g, trans)) return 7;
   if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm(P, dw, g, pro, s);
-  const WgradPlan W = wgrad_plan(g, trans);
+  const WgradPlan W = wgrad_plan(g, trans, bwd);
   if (W.halo) {
     const size_t lds = wgrad_halo_lds(W.tl, W.ncb);
     dim3 grid((unsigned)W.nsplit, W.gy, W.gz);
@@ -1910,19 +2049,21 @@ int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, c
     const int ncb = W.ncb;
     // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU) is opted into once per instantiation, before any
     // graph capture (the first call of every shape runs eagerly)
-#define HW_(N_, C_)                                                                                      \
-    if (npw == N_ && ncb == C_) {                                                                       \
+#define HW_(N_, C_, B_)                                                                                  \
+    if (npw == N_ && ncb == C_ && bwd == B_) {                                                          \
       static bool lds_attr = false;                                                                     \
       if (!lds_attr) {                                                                                  \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_halo_kernel<N_, C_>),       \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_halo_kernel<N_, C_, B_>),   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kDwMaxLds);               \
         lds_attr = true;                                                                                \
       }                                                                                                 \
-      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, W.tl, KT, \
-                         W.ntiles);                                                                     \
+      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_, B_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, W.tl, \
+                         KT, W.ntiles);                                                                 \
       return 0;                                                                                         \
     }
-    HW_(1, 1) HW_(2, 1) HW_(3, 1) HW_(1, 2) HW_(2, 2) HW_(3, 2) HW_(1, 3) HW_(2, 3) HW_(3, 3)
+    HW_(1, 1, false) HW_(2, 1, false) HW_(3, 1, false) HW_(1, 2, false) HW_(2, 2, false) HW_(3, 2, false)
+    HW_(1, 3, false) HW_(2, 3, false) HW_(3, 3, false)
+    HW_(1, 1, true) HW_(2, 1, true) HW_(3, 1, true) HW_(1, 2, true) HW_(2, 2, true) HW_(3, 2, true)
 #undef HW_
     return 6;
   }

@@ -45,6 +45,16 @@ struct ConvArgs {
   // accumulate: y += conv(x) (the stored bf16 output is read, added in fp32 and re-rounded -- exactly a
   // separate bf16 add); data-gradients of sibling launches that read the same input.  No BN epilogue.
   int accum;
+  // Deferred BN-BACKWARD prologue (data-gradient launches on the halo kernel; the mirror of xc): input
+  // group i holds dL/dz of a training BatchNorm(+ReLU) whose input y_i is this conv's forward output and
+  // whose data-gradient dL/dy was never written.  Staging rebuilds it, bit-identical to bn_act_bwd_apply:
+  // dy = k1 * (relu ? [scale*y + shift > 0] : 1) * dz + k2 * y + k3 (bwd8 in common.h).
+  // gy[i]: that y (nullptr: the group is a plain gradient); gs[i]: its stats [4][Cgi] (scale, shift rows);
+  // gk[i]: its backward coef [3][Cgi]; bit i of grelu: its ReLU.
+  const uint16_t* gy[kMaxGroups];
+  const float* gs[kMaxGroups];
+  const float* gk[kMaxGroups];
+  unsigned grelu;
   ConvGeom g;
 };
 
@@ -54,6 +64,11 @@ struct WgradPtrs {
   const uint16_t* x[kMaxGroups];
   const float* xc[kMaxGroups];
   unsigned xrelu;
+  // deferred BN-backward prologue of the dY groups (see ConvArgs::gy; halo weight-gradient only)
+  const uint16_t* gy[kMaxGroups];
+  const float* gs[kMaxGroups];
+  const float* gk[kMaxGroups];
+  unsigned grelu;
 };
 
 // conv_wgrad_gemm.hip: LDS-tiled weight-gradient GEMM (LDS-DMA staging, transposed fragment reads)
@@ -72,8 +87,11 @@ void conv_set_halo(int on);
 void conv_set_small_halo(int on);   // opt-in 128-pixel halo tiles (tests / A-B)
 void conv_set_wlds(int on);         // halo kernels' weights in LDS (opt-in WL) or global memory (default)
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
-bool conv_uses_halo(const ConvGeom& g, bool trans);
-long conv_stat_blocks(const ConvGeom& g, bool trans = false);   // trans: strided transposed (conv_igemm's flag)
+// bwd: the launch carries a deferred BN-backward prologue (ConvArgs::gy): no PIPE variant, larger table
+bool conv_uses_halo(const ConvGeom& g, bool trans, bool bwd = false);
+long conv_stat_blocks(const ConvGeom& g, bool trans = false, bool bwd = false);   // trans: conv_igemm's flag
+// whether conv_wgrad runs the halo weight-gradient kernel (the only one with the BN-backward prologue)
+bool conv_wgrad_uses_halo(const ConvGeom& g, bool trans);
 // returns 0, or an error code (conv_error_string) -- the bindings raise it as a Python error
 int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s);
 const char* conv_error_string(int rc);
@@ -88,10 +106,12 @@ int conv_gemm_num_cfgs();
 int conv_gemm_cfg_tco(int rows);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
 int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
-int conv_wgrad_replicas(const ConvGeom& g, bool trans);
+int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd = false);   // bwd: see conv_wgrad
 // xc / xrelu: the deferred-BN prologue of the x groups (see ConvArgs; xc may be nullptr)
+// gy/gs/gk/grelu: the deferred BN-backward prologue of the dY groups (nullable; halo kernel only)
 int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,
-               const float* const* xc, unsigned xrelu, hipStream_t s);
+               const float* const* xc, unsigned xrelu, hipStream_t s, const uint16_t* const* gy = nullptr,
+               const float* const* gs = nullptr, const float* const* gk = nullptr, unsigned grelu = 0);
 // dst[row][(t_base + t)*Cpk + c_base + c] = src[row*s_row + c*s_ch + t], row < nrow, c < nch, t < T
 void pack_weight(const float* src, uint16_t* dst, int nrow, int nch, int T, int Cpk, int Kp, int t_base,
                  int c_base, long s_row, long s_ch, hipStream_t s);

@@ -126,6 +126,73 @@ class BwdStatsHandle:
         self.relu = False
 
 
+class DeferredGrad:
+    """A BatchNorm(+ReLU) data-gradient that was never written: dy = bwd(dz, y) per channel (``coef`` =
+    the finalized backward coefficients, ``stats`` the forward scale/shift for the ReLU test).  The BN
+    backward returns an uninitialised ``token`` tensor of dy's shape in its place; the conv that produced
+    y (the only reader of y, guaranteed by the executor) either rebuilds dy while staging its data- and
+    weight-gradient loads (the halo kernels' BN-backward prologue: the mirror of :class:`Deferred`), or
+    :func:`resolve` writes the token (one ``bn_act_bwd_apply`` pass) and it is a plain gradient again."""
+    __slots__ = ('dz', 'y', 'stats', 'coef', 'relu', 'token', 'claims', 'done')
+
+    def __init__(self, dz, y, stats, coef, relu, token, claims):
+        self.dz, self.y, self.stats, self.coef, self.relu, self.token = dz, y, stats, coef, relu, token
+        self.claims, self.done = claims, False
+
+
+_DEFERRED = {}   # token data_ptr -> DeferredGrad (alive between a BN backward and its producers' backward)
+# env MSP_DEFER_DY=0: every BN backward writes dy (A/B)
+DEFER_DY = os.environ.get('MSP_DEFER_DY', '1') != '0'
+_DY_CONSUMERS = {'_ConvFnBackward', '_MultiConvFnBackward'}
+
+
+def _register_deferred(dz, y, stats, coef, relu, claims):
+    token = torch.empty_like(y)
+    _DEFERRED[token.data_ptr()] = DeferredGrad(dz, y, stats, coef, relu, token, claims)
+    return token
+
+
+def peek_deferred(g):
+    """The unresolved :class:`DeferredGrad` whose token is ``g`` (None for a plain gradient)."""
+    if g is None or not _DEFERRED:
+        return None
+    d = _DEFERRED.get(g.data_ptr())
+    if d is None or d.done or d.token.shape != g.shape:
+        return None
+    return d
+
+
+def claim_deferred(d):
+    """A producer consumed ``d`` through its staging prologue (one of the BN's ``claims`` readers)."""
+    d.claims -= 1
+    if d.claims <= 0:
+        _DEFERRED.pop(d.token.data_ptr(), None)
+
+
+def resolve(g):
+    """Make ``g`` a plain gradient: write a deferred token (one apply pass) the first time it is asked."""
+    d = peek_deferred(g)
+    if d is not None:
+        C = require()
+        Cp = d.y.shape[-1]
+        C.bn_act_bwd_apply(d.dz, d.y, d.stats, d.coef, d.token, d.y.numel() // Cp, Cp, d.relu)
+        d.done = True
+        d.claims -= 1
+        if d.claims <= 0:
+            _DEFERRED.pop(d.token.data_ptr(), None)
+    return g
+
+
+def clear_deferred():
+    """Step boundary: drop every token (all have been claimed or resolved by the end of backward)."""
+    _DEFERRED.clear()
+
+
+def _dy_deferrable(ts):
+    """Every input is produced by a conv node that knows deferred data-gradients (it claims or resolves)."""
+    return all(t.grad_fn is not None and type(t.grad_fn).__name__ in _DY_CONSUMERS for t in ts)
+
+
 class _Pending:
     """SyncBN statistic exchanges waiting to leave as ONE collective.
 
@@ -229,6 +296,7 @@ def flush_pending():
     """Issue every parked exchange (step boundaries; idempotent)."""
     _FWD.flush()
     _BWD.flush()
+    clear_deferred()
 
 
 def _world(group):
@@ -324,6 +392,7 @@ class _BNAct(torch.autograd.Function):
             count = float(P)
         ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
         ctx.defer_bwd = defer_bwd
+        ctx.defer_dy = bool(mode[2]) if len(mode) > 2 else False
         ctx.handle = handle if training else None
         if ctx.handle is not None:
             handle.y, handle.stats, handle.relu, handle.part = y, stats, relu, None
@@ -368,13 +437,15 @@ class _BNAct(torch.autograd.Function):
         g_t = st.weight_sink if st.weight_sink is not None else dgamma
         b_t = st.bias_sink if st.bias_sink is not None else dbeta
         coef = torch.empty(3, Cp, dtype=torch.float32, device=dev)
+        defer_dy = ctx.defer_dy and any(ctx.needs_input_grad[9:])
         if park:
-            dy = torch.empty_like(y)
             relu, count, hook = ctx.relu, ctx.count, st.ready_hook
+            dy = _register_deferred(dz, y, stats, coef, relu, ctx.k) if defer_dy else torch.empty_like(y)
 
             def job(sums, st=st, Cp=Cp, P=P):
                 C.bn_bwd_finalize(sums, st.C, Cp, count, stats, g_t, b_t, coef, 1.0 / world)
-                C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, relu)
+                if not defer_dy:
+                    C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, relu)
                 if hook is not None:
                     hook([t for t in (st.weight, st.bias) if t is not None])
             _BWD.add(sums, st.group, job, dy.data_ptr())
@@ -400,8 +471,11 @@ class _BNAct(torch.autograd.Function):
                 b_t[:st.C] += tot[0][:st.C]
         # no input needs a data-gradient (the first DUCK's in_bn over the image): only dgamma/dbeta
         need_dy = any(ctx.needs_input_grad[9:])
-        dy = torch.empty_like(y) if need_dy else None
-        if need_dy:
+        dy = None
+        if need_dy and defer_dy:   # the producing conv rebuilds dy in its staging (or resolves it)
+            dy = _register_deferred(dz, y, stats, coef, ctx.relu, ctx.k)
+        elif need_dy:
+            dy = torch.empty_like(y)
             C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
         if h is not None:   # break the output -> node -> ctx -> handle -> output cycle now
             h.y = h.stats = h.part = None
@@ -445,7 +519,9 @@ def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=Non
     ts, coefs, mask = split_inputs(xs)
     if defer_bwd and training and _world(st.group) > 1:
         _check_deferrable(ts)
-    out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd), (coefs, mask),
+    # the data-gradient stays deferred (DeferredGrad) when every input is a conv output read by this BN only
+    defer_dy = DEFER_DY and defer_bwd and training and not coefs and _dy_deferrable(ts)
+    out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd, defer_dy), (coefs, mask),
                               st.weight, st.bias, *ts)
     return Deferred(out, stats, relu) if deferred else out
 

@@ -203,6 +203,38 @@ def _taps(tl):
     return [t[0] for t in tl], [t[1] for t in tl]
 
 
+def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
+    """Deferred BN data-gradients among this launch's incoming gradient groups (``ops.bn.DeferredGrad``).
+
+    Returns (gys, bwd) where ``gys`` are the tensors the kernels read (dz for a deferred group) and
+    ``bwd`` = (gy, gs, gk, grelu, claims) for the kernels' BN-backward staging prologue -- or None, when
+    no group is deferred or a launch of this plan cannot rebuild dY (only the non-chunked stride-1 halo
+    data-gradient and the halo weight-gradient can): then every deferred group is resolved (written)
+    and the launches see plain gradients, exactly as before."""
+    from .bn import peek_deferred, resolve
+    ds = [peek_deferred(g) for g in grads]
+    if not any(d is not None for d in ds):
+        return list(grads), None
+    C = require()
+    ok = not plan.transposed and plan.stride == 1 and plan.bias is None
+    if ok and dgrad:
+        ok = bool(C.conv_uses_halo(dims_d, taps_d[0], taps_d[1], False, True))
+    if ok:
+        ok = bool(C.conv_wgrad_uses_halo(dims_w, taps_w[0], taps_w[1], False))
+    if not ok:
+        return [resolve(g) for g in grads], None
+    gys, gy, gs, gk, grelu = [], [], [], [], 0
+    for i, (g, d) in enumerate(zip(grads, ds)):
+        if d is None:
+            gys.append(g)
+            gy.append(None); gs.append(None); gk.append(None)
+        else:
+            gys.append(d.dz)
+            gy.append(d.y); gs.append(d.stats); gk.append(d.coef)
+            grelu |= int(bool(d.relu)) << i
+    return gys, (gy, gs, gk, grelu, [d for d in ds if d is not None])
+
+
 class _ConvFn(torch.autograd.Function):
     # pro = (coefs, relu mask): deferred-BN prologue of the input groups (ops.bn.Deferred); the same
     # prologue runs again in the weight-gradient staging, so z never exists in HBM
@@ -255,28 +287,38 @@ class _ConvFn(torch.autograd.Function):
         for g in grads[:plan.Go]:
             gys.append(torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None
                        else g.contiguous())
+        need_dx = any(ctx.needs_input_grad[5:5 + ctx.nx])
+        Kp_d = plan.Kp_d
+        dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
+        if plan.transposed:
+            dy, dx = _taps(plan.taps_fwd)
+            trans = False
+        else:
+            dy, dx = _taps(plan.taps_bwd)
+            trans = plan.stride > 1
+        # deferred BN data-gradients: rebuilt in the staging of both launches below, or resolved here
+        gys, bwd = _bwd_operands(gys, plan, dims_d, (dy, dx), plan.fwd_dims(n, ih, iw, oh, ow),
+                                 _taps(plan.taps_fwd), dgrad=need_dx)
+        bk = {} if bwd is None else dict(gy=bwd[0], gs=bwd[1], gk=bwd[2], grelu=bwd[3])
         dxs = [None] * ctx.nx
-        if any(ctx.needs_input_grad[5:5 + ctx.nx]):
+        if need_dx:
             wd, Kp_d = plan.pack_dgrad(dev)
             dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
-            dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
-            if plan.transposed:
-                dy, dx = _taps(plan.taps_fwd)
-                trans = False
-            else:
-                dy, dx = _taps(plan.taps_bwd)
-                trans = plan.stride > 1
             h = ctx.bn_handle
             if h is not None and h.y is not None and not trans:
                 # dL/dx is the BN output's gradient: emit the BN backward partials in the epilogue
-                nblk = C.conv_stat_blocks(dims_d, dy, dx)
+                nblk = C.conv_stat_blocks(dims_d, dy, dx, False, bwd is not None)
                 part = torch.empty(nblk, 2, plan.Gi * plan.Cgi, dtype=torch.float32, device=dev)
-                C.conv_fwd_bn(gys, wd, dxs, part, dims_d, dy, dx, h.y, h.stats, h.relu)
+                C.conv_fwd_bn(gys, wd, dxs, part, dims_d, dy, dx, h.y, h.stats, h.relu, **bk)
                 h.part = part
             else:
-                C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans)
+                C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans, **bk)
             ctx.bn_handle = None
-        wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev, ctx.pro)
+        wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev, ctx.pro, bk)
+        if bwd is not None:
+            from .bn import claim_deferred
+            for d in bwd[4]:
+                claim_deferred(d)
         bgrad = None
         if plan.bias is not None:
             bg = gys[0].view(-1, plan.Cgo)[:, :plan.co_l].float().sum(0)
@@ -293,8 +335,10 @@ class _ConvFn(torch.autograd.Function):
         return tuple(out)
 
 
-def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0)):
+def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None):
+    """``bk``: the BN-backward prologue kwargs of the dY groups (see :func:`_bwd_operands`)."""
     C = require()
+    bk = bk or {}
     coefs, rmask = pro
     n, ih, iw, oh, ow = shape
     res = []
@@ -319,9 +363,9 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0)):
     dims = plan.fwd_dims(n, ih, iw, oh, ow)
     dy, dx = _taps(plan.taps_fwd)
     KT = plan.T * plan.Cip
-    nrep = C.conv_wgrad_replicas(dims, dy, dx, False)   # split-K dW slabs, summed in fixed order on unpack
+    nrep = C.conv_wgrad_replicas(dims, dy, dx, False, bool(bk))   # split-K dW slabs, summed in fixed order
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
-    C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask)
+    C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask, **bk)
     cin_tot = plan.Gi * plan.ci_l
     for b, nd in zip(plan.branches, need):
         if not nd:
@@ -383,19 +427,26 @@ class _MultiConvFn(torch.autograd.Function):
             gys = [torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None else g.contiguous()
                    for g in grads[o:o + plan.Go]]
             o += plan.Go
-            per_plan.append(gys)
+            dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, plan.Kp_d, plan.stride]
+            dy, dx = _taps(plan.taps_bwd)
+            gys, bwd = _bwd_operands(gys, plan, dims_d, (dy, dx), plan.fwd_dims(n, ih, iw, oh, ow),
+                                     _taps(plan.taps_fwd), dgrad=ctx.needs_input_grad[3])
+            bk = {} if bwd is None else dict(gy=bwd[0], gs=bwd[1], gk=bwd[2], grelu=bwd[3])
+            per_plan.append((gys, bk, bwd))
             if ctx.needs_input_grad[3]:
                 wd, Kp_d = plan.pack_dgrad(dev)
                 first = dxt is None
                 if first:
                     dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
-                dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, Kp_d, plan.stride]
-                dy, dx = _taps(plan.taps_bwd)
-                C.conv_fwd(gys, wd, [dxt], None, None, dims_d, dy, dx, False, accumulate=not first)
+                C.conv_fwd(gys, wd, [dxt], None, None, dims_d, dy, dx, False, accumulate=not first, **bk)
         wgrads = []
-        for plan, gys in zip(ctx.plans, per_plan):
+        for plan, (gys, bk, bwd) in zip(ctx.plans, per_plan):
             oh, ow = plan.out_hw(ih, iw)
-            wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro)
+            wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro, bk)
+            if bwd is not None:
+                from .bn import claim_deferred
+                for d in bwd[4]:
+                    claim_deferred(d)
             if plan.ready_hook is not None:
                 plan.ready_hook([b.weight for b in plan.branches])
         ctx.plans = None

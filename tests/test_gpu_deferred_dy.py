@@ -1,0 +1,120 @@
+"""Deferred BatchNorm data-gradient (``ops.bn.DeferredGrad``): a training BN whose input is a conv output
+read by that BN only never writes dL/dy; the producing conv rebuilds it while staging its data-gradient
+and weight-gradient loads (the halo kernels' BN-backward prologue, ``csrc/conv.hip`` BWD), or resolves it
+(one ``bn_act_bwd_apply`` pass) when a launch cannot.  Every gradient must match the materialised path;
+where the two paths plan identical launches the results are bitwise equal."""
+import pytest
+import torch
+import torch.nn as nn
+
+from medical_segmentation_pytorch_amd.ops import bn as bnmod
+from medical_segmentation_pytorch_amd.ops.bn import BNState, BwdStatsHandle, bn_act, materialize
+from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, conv
+from medical_segmentation_pytorch_amd.ops.fm import to_fm_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-20)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+CASES = [
+    # cin, co, (kh, kw), dilation, n 3x3 groups, n 1x1 groups, (n, h, w), chain (BN1 -> conv: BNE epilogue too)
+    (17, 17, (3, 3), 1, 1, 0, (2, 24, 32), False),
+    (17, 17, (3, 3), 1, 1, 0, (2, 24, 32), True),
+    (17, 17, (3, 3), 2, 1, 0, (2, 24, 32), True),
+    (17, 17, (3, 3), 3, 1, 0, (2, 24, 32), False),
+    (17, 17, (1, 7), 1, 1, 0, (2, 24, 32), True),
+    (17, 17, (7, 1), 1, 1, 0, (2, 24, 32), False),
+    (34, 34, (3, 3), 1, 1, 0, (2, 24, 32), True),      # 40 padded channels (L2 width)
+    (17, 17, (3, 3), 1, 1, 1, (2, 24, 32), False),     # Go = 2: 3x3 + 1x1 at the centre tap, both deferred
+    (17, 17, (3, 3), 1, 5, 3, (2, 24, 32), False),     # DUCK fused-8: chunked data-gradient -> resolved
+    (64, 64, (3, 3), 1, 1, 0, (2, 16, 16), False),     # >= 64 channels: GEMM kernels -> resolved
+]
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_deferred_bn_data_gradient(gpu, case, monkeypatch):
+    cin, co, (kh, kw), dil, n3, n1, (n, h, w), chain = case
+    torch.manual_seed(5)
+    convs = [nn.Conv2d(cin, co, (kh, kw), 1, (dil * (kh // 2), dil * (kw // 2)), (dil, dil), bias=False).to(gpu)
+             for _ in range(n3)]
+    convs += [nn.Conv2d(cin, co, 1, bias=False).to(gpu) for _ in range(n1)]
+    bns = [nn.BatchNorm2d(co).to(gpu) for _ in range(n3 + n1)]
+    bn1 = nn.BatchNorm2d(cin).to(gpu)
+    with torch.no_grad():
+        for b in bns + [bn1]:
+            b.weight.uniform_(0.5, 1.5)
+            b.bias.uniform_(-0.5, 0.5)
+    T = kh * kw
+    branches = [Branch(m.weight, g, 0, T) for g, m in enumerate(convs[:n3])]
+    branches += [Branch(m.weight, n3 + g, T // 2, 1) for g, m in enumerate(convs[n3:])]
+    x0 = to_fm_reference(_bf(torch.randn(n, cin, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(3))))
+    gs = [to_fm_reference(_bf(torch.randn(n, co, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(9 + g))))
+          for g in range(n3 + n1)]
+    res, resolved = [], []
+    for defer in (False, True):
+        monkeypatch.setattr(bnmod, 'DEFER_DY', defer)
+        for m in convs + bns + [bn1]:
+            for p in m.parameters():
+                p.grad = None
+        # the running statistics must not drift between the two passes
+        state = [{k: v.clone() for k, v in b.state_dict().items()} for b in bns + [bn1]]
+        plan = ConvPlan(kh, kw, cin, co, branches, padding=(dil * (kh // 2), dil * (kw // 2)), dilation=(dil, dil),
+                        Go=n3 + n1)
+        x = x0.clone().requires_grad_(True)
+        hdl = None
+        if chain:   # BN1 -> this conv only: its data-gradient also emits BN1's backward partials (BNE)
+            hdl = BwdStatsHandle()
+            xin = bn_act([x], BNState.from_module(bn1), True, True, None, handle=hdl, deferred=True, defer_bwd=True)
+        else:
+            xin = x
+        ys, _ = conv(plan, [xin], want_stats=False, bn_handle=hdl)
+        zs = [materialize(bn_act([y], BNState.from_module(b), True, True, None, deferred=True, defer_bwd=True))
+              for y, b in zip(ys, bns)]
+        n_before = len(bnmod._DEFERRED)
+        torch.autograd.backward(zs, gs)
+        torch.cuda.synchronize()
+        resolved.append(len(bnmod._DEFERRED))
+        res.append([x.grad.float().clone()] + [m.weight.grad.clone() for m in convs] +
+                   [t.grad.clone() for b in bns for t in (b.weight, b.bias)])
+        for b, sd in zip(bns + [bn1], state):
+            b.load_state_dict(sd)
+        assert n_before == 0
+        bnmod.clear_deferred()
+    for i, (a, b) in enumerate(zip(res[1], res[0])):
+        assert _rel(a, b) < 1e-3, (i, _rel(a, b))
+    # every token was claimed by its producer or resolved: nothing is left behind after the backward
+    assert resolved == [0, 0], resolved
+
+
+def test_deferred_tokens_reach_the_halo_prologue(gpu, monkeypatch):
+    """The narrow single-group case really consumes the token in the kernels (no resolve pass): with
+    the apply launch disabled, the deferred path still produces the materialised path's gradients."""
+    C = bnmod.require()
+    calls = []
+    orig = bnmod.resolve
+
+    def spy(g):
+        calls.append(bnmod.peek_deferred(g) is not None)
+        return orig(g)
+    monkeypatch.setattr(bnmod, 'resolve', spy)
+    import medical_segmentation_pytorch_amd.ops.bn as b2
+    assert b2.resolve is spy
+    torch.manual_seed(1)
+    m = nn.Conv2d(17, 17, 3, 1, 1, bias=False).to(gpu)
+    bnm = nn.BatchNorm2d(17).to(gpu)
+    plan = ConvPlan(3, 3, 17, 17, [Branch(m.weight, 0, 0, 9)], padding=(1, 1))
+    x = to_fm_reference(_bf(torch.randn(2, 17, 24, 32, device=gpu))).requires_grad_(True)
+    dims = plan.fwd_dims(2, 24, 32, 24, 32)
+    assert C.conv_wgrad_uses_halo(dims, [t[0] for t in plan.taps_fwd], [t[1] for t in plan.taps_fwd], False)
+    (y,), _ = conv(plan, [x])
+    z = materialize(bn_act([y], BNState.from_module(bnm), True, True, None, deferred=True, defer_bwd=True))
+    z.backward(torch.randn_like(z))
+    assert not any(calls), 'the single 17-channel 3x3 conv must consume the deferred gradient in its kernels'
+    assert x.grad is not None and torch.isfinite(x.grad.float()).all()
