@@ -345,7 +345,7 @@ class _BNAct(torch.autograd.Function):
     def forward(ctx, st: BNState, relu: bool, training: bool, part_info, handle, mode, pro, gamma, beta, *xs):
         C = require()
         ctx.set_materialize_grads(False)   # no zero-filled grad for the non-differentiable stats output
-        deferred, defer_bwd = mode
+        deferred, defer_bwd = mode[0], mode[1]
         xs = [x.contiguous() for x in xs]
         coefs, rmask = pro
         y0 = xs[0]
