@@ -100,6 +100,8 @@ def test_deferred_tokens_reach_the_halo_prologue(gpu, monkeypatch):
     calls = []
     orig = bnmod.resolve
 
+    monkeypatch.setattr(bnmod, 'DEFER_DY', True)
+
     def spy(g):
         calls.append(bnmod.peek_deferred(g) is not None)
         return orig(g)
