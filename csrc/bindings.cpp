@@ -850,8 +850,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_uses_gemm", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans) {
     return conv_gemm_ok(make_geom(dims, dy, dx), trans);
   });
-  m.def("conv_set_small_halo", [](bool on) { conv_set_small_halo(on ? 1 : 0); });
-  m.def("conv_set_wlds", [](bool on) { conv_set_wlds(on ? 1 : 0); });
   m.def("conv_set_phase", [](bool on) { conv_set_phase(on ? 1 : 0); });
   m.def("pack_weight", &pack_weight_t);
   m.def("unpack_wgrad", &unpack_wgrad_t, py::arg("src"), py::arg("dst"), py::arg("nrow"), py::arg("nch"),

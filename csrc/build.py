@@ -20,9 +20,8 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, 'medical_segmentation_pytorch_amd')
-# MSP_BUILD_VARIANT=ko: a profiling build with the halo kernels' perf knock-outs compiled in
-# (-DMSP_HALO_KNOCKOUTS=1; selected at run time by env MSP_HALO_DBG), written to
-# build/ko/_C.so and loaded instead of the product extension when env MSP_C_SO points at it
+# MSP_BUILD_VARIANT=<name>: a side build (e.g. with extra -D flags in MSP_BUILD_DEFINES) written to
+# build/<name>/_C.so and loaded instead of the product extension when env MSP_C_SO points at it
 VARIANT = os.environ.get('MSP_BUILD_VARIANT', '')
 BUILD = os.path.join(ROOT, 'build', 'csrc' + (f'_{VARIANT}' if VARIANT else ''))
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950').split(';')[0]
@@ -44,8 +43,8 @@ def write_ninja(jobs):
     kernels = sorted(f for f in os.listdir(HERE) if f.endswith('.hip'))
     common = f'-O3 -fPIC -std=c++17 -D_GLIBCXX_USE_CXX11_ABI={abi} -I{HERE}'
     kflags = f'{common} --offload-arch={ARCH} -munsafe-fp-atomics -Wno-unused-result'
-    if VARIANT == 'ko':
-        kflags += ' -DMSP_HALO_KNOCKOUTS=1'
+    if VARIANT:
+        kflags += ' ' + os.environ.get('MSP_BUILD_DEFINES', '')
     bflags = (f'{common} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_C '
               f'-DTORCH_API_INCLUDE_EXTENSION_H -I{ROCM}/include -I{pyinc} -I{pybind11.get_include()} '
               + ' '.join(f'-isystem {p}' for p in tinc) + ' -Wno-deprecated-declarations')

@@ -854,21 +854,11 @@ struct HaloGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, pitch, CC, nch, KS;
   int xtab;                          // deferred-BN prologue present: LDS coefficient table (3 x Cip fp32)
   int mi, pipe, nj;                  // row-group size (16*mi rows), PIPE mode, pixel columns per wave
-  int wl;                            // non-PIPE: the packed weights staged in LDS (WL instantiation)
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
-  int dbg;                           // perf knock-outs (env MSP_HALO_DBG; 0 in production): 1 no y stores,
-                                     // 2 no staging loads, 4 no MFMAs, 8 no staging, 16 no epilogue,
-                                     // 32 no weight (A) loads
   float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
 };
 
-// Perf knock-outs of the halo kernel (profiling only): compiled in with -DMSP_HALO_KNOCKOUTS=1 and
-// selected by env MSP_HALO_DBG; in production builds HALO_KO is the constant false and folds away.
-#ifndef MSP_HALO_KNOCKOUTS
-#define MSP_HALO_KNOCKOUTS 0
-#endif
-#define HALO_KO(hg, bit) (MSP_HALO_KNOCKOUTS && ((hg).dbg & (bit)))
 
 constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel) units each)
 constexpr int kHaloWaves = 4;
@@ -890,14 +880,11 @@ constexpr int kPipeMaxLds = 78 * 1024;   // PIPE: tile + stats + prologue table 
 // registers while the current one runs on the MFMAs, and the accumulators persist across chunks
 // (single row group).
 
-// WL (whole-input, non-PIPE; opt-in, env MSP_HALO_WLDS=1): the block's packed weight rows are staged in
-// LDS next to the input tile, so the k-loop reads A from LDS instead of one global (L2) load per k-step
-// with a one-step prefetch (measured neutral: see halo_wlds_enabled)
 // BWD: the data-gradient staging rebuilds dY from (dz, y) per input group (ConvArgs::gy, the deferred
-// BN-backward prologue: no bn_act_bwd_apply pass writes dY); never with PIPE / WL
-template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool WL = false, bool BWD = false>
+// BN-backward prologue: no bn_act_bwd_apply pass writes dY); never with PIPE
+template <int MI, int NJ, bool CHUNKED, bool BNE = false, bool PIPE = false, bool BWD = false>
 __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 && NJ <= 4) ? 4 : 3)) void conv_halo_kernel(ConvArgs a, HaloGeom hg) {
-  static_assert(!(BWD && (PIPE || WL)), "BN-backward prologue: standard / chunked staging only");
+  static_assert(!(BWD && PIPE), "BN-backward prologue: standard / chunked staging only");
   extern __shared__ uint4 halo_smem[];
   uint16_t* tile = reinterpret_cast<uint16_t*>(halo_smem);
   __shared__ int s_ua[CHUNKED ? kHaloMaxKS * 4 : 1];
@@ -956,7 +943,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   // the next tile).  Row pitch = an odd number of 16-B slots.
   uint16_t* sA = reinterpret_cast<uint16_t*>(s_coef + (hg.xtab ? 3 * Cip : 0));
   const int pitchA = (4 * hg.KS + 1) * 8;
-  if (PIPE || WL) {
+  if (PIPE) {
     const int rowsA = ((rows + 16 * MI - 1) / (16 * MI)) * 16 * MI;
     const int per_row = 4 * hg.KS;
     for (int e = tid; e < rowsA * per_row; e += 64 * kHaloWaves) {
@@ -1009,7 +996,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
         const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
         dst[u] = __mul24(hp, hg.pitch) + c8 * 8;
-        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
+        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
           const int ci = c0 + c8 * 8;
           const int pix = iy * g.IW + ix;
           if (g.Gi == 1) {
@@ -1105,7 +1092,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       if (tid + u * 64 * kHaloWaves < total) {
         const int iy = iy0 + hy, ix = ix0 + hx;
         pd[u] = __mul24(hp, hg.pitch) + c8 * 8;
-        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
+        if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
           const int ci = c8 * 8;
           const int pix = iy * g.IW + ix;
           pd[u] |= (c8 + 1) << 16;
@@ -1183,7 +1170,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
     int c8 = tid % C8c, hp = tid / C8c;
     int hy = hp / hg.HWD, hx = hp - hy * hg.HWD;
     const int iy0 = ty0 + hg.ey0, ix0 = tx0 + hg.ex0;
-    for (int base = tid; base < ((HALO_KO(hg, 8)) ? 0 : total); base += 64 * kHaloWaves * kHaloLd) {
+    for (int base = tid; base < total; base += 64 * kHaloWaves * kHaloLd) {
       uint4 v[kHaloLd];
       uint4 yv[BWD ? kHaloLd : 1];
       int dst[kHaloLd], cc[kHaloLd];
@@ -1196,7 +1183,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         if (base + u * 64 * kHaloWaves < total) {
           const int iy = iy0 + hy, ix = ix0 + hx;
           dst[u] = __mul24(hp, hg.pitch) + c8 * 8;
-          if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW && !(HALO_KO(hg, 2))) {
+          if ((unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
             const int ci = c8 * 8;
             const int pix = iy * g.IW + ix;
             cc[u] = c8;
@@ -1287,15 +1274,12 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         }
       }
       auto load_a = [&](uint4* A, int ks) {
-        if (HALO_KO(hg, 32)) {   // knock-out: no weight loads (register-made A fragments)
-#pragma unroll
-          for (int i = 0; i < MI; ++i) A[i] = make_uint4(ks, lr, i, 0);
-        } else if (CHUNKED) {
+        if (CHUNKED) {
           const int ua = s_ua[4 * ks + lg];
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             A[i] = ua >= 0 ? *reinterpret_cast<const uint4*>(wrow[i] + ua + c0) : make_uint4(0, 0, 0, 0);
-        } else if (PIPE || WL) {
+        } else if (PIPE) {
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             A[i] = *reinterpret_cast<const uint4*>(sA + (co0 + 16 * i + lr) * pitchA + 32 * ks + 8 * lg);
@@ -1314,28 +1298,15 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         uint4 B[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
-        if (!(HALO_KO(hg, 4))) {
 #pragma unroll
-          for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
-        } else {
-          acc[0][0][0] += __uint_as_float(A[0].x ^ B[0].y) * 1e-30f;   // keep the loads alive
-        }
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
         if (more) {
 #pragma unroll
           for (int i = 0; i < MI; ++i) A[i] = An[i];
         }
       }
-    }
-    if (HALO_KO(hg, 16)) {   // knock-out: no epilogue (keep the accumulators alive)
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) t += acc[i][j][0] + acc[i][j][3];
-      if (t == 1234.5f) a.stat_part[0] = t;
-      continue;
     }
     // epilogue: bias, bf16 round (v_cvt_pk), 8-B NHWC stores, per-row (sum, sum^2) of the stored
     // values reduced over the 16 pixel lanes with DPP row adds.
@@ -1420,8 +1391,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
             v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
             v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
-          if (!(HALO_KO(hg, 1)))
-            *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             cs[i][r] += v[r];
@@ -1448,7 +1418,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
             o[2] += __uint_as_float(ov.y << 16); o[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
           const uint32_t lo = pack2(o[0], o[1]), hi = pack2(o[2], o[3]);
-          if (!(HALO_KO(hg, 1))) *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(yb[i] + pm) = make_uint2(lo, hi);
           const float v0 = __uint_as_float(lo << 16), v1 = __uint_as_float(lo & 0xffff0000u);
           const float v2 = __uint_as_float(hi << 16), v3 = __uint_as_float(hi & 0xffff0000u);
           cs[i][0] += v0; cs[i][1] += v1; cs[i][2] += v2; cs[i][3] += v3;
@@ -1541,14 +1511,10 @@ int conv_rows_alloc(int rows) {
   return r;
 }
 
-static int g_pipe_mode = -1;   // env MSP_HALO_PIPE=0 disables the persistent pipelined halo kernels
-static bool pipe_enabled() {
-  if (g_pipe_mode < 0) { const char* e = getenv("MSP_HALO_PIPE"); g_pipe_mode = (e == nullptr || e[0] != '0') ? 1 : 0; }
-  return g_pipe_mode == 1;
-}
-// PIPE row-group size: MI 2 or 3 at NJ 4 -- accumulators that leave room for the kPipeLd prefetch
-// registers at 2 blocks/CU without spilling (NJ 8 and MI 4 spill there)
-static int pipe_pick_mi(int rows) { return rows <= 32 ? 2 : 3; }
+// PIPE (persistent, next tile prefetched in registers) runs the MI 3 / NJ 4 row groups of thin-halo 3x3
+// convs (the L2 3x3s): there its 256-pixel tile is also the standard kernel's; measured slower for the
+// MI <= 2 layers (which lose their 512-pixel tile) and the 1x7 / dilated halos.  MI 3 at NJ 4 leaves room
+// for the kPipeLd prefetch registers at 2 blocks/CU without spilling (NJ 8 and MI 4 spill there).
 static size_t pipe_a_bytes(int rows, int mi, int ks) {
   return (size_t)cdiv(rows, 16 * mi) * 16 * mi * (4 * ks + 1) * 16;
 }
@@ -1572,57 +1538,21 @@ static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
 // MI <= 2, else 4); TW in {16, 32, 64} minimising (tiles) x (stores + halo loads).  The input is staged
 // whole (one chunk, LDS <= 64 KB) or -- single row group only -- in chunks of CC channels (CC | Cip, a
 // chunk's staging fits the kHaloLd registers per thread), widest CC first.
-// env MSP_HALO_NJ4=1: 256-pixel tiles (NJ = 4) for MI <= 2 too -- half the accumulators, 4 blocks / CU
-// instead of 3 (more blocks in different phases overlap staging, MFMAs and epilogue stores; A/B)
-static int g_nj4 = -1;
-static bool halo_nj4() {
-  if (g_nj4 < 0) { const char* e = getenv("MSP_HALO_NJ4"); g_nj4 = (e != nullptr && e[0] == '1') ? 1 : 0; }
-  return g_nj4 == 1;
-}
-static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe && !halo_nj4()) ? 8 : 4; }
-// env MSP_HALO_SMALL=1 enables the 128-pixel (NJ 2) halo tiles for inputs too wide for 256 pixels.  Off by
-// default: measured 1.3 % slower per step (L4 3x3 fwd -10 %, but dgrad +8 %, 1x7 fwd +26 %: at NJ 2 each
-// B fragment feeds only MI MFMAs and the halo ring is 40 % of the tile; profiles/r02/conv_bench_L4_small.log)
-static int g_small_tile = -1;
-static bool halo_small_tile_enabled() {
-  if (g_small_tile < 0) { const char* e = getenv("MSP_HALO_SMALL"); g_small_tile = (e != nullptr && e[0] == '1') ? 1 : 0; }
-  return g_small_tile == 1;
-}
-
-// env MSP_HALO_WLDS=1: the WL instantiations (weights in LDS).  Off by default: measured neutral to
-// slower (L1 3x3 fwd 0.535 -> 0.562 ms, 1x7 0.459 -> 0.435, the rest within noise; bench 505.7 img/s
-// either way; profiles/r03/conv_bench_v10_wl_{on,off}_bs128.log) -- the one-step global prefetch of A
-// already hides the L2 latency in the short (7-k-step) L1/L2 loops.
-static int g_wlds = -1;
-static bool halo_wlds_enabled() {
-  if (g_wlds < 0) { const char* e = getenv("MSP_HALO_WLDS"); g_wlds = (e != nullptr && e[0] == '1') ? 1 : 0; }
-  return g_wlds == 1;
-}
-
+static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe) ? 8 : 4; }
 static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
   return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
 }
 
 // LDS cap of a halo tile + its stats rows + the prologue table.  Two blocks per CU hold up to ~76 KB of
 // dynamic LDS each (160 KB per CU minus the static tap tables); 64 KB measured 0.6 % slower per step
-// (L3 3x3 d3 leaves the gather kernel: fwd 0.49 -> 0.28 ms).  env MSP_HALO_TILE_KB overrides (A/B).
-static size_t halo_tile_cap() {
-  static long kb = -1;
-  if (kb < 0) {
-    const char* e = getenv("MSP_HALO_TILE_KB");
-    kb = (e != nullptr && atol(e) >= 16 && atol(e) <= 78) ? atol(e) : kHaloTileKB;
-  }
-  return (size_t)kb * 1024;
-}
+// (L3 3x3 d3 leaves the gather kernel: fwd 0.49 -> 0.28 ms).
+static size_t halo_tile_cap() { return (size_t)kHaloTileKB * 1024; }
 
 // Fallback row-group size of the halo kernel.  conv_pick_mi's MI <= 2 comes with the 512-pixel (NJ = 8)
 // tile; when that tile (+ halo) does not fit the LDS cap the 256-pixel MI 3/4 tile often does, instead of
 // falling back to the gather kernel (L3 5x3x3 + 3x1x1 DUCK split, 216 rows x 72 ch: 1.46 -> 0.57 ms fwd).
-// env MSP_HALO_MI_RULE=0 disables the fallback (A/B).
 static int halo_fallback_mi(int rows) {
-  static int rule = -1;
-  if (rule < 0) { const char* e = getenv("MSP_HALO_MI_RULE"); rule = (e != nullptr && e[0] == '0') ? 0 : 1; }
-  if (!rule || conv_pick_mi(rows) > 2) return 0;
+  if (conv_pick_mi(rows) > 2) return 0;
   return cdiv(rows, 48) * 48 <= cdiv(rows, 64) * 64 ? 3 : 4;
 }
 
@@ -1639,25 +1569,21 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg, bool bwd =
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
   const int C8 = Cip / 8;
-  // try 0: PIPE (whole input, halo tile within the prefetch registers); try 1: the standard kernels
-  // PIPE pays where its 256-pixel tile is also the standard kernel's (MI 3) and the 3x3 halo is thin;
-  // measured slower for the MI<=2 layers (which lose their 512-pixel tile) and the 1x7 / dilated halos
-  // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi); try 3: a
-  // 128-pixel tile (NJ = 2) for inputs too wide for a 256-pixel halo tile (136 channels at 44^2: the
-  // gather kernel re-reads every input pixel once per tap from L2)
-  const bool pipe_ok = !bwd && pipe_enabled() && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
+  // try 0: PIPE (whole input, halo tile within the prefetch registers); try 1: the standard kernels;
+  // try 2: the standard kernel with the fallback 256-pixel row group (halo_fallback_mi).  (Round 2's
+  // 128-pixel NJ = 2 tile for wider inputs measured 1.3 % slower per step, profiles/r02/conv_bench_L4_small.log,
+  // and is gone, as are the weights-in-LDS WL variant (neutral, profiles/r03/conv_bench_v10_wl_*) and the
+  // 256-pixel NJ = 4 tiles for MI <= 2.)
+  const bool pipe_ok = !bwd && conv_pick_mi(rows) == 3 && ey1 - ey0 == 2 && ex1 - ex0 == 2;
   const size_t tab = (bwd ? 20 : 12) * (size_t)Cip;   // prologue table bytes
-  for (int attempt = pipe_ok ? 0 : 1; attempt < 4; ++attempt) {
+  for (int attempt = pipe_ok ? 0 : 1; attempt < 3; ++attempt) {
   const bool pipe = attempt == 0;
   if (attempt == 2 && halo_fallback_mi(rows) == 0) continue;
-  if (attempt == 3 && !halo_small_tile_enabled()) break;
-  const int mi = pipe ? pipe_pick_mi(rows)
-                      : (attempt == 1 ? conv_pick_mi(rows) : (attempt == 2 ? halo_fallback_mi(rows)
-                                                                           : std::max(3, conv_pick_mi(rows))));
+  const int mi = pipe ? 3 : (attempt == 1 ? conv_pick_mi(rows) : halo_fallback_mi(rows));
   const int n_rg = cdiv(rows, 16 * mi);
-  const int nj = attempt == 3 ? 2 : halo_nj(mi, pipe);
+  const int nj = halo_nj(mi, pipe);
   const int tp = kHaloWaves * nj * 16;
-  for (int pass = 0; pass < (pipe || attempt == 3 ? 1 : 2); ++pass) {   // pass 0: whole input; 1: chunks
+  for (int pass = 0; pass < (pipe ? 1 : 2); ++pass) {   // pass 0: whole input; 1: chunks
     if (pass == 1 && (n_rg != 1 || bwd)) break;   // BWD: no chunked staging (its y registers would spill)
     for (int d = C8; d >= 1; --d) {
       if (C8 % d != 0) continue;
@@ -1695,17 +1621,6 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg, bool bwd =
       hg.mi = mi;
       hg.nj = nj;
       hg.pipe = pipe ? 1 : 0;
-      hg.wl = 0;
-      if (!pipe && !bwd && pass == 0 && halo_wlds_enabled()) {
-        // weights in LDS when the block still fits next to its tile and no block per CU is lost: the
-        // non-PIPE kernels run (MI <= 2 && NJ <= 4) ? 4 : 3 blocks per CU by registers
-        const size_t lds0 = halo_lds_bytes(hg.HH, hg.HWD, pitch, rows) + 12 * (size_t)Cip;
-        const size_t lds1 = lds0 + pipe_a_bytes(rows, mi, ks);
-        const size_t stat = 4 * 4 * kHaloMaxKS + 512;   // static tap tables + slack
-        auto by_lds = [&](size_t b) { return (int)((160 * 1024) / (b + stat)); };
-        const int by_vgpr = (mi <= 2 && nj <= 4) ? 4 : 3;
-        if (lds1 <= halo_tile_cap() && std::min(by_vgpr, by_lds(lds1)) >= std::min(by_vgpr, by_lds(lds0))) hg.wl = 1;
-      }
       hg.tw_shift = hg.TW == 16 ? 4 : (hg.TW == 32 ? 5 : 6);
       hg.inv_c8 = 1.0f / (float)d;
       {
@@ -1732,8 +1647,6 @@ static bool halo_enabled() {
 }
 
 void conv_set_halo(int on) { g_halo_mode = on ? 1 : 0; }
-void conv_set_small_halo(int on) { g_small_tile = on ? 1 : 0; }
-void conv_set_wlds(int on) { g_wlds = on ? 1 : 0; }
 bool conv_uses_halo(const ConvGeom& g, bool trans, bool bwd) {
   HaloGeom hg;
   if (conv_gemm_ok(g, trans)) return false;   // wide inputs: the LDS-tiled GEMM kernel (conv_gemm.hip)
@@ -1816,14 +1729,11 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
     const int hmi = hg.mi;
     hg.xtab = 0;
     for (int i = 0; i < a.g.Gi; ++i) hg.xtab |= a.xc[i] != nullptr;
-    static int dbg = -1;
-    if (dbg < 0) { const char* e = getenv("MSP_HALO_DBG"); dbg = e != nullptr ? atoi(e) : 0; }
-    hg.dbg = dbg;
     if (hg.xtab && a.bn_y != nullptr) return 3;   // BN prologue (forward) and BN epilogue (dgrad) never meet
     if (bwd && hg.xtab) return 3;
     const size_t lds = halo_lds(hg, a.g.Go * a.g.Cgo) +
                        (bwd ? 5 * 4 * (size_t)a.g.Gi * a.g.Cgi : (hg.xtab ? 3 * 4 * (size_t)a.g.Gi * a.g.Cgi : 0)) +
-                       ((hg.pipe || hg.wl) ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
+                       (hg.pipe ? pipe_a_bytes(a.g.Go * a.g.Cgo, hg.mi, hg.KS) : 0);
     // BNE: the BN-backward epilogue is its own instantiation, so plain launches keep their registers.
     // The prologue table may take the dynamic LDS past 64 KB: opted into once per instantiation,
     // before any graph capture (the first call of every shape runs eagerly).
@@ -1837,45 +1747,29 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
       }                                                                                                      \
       hipLaunchKernelGGL((K_), dim3(blocks), dim3(64 * kHaloWaves), lds, s, a, hg);                         \
     }
-#define HS_(MI_, BNE_)                                                                                       \
-    if (hmi == MI_ && bne == BNE_ && !pipe && hg.nj == 2) {                                                  \
-      HC_LAUNCH_((conv_halo_kernel<MI_, 2, false, BNE_>))                                                    \
-      return 0;                                                                                              \
-    }
 #define HB_(MI_, BNE_)                                                                                       \
     if (bwd && hmi == MI_ && bne == BNE_) {                                                                  \
-      const int nj_ = hg.nj;                                                                                 \
-      if (MI_ >= 3 && nj_ == 2) {                                                                            \
-        if constexpr (MI_ >= 3) HC_LAUNCH_((conv_halo_kernel<(MI_ >= 3 ? MI_ : 3), 2, false, BNE_, false, false, true>)) \
-      } else if (MI_ <= 2 && nj_ == 4) {                                                                     \
-        HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_, false, false, true>))                              \
-      } else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, false, true>))       \
+      HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, true>))                     \
       return 0;                                                                                              \
     }
 #define HC_(MI_, BNE_)                                                                                       \
     if (hmi == MI_ && bne == BNE_ && !pipe) {                                                                \
-      if (MI_ <= 2 && hg.nj == 4) {                                                                          \
-        if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, 4, true, BNE_>))                                   \
-        else HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_>))                                             \
-      } else if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))            \
-      else if (hg.wl) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_, false, true>))      \
+      if (hg.nch > 1) HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), true, BNE_>))                   \
       else HC_LAUNCH_((conv_halo_kernel<MI_, (MI_ <= 2 ? 8 : 4), false, BNE_>))                             \
       return 0;                                                                                              \
     }
-#define HP_(MI_, BNE_)                                                                                       \
-    if (hmi == MI_ && bne == BNE_ && pipe) {                                                                 \
-      HC_LAUNCH_((conv_halo_kernel<MI_, 4, false, BNE_, true>))                                              \
+#define HP_(BNE_)                                                                                            \
+    if (hmi == 3 && bne == BNE_ && pipe) {                                                                   \
+      HC_LAUNCH_((conv_halo_kernel<3, 4, false, BNE_, true>))                                                \
       return 0;                                                                                              \
     }
     const bool bne = a.bn_y != nullptr;
     HB_(1, false) HB_(2, false) HB_(3, false) HB_(4, false) HB_(1, true) HB_(2, true) HB_(3, true) HB_(4, true)
-    HS_(3, false) HS_(4, false) HS_(3, true) HS_(4, true)
     HC_(1, false) HC_(2, false) HC_(3, false) HC_(4, false) HC_(1, true) HC_(2, true) HC_(3, true) HC_(4, true)
-    HP_(2, false) HP_(3, false) HP_(2, true) HP_(3, true)
+    HP_(false) HP_(true)
     return 4;   // no instantiation for this row-group size
 #undef HB_
 #undef HP_
-#undef HS_
 #undef HC_
 #undef HC_LAUNCH_
   }
@@ -1949,12 +1843,8 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans, bool bwd = false) {
   if (!trans && wgrad_halo_ok(g, P.tl)) {
     P.halo = true;
     P.ntiles = (long)g.N * P.tl.tiles_y * P.tl.tiles_x;
-    // co sub-tiles per block: as many as the LDS budget allows (<= kDwMaxNcb; env MSP_DW_NCB caps it)
-    static int max_ncb = -1;
-    if (max_ncb < 0) {
-      const char* e = getenv("MSP_DW_NCB");
-      max_ncb = (e != nullptr && atoi(e) > 0) ? std::min(atoi(e), kDwMaxNcb) : kDwMaxNcb;
-    }
+    // co sub-tiles per block: as many as the LDS budget allows (<= kDwMaxNcb)
+    const int max_ncb = kDwMaxNcb;
     // The kernel's time ~ (tiles per block) x (co sub-tiles per block) + the per-tile input-halo
     // staging that NCB sub-tiles share: with the grid fixed at ~split_target blocks, cost ~ gy * ncb +
     // kDwHaloCost * gy.  Balancing matters: 4 sub-tiles (a 5-group fused conv at 24 ch) run as 2 + 2,
@@ -1975,12 +1865,7 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans, bool bwd = false) {
     // single ci sub-tile (L1: 256 vs 512 blocks 0.642 vs 0.648 ms); with two ci sub-tiles (L2, 40 ch)
     // 512 blocks win (3x3 0.442 -> 0.417 ms, fused-8 2.59 -> 2.43 ms at bs128;
     // profiles/r03/conv_bench_v9_dw_split_bs128.log)
-    static long split_target = -1;   // blocks in the grid; env MSP_DW_SPLIT overrides (tuning)
-    if (split_target < 0) {
-      const char* e = getenv("MSP_DW_SPLIT");
-      split_target = (e != nullptr && atol(e) > 0) ? atol(e) : 0;
-    }
-    const long target = split_target > 0 ? split_target : (P.gz >= 2 ? 2 : 1) * kDwSplitTarget;
+    const long target = (P.gz >= 2 ? 2 : 1) * kDwSplitTarget;   // blocks in the grid
     P.nsplit = std::max(1L, std::min(target / ((long)P.gy * P.gz), P.ntiles));
     return P;
   }
@@ -1990,10 +1875,8 @@ static WgradPlan wgrad_plan(const ConvGeom& g, bool trans, bool bwd = false) {
   P.co_t = rows <= 32 ? 32 : 64;
   // K tile 64: the 64 x 128 tile needs 149 VGPRs + 128 AGPRs (1 wave/SIMD); at 64 (2 waves/SIMD) the
   // strided weight gradients run 1.5-1.9x faster (L1 3x3 s2: 50 -> 76 TF, L3: 80 -> 155 TF; step +0.8 %,
-  // profiles/r02/conv_bench_s2_wgrad_kt.log).  env MSP_DW_GEN_KT=128 restores the wide tile (A/B).
-  static int kt_cap = -1;
-  if (kt_cap < 0) { const char* e = getenv("MSP_DW_GEN_KT"); kt_cap = (e != nullptr && atoi(e) == 128) ? 128 : 64; }
-  P.k_t = (KT <= 64 || kt_cap == 64) ? 64 : 128;
+  // profiles/r02/conv_bench_s2_wgrad_kt.log).
+  P.k_t = 64;
   P.gx = cdiv(KT, P.k_t);
   P.gy = cdiv(rows, P.co_t);
   P.nsplit = std::max(1L, std::min(2048L / ((long)P.gx * P.gy), nchunks));
@@ -2074,7 +1957,7 @@ int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, c
     else hipLaunchKernelGGL((conv_wgrad_kernel<CO_, K_, false>), grid, dim3(256), 0, s, P, dw, g, KT);      \
     return 0;                                                                                        \
   }
-  WG(32, 64) WG(32, 128) WG(64, 64) WG(64, 128)
+  WG(32, 64) WG(64, 64)
 #undef WG
   return 6;
 }
@@ -2161,11 +2044,8 @@ int conv_plan_selfcheck(int verbose) {
                     fail("PIPE LDS budget", g);
                   if (hg.nch != 1 || C8 != d) fail("PIPE with channel chunks", g);
                 }
-                if (hg.wl) {
-                  if (hg.pipe || hg.nch != 1) fail("WL outside the whole-input non-PIPE kernel", g);
-                  if (halo_lds(hg, rows) + 12 * (size_t)cin + pipe_a_bytes(rows, hg.mi, hg.KS) > halo_tile_cap())
-                    fail("WL LDS budget", g);
-                }
+                if (hg.nj != (hg.mi <= 2 && !hg.pipe ? 8 : 4) || (hg.pipe && hg.mi != 3))
+                  fail("halo tile: no instantiation for this (MI, NJ, PIPE)", g);
                 if (cdiv(rows, 16 * hg.mi) * 16 * hg.mi > conv_rows_alloc(rows)) fail("weight rows under-allocated", g);
                 const long blocks = halo_blocks(g, hg);
                 if (blocks < 1 || blocks > (1L << 31) - 1) fail("halo grid size", g);

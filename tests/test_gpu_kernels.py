@@ -42,31 +42,6 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize('case', CONV_CASES[-2:])
-def test_conv_small_halo_tile(gpu, case, monkeypatch):
-    """The opt-in 128-pixel (NJ 2) halo tile (MSP_HALO_SMALL=1) on the shapes that take it."""
-    from medical_segmentation_pytorch_amd.ops import _ext
-    C = _ext.require()
-    C.conv_set_small_halo(True)
-    try:
-        test_conv_fwd_bwd(gpu, case)
-    finally:
-        C.conv_set_small_halo(False)
-
-
-@pytest.mark.parametrize('case', CONV_CASES[:6])
-def test_conv_halo_weights_in_lds(gpu, case):
-    """The opt-in WL halo kernels (packed weights staged in LDS, MSP_HALO_WLDS=1) -- both paths stay
-    covered."""
-    from medical_segmentation_pytorch_amd.ops import _ext
-    C = _ext.require()
-    C.conv_set_wlds(True)
-    try:
-        test_conv_fwd_bwd(gpu, case)
-    finally:
-        C.conv_set_wlds(False)
-
-
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_fwd_bwd(gpu, case):
     n, h, w, ci, co, (kh, kw), s, pad, dil = case

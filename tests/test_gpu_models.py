@@ -31,6 +31,32 @@ def _smp(arch, encoder):
     return getattr(smp, arch)(encoder_name=encoder, encoder_weights=None, in_channels=3, classes=2)
 
 
+def _pretrain(model, gpu, size, batch, steps):
+    """A well-conditioned gradient oracle: at random init, training-mode DUCKNet / small ResNets amplify ANY
+    bf16 rounding (PyTorch's own autocast reached only 0.15-0.27 mean grad cos vs fp32 on DUCKNet,
+    profiles/r03/parity_probe_ducknet_train.log), so the weights are first trained ``steps`` Adam steps on
+    input-correlated synthetic labels (the fused training step itself, same batch shape)."""
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep
+    g = torch.Generator().manual_seed(7)
+    xs = torch.empty(batch, 3, size, size, device=gpu)
+    ys = torch.empty(batch, size, size, dtype=torch.long, device=gpu)
+
+    def feed(x, y):
+        x.copy_(torch.randn(batch, 3, size, size, generator=g).to(gpu))
+        y.copy_((F.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long())
+    step = FusedStep(model, xs, ys, optimizer='adam', lr=1e-3, use_graph=False, feed=feed, total_steps=steps + 1,
+                     pct_start=0.1)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    for p in model.parameters():   # (the arena grad views of the pretraining engine)
+        p.grad = None
+    return model
+
+
+ORACLE_STEPS = 200
+
+
 @pytest.mark.parametrize('model_fn,size,batch', [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64, 2),
                                                  (lambda: _smp_unet('resnet18'), 64, 4),
                                                  (lambda: _smp_unet('resnet50'), 64, 2),
@@ -52,12 +78,15 @@ def _smp(arch, encoder):
                                                  (lambda: _smp('PAN', 'resnet18'), 128, 4),
                                                  (lambda: _smp('MAnet', 'resnet18'), 64, 4)])
 def test_fused_matches_eager(gpu, model_fn, size, batch):
-    """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is."""
+    """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is -- measured
+    on a well-conditioned oracle (pretrained weights, see _pretrain): autocast-bf16 must itself reach mean
+    grad cos > 0.9 vs fp32 there, the fused mean must be within 0.03 of it and every parameter > 0.8."""
     torch.manual_seed(0)
     model = model_fn().to(gpu).train()
     for m in model.modules():   # decoder dropout would draw different masks in the three runs
         if isinstance(m, torch.nn.modules.dropout._DropoutNd):
             m.p = 0.0
+    _pretrain(model, gpu, size, batch, ORACLE_STEPS)
     ref = copy.deepcopy(model)
     ref16 = copy.deepcopy(model)
     x = torch.randn(batch, 3, size, size, device=gpu)
@@ -93,15 +122,9 @@ def test_fused_matches_eager(gpu, model_fn, size, batch):
     mf = sum(cf) / len(cf)
     mb = sum(cb) / len(cb)
     print(f'grad cos mean: fused {mf:.4f} autocast-bf16 {mb:.4f}; min fused {min(cf):.4f} bf16 {min(cb):.4f}')
-    # The fp32 oracle is only as good as the model's conditioning: at these sizes random-init training-mode
-    # DUCKNet (and the small ResNets at 64 px) amplify ANY bf16 rounding -- PyTorch's own autocast reaches
-    # only 0.15-0.27 mean grad cos vs fp32, even with input-correlated labels and smooth inputs
-    # (profiles/r03/parity_probe_ducknet_train.log).  So: the fused engine must track autocast-bf16's
-    # distance to fp32 (mean, and the worst parameter), tightly where the oracle is well conditioned.
-    margin = 0.05 if mb > 0.7 else 0.1
-    assert mf > mb - margin, (mf, mb)
-    if mb > 0.7:
-        assert min(cf) > min(cb) - 0.15, (min(cf), min(cb))
+    assert mb > 0.9, f'oracle not well conditioned (autocast-bf16 vs fp32 mean grad cos {mb:.3f}): train longer'
+    assert mf > mb - 0.03, (mf, mb)
+    assert min(cf) > 0.8, (min(cf), min(cb))
     for (k, a), (_, b) in zip(model.state_dict().items(), ref.state_dict().items()):
         if 'num_batches_tracked' in k:
             assert int(a) == int(b), k
