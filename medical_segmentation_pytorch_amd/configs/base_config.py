@@ -123,6 +123,9 @@ class BaseConfig:
                                           # kernels; 1.8x the NCHW step on MI355X, profiles/r02/eager_sweep)
         self.bucket_cap_mb = 64        # gradient bucket size for the RCCL all-reduce
         self.grad_compress = None      # None | 'bf16' all-reduce compression
+        self.lr_scale = 'reference'    # lr vs batch: 'reference' (x gpu_num) | 'sqrt' | 'linear' in
+                                       # global_batch / lr_ref_batch (utils/optimizer.lr_batch_factor)
+        self.lr_ref_batch = 16         # the batch base_lr is tuned for (MyConfig train_bs)
         self.syncbn_comm = 'auto'      # SyncBN statistic exchange: 'auto' (IPC peer-memory kernel on one node,
                                        # RCCL otherwise) | 'ipc' | 'rccl'  (env MSP_SYNCBN_COMM overrides)
         self.gpu_augment = True        # run augmentation on the GPU over an HBM-resident dataset

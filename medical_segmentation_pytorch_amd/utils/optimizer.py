@@ -178,16 +178,36 @@ class FusedGradScaler:
             self.state[3] = float(optimizer.step_count)
 
 
+def lr_batch_factor(config):
+    """Large-batch learning-rate scaling on top of the reference rule.
+
+    ``config.lr_scale`` = ``'reference'`` (default; reference ``utils/optimizer.py:9,15``: x gpu_num, the
+    per-GPU batch is fixed at MyConfig's 16), ``'sqrt'`` (x sqrt(global batch / lr_ref_batch)) or
+    ``'linear'`` (x global batch / lr_ref_batch).  The global batch is train_bs x gpu_num; lr_ref_batch
+    (16) is the batch the reference's base_lr was tuned for.  With Adam the square-root rule is the stable
+    one (the update is scale-free, so its noise falls as 1/sqrt(batch)); warm-up comes from the OneCycle
+    schedule's warmup_epochs."""
+    rule = getattr(config, 'lr_scale', 'reference') or 'reference'
+    if rule == 'reference':
+        return float(config.gpu_num)
+    ratio = config.train_bs * config.gpu_num / float(getattr(config, 'lr_ref_batch', 16) or 16)
+    if rule == 'sqrt':
+        return ratio ** 0.5
+    if rule == 'linear':
+        return ratio
+    raise ValueError(f"lr_scale must be 'reference', 'sqrt' or 'linear', got {rule!r}")
+
+
 def get_optimizer(config, model):
     fused = getattr(config, '_fused', False)
     if config.optimizer_type == 'sgd':
-        config.lr = config.base_lr * config.gpu_num
+        config.lr = config.base_lr * lr_batch_factor(config)
         if fused:
             return FusedOptimizer(model, 'sgd', lr=config.lr, momentum=config.momentum,
                                   weight_decay=config.weight_decay)
         return SGD(model.parameters(), lr=config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
     if config.optimizer_type in ['adam', 'adamw']:
-        config.lr = 0.1 * config.base_lr * config.gpu_num
+        config.lr = 0.1 * config.base_lr * lr_batch_factor(config)
         if fused:
             return FusedOptimizer(model, config.optimizer_type, lr=config.lr)
         cls = Adam if config.optimizer_type == 'adam' else AdamW

@@ -61,6 +61,9 @@ def main():
     ap.add_argument('--train-images', type=int, default=880, help='Kvasir-SEG train split size')
     ap.add_argument('--val-images', type=int, default=100)
     ap.add_argument('--base-lr', type=float, default=0.01, help='reference rule: adam lr = 0.1 * base_lr * gpu_num')
+    ap.add_argument('--lr-scale', default='reference', choices=['reference', 'sqrt', 'linear'],
+                    help='large-batch lr rule (utils/optimizer.lr_batch_factor)')
+    ap.add_argument('--begin-val', type=int, default=0, help='first validated epoch')
     ap.add_argument('--model', default='ducknet')
     ap.add_argument('--base-channel', type=int, default=17)
     ap.add_argument('--val-fp32', action='store_true', help='validate the EMA model in fp32 eager (reference protocol)')
@@ -73,7 +76,8 @@ def main():
     cmd = [sys.executable, '-u', os.path.join(ROOT, 'main.py'), '--dataset', 'synthetic', '--model', a.model,
            '--base_channel', str(a.base_channel), '--crop_size', str(a.size), '--synthetic_size', str(a.size),
            '--synthetic_num', str(a.train_images), str(a.val_images), str(a.val_images), '--train_bs', str(a.batch),
-           '--total_epoch', str(a.epochs), '--val_interval', str(a.val_every), '--begin_val_epoch', '0',
+           '--total_epoch', str(a.epochs), '--val_interval', str(a.val_every), '--begin_val_epoch', str(a.begin_val),
+           '--lr_scale', a.lr_scale,
            '--val_bs', '16', '--save_dir', save, '--base_lr', str(a.base_lr), '--use_tb', '--load_ckpt',
            '--no_progress_bar', '--log_interval', '1000'] + (['--val_fp32'] if a.val_fp32 else []) + a.extra
     print('[acc]', ' '.join(cmd), file=sys.stderr, flush=True)
@@ -83,7 +87,9 @@ def main():
         sys.exit(r.returncode)
     out = {'entry': 'python main.py (SegTrainer.run -> val_best on best.pth)', 'model': f'{a.model}-{a.base_channel}',
            'batch': a.batch, 'epochs': a.epochs, 'size': a.size, 'train_images': a.train_images,
-           'val_images': a.val_images, 'adam_lr': 0.1 * a.base_lr, 'val_fp32': a.val_fp32,
+           'val_images': a.val_images, 'lr_scale': a.lr_scale,
+           'adam_lr': json.load(open(os.path.join(save, 'config.json'))).get('lr', 0.1 * a.base_lr),
+           'val_fp32': a.val_fp32,
            'data': 'synthetic polyp frames (datasets/synthetic.py), MyConfig augmentation on the GPU (DeviceAugLoader)',
            'process_wall_s': round(time.time() - t0, 1),
            **summarise(os.path.join(save, 'val_history.json'), a.target)}
