@@ -816,6 +816,58 @@ void comm_allreduce_t(const at::Tensor& in, const at::Tensor& out, const std::ve
                     cur_stream());
 }
 
+// ---- conv_bwd.hip: fused data- + weight-gradient of a narrow stride-1 conv ---------------------------
+int64_t conv_bwd_fused_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  return conv_bwd_fused_blocks(make_geom(dims, dy, dx));
+}
+
+void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy, const c10::optional<at::Tensor>& gs,
+                      const c10::optional<at::Tensor>& gk, bool grelu, const at::Tensor& x,
+                      const c10::optional<at::Tensor>& xc, bool xrelu, const at::Tensor& wd, int64_t Kp_d,
+                      const at::Tensor& dxo, const c10::optional<at::Tensor>& bn_y,
+                      const c10::optional<at::Tensor>& bn_coef, bool bn_relu,
+                      const c10::optional<at::Tensor>& stat_part, const at::Tensor& dw, std::vector<int64_t> dims,
+                      std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  ConvGeom g = make_geom(dims, dy, dx);
+  const int64_t nblk = conv_bwd_fused_blocks(g);
+  TORCH_CHECK(nblk > 0, "conv_bwd_fused: shape not eligible");
+  const int64_t ny = (int64_t)g.N * g.OH * g.OW * g.Cgo, nx = (int64_t)g.N * g.IH * g.IW * g.Cgi;
+  CHECK_BF16(dz); TORCH_CHECK(dz.numel() == ny, "dz numel");
+  CHECK_BF16(x); TORCH_CHECK(x.numel() == nx, "x numel");
+  CHECK_BF16(dxo); TORCH_CHECK(dxo.numel() == nx, "dx numel");
+  CHECK_BF16(wd);
+  TORCH_CHECK(Kp_d % 32 == 0 && Kp_d >= g.T * g.Cgo && wd.numel() >= 32 * Kp_d, "packed dgrad weights");
+  CHECK_F32(dw); TORCH_CHECK(dw.numel() == nblk * g.Cgo * g.T * g.Cgi, "dw slabs numel");
+  FusedBwdArgs a{};
+  a.dz = bf(dz);
+  if (gy.has_value() && gy->defined()) {
+    CHECK_BF16(*gy); TORCH_CHECK(gy->numel() == ny, "gy numel");
+    TORCH_CHECK(gs.has_value() && gk.has_value(), "gy needs gs and gk");
+    CHECK_F32(*gs); CHECK_F32(*gk);
+    TORCH_CHECK(gs->numel() >= 2 * g.Cgo && gk->numel() >= 3 * g.Cgo, "gs [4][C], gk [3][C]");
+    a.gy = bf(*gy); a.gs = gs->data_ptr<float>(); a.gk = gk->data_ptr<float>();
+  }
+  a.grelu = grelu ? 1 : 0;
+  a.x = bf(x);
+  a.xc = f32_opt(xc);
+  if (a.xc) TORCH_CHECK(xc->numel() >= 2 * g.Cgi, "xc [4][C]");
+  a.xrelu = xrelu ? 1 : 0;
+  a.wd = bf(wd);
+  a.Kp = (int)Kp_d;
+  a.dxo = bf(dxo);
+  if (bn_y.has_value() && bn_y->defined()) {
+    CHECK_BF16(*bn_y); TORCH_CHECK(bn_y->numel() == nx, "bn_y numel");
+    TORCH_CHECK(bn_coef.has_value() && stat_part.has_value(), "BN epilogue needs bn_coef and stat_part");
+    CHECK_F32(*bn_coef); CHECK_F32(*stat_part);
+    TORCH_CHECK(bn_coef->numel() >= 3 * g.Cgi && stat_part->numel() == nblk * 2 * g.Cgi, "BN epilogue shapes");
+    a.bn_y = bf(*bn_y); a.bn_coef = bn_coef->data_ptr<float>(); a.stat_part = stat_part->data_ptr<float>();
+  }
+  a.bn_relu = bn_relu ? 1 : 0;
+  a.dw = f32(dw);
+  const int rc = conv_bwd_fused(a, g, cur_stream());
+  TORCH_CHECK(rc == 0, "conv_bwd_fused: launch failed (", rc, ")");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -928,6 +980,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_wgrad_blocks", &dwconv_wgrad_blocks_t);
   m.def("dwconv_wgrad", &dwconv_wgrad_t);
   m.def("colsum", &colsum_t);
+  m.def("conv_bwd_fused_blocks", &conv_bwd_fused_blocks_t);
+  m.def("conv_bwd_fused", &conv_bwd_fused_t);
   m.def("comm_buffer_bytes", &comm_buffer_bytes);
   m.def("comm_alloc", &comm_alloc_t);
   m.def("comm_open", &comm_open_t);

@@ -1,0 +1,422 @@
+// Fused backward of a narrow stride-1 convolution: data-gradient AND weight-gradient from ONE staging of
+// dY and x (the 17-channel DUCKNet level, reference models/ducknet.py:95-96,144-179: Widescope /
+// Midscope / Residual / Separated chains of conv-BN-ReLU at full resolution).
+//
+// For a chain BN1 -> conv C -> BN2 the separate kernels move 8 full-resolution tensor passes per conv:
+//   bn_act_bwd_apply(BN2)  read dz2, y2, write dy2        (3)
+//   dgrad(C) + BN1 partials  read dy2, y1, write dz1       (3)
+//   wgrad(C)                 read dy2, y1 (x = BN1(y1))    (2)
+// Here one persistent kernel stages, per pixel tile, dY = bwd(dz2, y2) (the deferred BN2 backward, bwd8 --
+// bit-identical to bn_act_bwd_apply) and x = relu(BN1(y1)) (the deferred forward prologue) into LDS once,
+// then runs the data-gradient MFMAs (dz1 + BN1's backward partials in the epilogue) and accumulates the
+// weight-gradient MFMAs of the same tile in registers: read dz2, y2, y1, write dz1 -- 4 passes.
+//
+// Tile: 4 waves x NJ x 16 output pixels (TH x TW), halo = the tap extents (symmetric tap sets only: the
+// forward and backward halos coincide).  LDS: the dY halo tile [HH*HWD][py] and the x halo tile
+// [HH*HWD][px] (pitch = an odd number of 16-B slots: the data-gradient's ds_read_b128 lane groups hit
+// distinct banks), plus per-wave BN partial rows.  Data-gradient: the halo kernel's scheme (A = packed
+// dgrad weights from L2 with a one-step prefetch, B = ds_read_b128 of the dY tile at per-unit tap offsets,
+// v_mfma_f32_16x16x32_bf16, 32 rows = input channels <= 32).  Weight-gradient: dW[co][t][ci] = sum_p
+// dY[p][co] x[p + tap_t][ci]: K = the tile's pixels in 32-pixel chunks, both operands read transposed
+// (ds_read_b64_tr_b16) from the same LDS tiles; wave w owns taps w, w+4, w+8 and all (co, ci) 16x16 blocks,
+// accumulating over the block's tiles; at the end each block writes its fp32 dW slab (deterministic split-K,
+// summed in fixed order by unpack_wgrad).  Channels 24..31 of a 24-wide tile read the next pixel's data:
+// those rows/columns of the 16x16 blocks are never stored.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int kFbWaves = 4;
+constexpr int kFbLd = 8;          // staging vectors in flight per thread
+constexpr int kFbMaxKS = 24;      // data-gradient k-steps (T <= 9 taps x <= 4 slots / 4)
+constexpr int kFbMaxT = 9;
+constexpr int kFbMaxLds = 76 * 1024;
+constexpr int kFbSlack = 64;      // elements past each tile (the 24..31 channel over-read of the last pixel)
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+DEVI uint2 fb_tr_read(const uint16_t* p) {
+  s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t __attribute__((address_space(3)))*)(p));
+  union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.hip ldg4)
+  const u32x4_t v =
+      *reinterpret_cast<const __attribute__((address_space(1))) u32x4_t*>(reinterpret_cast<uintptr_t>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <int NJ, bool BWD, bool XPRO, bool BNE>
+__global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
+  extern __shared__ uint4 fb_smem[];
+  constexpr int MI = 2;                       // 32 data-gradient rows (input channels <= 32)
+  constexpr int NT = 3;                       // weight-gradient taps per wave (T <= 9 = 3 x 4 waves)
+  constexpr int TP = kFbWaves * NJ * 16;      // pixels per tile
+  constexpr int NCH = TP / 32;                // weight-gradient k chunks per tile
+  const int hpx = fg.HH * fg.HWD;
+  uint16_t* tY = reinterpret_cast<uint16_t*>(fb_smem);
+  uint16_t* tX = tY + hpx * fg.py + kFbSlack;
+  float* s_stat = reinterpret_cast<float*>(tX + hpx * fg.px + kFbSlack);   // [waves][2][32]
+  __shared__ float s_bt[BWD ? 5 * 32 : 1];    // dY rebuild table: scale, shift (+inf: no ReLU), k1, k2, k3
+  __shared__ float s_xt[XPRO ? 3 * 32 : 1];   // x prologue: scale, shift, ReLU floor (0 / -inf)
+  __shared__ int s_ub[kFbMaxKS * 4];          // data-gradient unit -> dY tile offset
+  __shared__ int s_wb[kFbMaxT];               // weight-gradient tap -> x tile offset (pixel units)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Ci = a.Ci, Co = a.Co, T = a.T;
+  const int C8y = Co >> 3, C8x = Ci >> 3;
+  if constexpr (BWD) {
+    for (int c = tid; c < 32; c += 64 * kFbWaves) {
+      const bool on = c < Co;
+      s_bt[c] = on ? a.gs[c] : 0.f;
+      s_bt[32 + c] = (on && a.grelu) ? a.gs[Co + c] : INFINITY;
+      s_bt[64 + c] = on ? a.gk[c] : 0.f;
+      s_bt[96 + c] = on ? a.gk[Co + c] : 0.f;
+      s_bt[128 + c] = on ? a.gk[2 * Co + c] : 0.f;
+    }
+  }
+  if constexpr (XPRO) {
+    for (int c = tid; c < 32; c += 64 * kFbWaves) {
+      const bool on = c < Ci;
+      s_xt[c] = on ? a.xc[c] : 0.f;
+      s_xt[32 + c] = on ? a.xc[Ci + c] : 0.f;
+      s_xt[64 + c] = a.xrelu ? 0.f : -INFINITY;
+    }
+  }
+  for (int e = tid; e < fg.KS * 4; e += 64 * kFbWaves) {
+    int ub = 0;
+    if (e < T * C8y) {
+      const int t = e / C8y, c8 = e - t * C8y;
+      // data-gradient taps = the negated forward taps
+      ub = ((-a.dy[t] - fg.ey0) * fg.HWD + (-a.dx[t] - fg.ex0)) * fg.py + 8 * c8;
+    }
+    s_ub[e] = ub;
+  }
+  if (tid < kFbMaxT) s_wb[tid] = tid < T ? (a.dy[tid] * fg.HWD + a.dx[tid]) : 0;
+  if (BNE)
+    for (int c = tid; c < kFbWaves * 2 * 32; c += 64 * kFbWaves) s_stat[c] = 0.f;
+  __syncthreads();
+
+  // data-gradient: the wave's NJ 16-pixel columns -> dY tile pixel offsets
+  int pb[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int p = (wave * NJ + j) * 16 + lr;
+    pb[j] = ((p >> fg.tw_shift) * fg.HWD + (p & (fg.TW - 1))) * fg.py;   // + s_ub: tap offset - halo origin
+  }
+  // weight-gradient transposed-read pixel rows: chunk pixel 8*lg + q (lo) and + 4 (hi), q = lr >> 2
+  const int q = lr >> 2, p4 = lr & 3;
+  const int plo = 8 * lg + q, phi = plo + 4;
+  // tile pixel P -> halo pixel index (per chunk s: P = 32 s + plo / phi)
+  auto halo_pix = [&](int P) { return ((P >> fg.tw_shift) - fg.ey0) * fg.HWD + ((P & (fg.TW - 1)) - fg.ex0); };
+
+  f32x4_t accw[NT][2][2];
+#pragma unroll
+  for (int m = 0; m < NT; ++m)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) accw[m][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float cs[MI][4], cq[MI][4];   // BN1 partials (BNE), over the block's tiles
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[i][r] = 0.f; cq[i][r] = 0.f; }
+
+  const int per_img = fg.tiles_y * fg.tiles_x;
+  const long img_px = (long)a.H * a.W;
+  for (int tt = blockIdx.x; tt < fg.ntiles; tt += gridDim.x) {
+    const int n = tt / per_img, trem = tt - n * per_img;
+    const int tyi = trem / fg.tiles_x;
+    const int ty0 = tyi * fg.TH, tx0 = (trem - tyi * fg.tiles_x) * fg.TW;
+    const long imoff = (long)n * img_px;
+    if (tt != (int)blockIdx.x) __syncthreads();   // every wave is done with the previous tile's LDS
+    // ---- staging: dY = bwd(dz, y2) and x = prologue(y1), zero outside the image -------------------------
+    {
+      const int totY = hpx * C8y, totX = hpx * C8x, tot = totY + totX;
+      for (int base = tid; base < tot; base += 64 * kFbWaves * kFbLd) {
+        uint4 v[kFbLd], w[kFbLd];
+        int dst[kFbLd], cc[kFbLd];
+#pragma unroll
+        for (int u = 0; u < kFbLd; ++u) {
+          const int idx = base + u * 64 * kFbWaves;
+          v[u] = make_uint4(0, 0, 0, 0);
+          w[u] = make_uint4(0, 0, 0, 0);
+          dst[u] = -1;
+          cc[u] = -1;
+          if (idx < tot) {
+            const bool isy = idx < totY;
+            const int e = isy ? idx : idx - totY;
+            const int C8 = isy ? C8y : C8x;
+            const int hp = e / C8, c8 = e - hp * C8;
+            const int hy = hp / fg.HWD, hx = hp - hy * fg.HWD;
+            const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
+            dst[u] = isy ? hp * fg.py + 8 * c8 : -2 - (hp * fg.px + 8 * c8);   // <= -2: an x-tile slot
+            if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
+              const long pix = imoff + iy * a.W + ix;
+              if (isy) {
+                v[u] = fb_ldg4(a.dz + pix * Co + 8 * c8);
+                if (BWD) w[u] = fb_ldg4(a.gy + pix * Co + 8 * c8);
+              } else {
+                v[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
+              }
+              cc[u] = 8 * c8;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kFbLd; ++u) {
+          if (dst[u] == -1) continue;
+          uint4 val = v[u];
+          if (dst[u] >= 0) {
+            if (BWD && cc[u] >= 0) val = bwd8(val, w[u], s_bt + cc[u], 32);
+            *reinterpret_cast<uint4*>(tY + dst[u]) = val;
+          } else {
+            if (XPRO && cc[u] >= 0) {
+              float f[8];
+              unpack8(val, f);
+#pragma unroll
+              for (int k = 0; k < 8; ++k)
+                f[k] = fmaxf(fmaf(f[k], s_xt[cc[u] + k], s_xt[32 + cc[u] + k]), s_xt[64 + cc[u] + k]);
+              val = pack8(f);
+            }
+            *reinterpret_cast<uint4*>(tX + (-2 - dst[u])) = val;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- data-gradient: dz1 = conv(dY, W_d) (+ BN1 backward partials) -----------------------------------
+    {
+      const uint16_t* wrow[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) wrow[i] = a.wd + (long)(16 * i + lr) * a.Kp + 8 * lg;
+      f32x4_t acc[MI][NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      uint4 A[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i]);
+      for (int ks = 0; ks < fg.KS; ++ks) {
+        uint4 An[MI];
+        const bool more = ks + 1 < fg.KS;
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) An[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * (ks + 1));
+        }
+        const int ub = s_ub[4 * ks + lg];
+        uint4 B[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tY + pb[j] + ub);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) A[i] = An[i];
+        }
+      }
+      // epilogue: dz1 (bf16, NHWC) for the in-image pixels and channels < Ci
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int cb = 16 * i + 4 * lg;
+        if (cb >= Ci) continue;
+        float sc[4], sh[4], mu[4];
+        if (BNE) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sc[r] = a.bn_coef[cb + r];
+            sh[r] = a.bn_relu ? a.bn_coef[Ci + cb + r] : INFINITY;
+            mu[r] = a.bn_coef[2 * Ci + cb + r];
+          }
+        }
+        uint2 yy[NJ];
+        long pm[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int p = (wave * NJ + j) * 16 + lr;
+          const int ty = ty0 + (p >> fg.tw_shift), tx = tx0 + (p & (fg.TW - 1));
+          pm[j] = (ty < a.H && tx < a.W) ? (imoff + (long)ty * a.W + tx) * Ci + cb : -1;
+          if (BNE) yy[j] = pm[j] >= 0 ? *reinterpret_cast<const uint2*>(a.bn_y + pm[j]) : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if (pm[j] < 0) continue;
+          const uint32_t lo = pack2(acc[i][j][0], acc[i][j][1]), hi = pack2(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(a.dxo + pm[j]) = make_uint2(lo, hi);
+          if (BNE) {
+            const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+            const float y4[4] = {__uint_as_float(yy[j].x << 16), __uint_as_float(yy[j].x & 0xffff0000u),
+                                 __uint_as_float(yy[j].y << 16), __uint_as_float(yy[j].y & 0xffff0000u)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gr = fmaf(y4[r], sc[r], sh[r]) > 0.f ? g4[r] : 0.f;
+              cs[i][r] += gr;
+              cq[i][r] += gr * (y4[r] - mu[r]);
+            }
+          }
+        }
+      }
+    }
+
+    // ---- weight-gradient: accw[m][i][j] += dY[chunk][co block i]^T x[chunk + tap][ci block j] ----------
+#pragma unroll 2
+    for (int s = 0; s < NCH; ++s) {
+      const int hlo = halo_pix(32 * s + plo), hhi = halo_pix(32 * s + phi);
+      uint4 fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint2 lo = fb_tr_read(tY + hlo * fg.py + 16 * i + 4 * p4);
+        const uint2 hi = fb_tr_read(tY + hhi * fg.py + 16 * i + 4 * p4);
+        fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int m = 0; m < NT; ++m) {
+        const int t = wave + kFbWaves * m;
+        if (t >= T) break;   // wave-uniform
+        const int sw = s_wb[t];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint2 lo = fb_tr_read(tX + (hlo + sw) * fg.px + 16 * j + 4 * p4);
+          const uint2 hi = fb_tr_read(tX + (hhi + sw) * fg.px + 16 * j + 4 * p4);
+          const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) accw[m][i][j] = mfma16x16x32(fa[i], fb, accw[m][i][j]);
+        }
+      }
+    }
+  }   // tile loop
+
+  // ---- BN1 partials: this block's row -------------------------------------------------------------------
+  if (BNE) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int cb = 16 * i + 4 * lg;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s2 = row16_sum(cs[i][r]), q2 = row16_sum(cq[i][r]);
+        if (lr == 0 && cb + r < Ci) {
+          s_stat[(wave * 2 + 0) * 32 + cb + r] = s2;
+          s_stat[(wave * 2 + 1) * 32 + cb + r] = q2;
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < Ci; c += 64 * kFbWaves) {
+      float s2 = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < kFbWaves; ++wv) { s2 += s_stat[(wv * 2 + 0) * 32 + c]; q2 += s_stat[(wv * 2 + 1) * 32 + c]; }
+      a.stat_part[((long)blockIdx.x * 2 + 0) * Ci + c] = s2;
+      a.stat_part[((long)blockIdx.x * 2 + 1) * Ci + c] = q2;
+    }
+  }
+  // ---- dW slab of this block: [Co][T * Ci], element (co, t*Ci + ci) -------------------------------------
+  float* slab = a.dw + (long)blockIdx.x * Co * (T * Ci);
+#pragma unroll
+  for (int m = 0; m < NT; ++m) {
+    const int t = wave + kFbWaves * m;
+    if (t >= T) break;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = 16 * j + lr;
+        if (ci >= Ci) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = 16 * i + 4 * lg + r;
+          if (co < Co) slab[(long)co * (T * Ci) + t * Ci + ci] = accw[m][i][j][r];
+        }
+      }
+  }
+}
+
+size_t fb_lds(const FusedBwdGeom& fg) {
+  return ((size_t)fg.HH * fg.HWD * (fg.py + fg.px) + 2 * kFbSlack) * 2 + (size_t)kFbWaves * 2 * 32 * 4;
+}
+
+}  // namespace
+
+// Plan: eligible shapes and the tile geometry (0 = not eligible).  Symmetric tap sets only (3x3 with any
+// dilation, 1x7 / 7x1): the dY halo of the data-gradient and the x halo of the weight-gradient coincide.
+bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
+  if (g.stride != 1 || g.Gi != 1 || g.Go != 1 || g.OH != g.IH || g.OW != g.IW) return false;
+  if (g.Cgi > 32 || g.Cgo > 32 || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2) return false;
+  int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
+  for (int t = 0; t < g.T; ++t) {
+    bool mirrored = false;
+    for (int u = 0; u < g.T; ++u) mirrored |= g.dy[u] == -g.dy[t] && g.dx[u] == -g.dx[t];
+    if (!mirrored) return false;
+    ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
+    ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
+  }
+  const int C8y = g.Cgo / 8, C8x = g.Cgi / 8;
+  const int py = 8 * ((C8y & 1) ? C8y : C8y + 1), px = 8 * ((C8x & 1) ? C8x : C8x + 1);
+  const int KS = (g.T * C8y + 3) / 4;
+  if (KS > kFbMaxKS) return false;
+  double best = 1e30;
+  bool found = false;
+  for (int nj = 8; nj >= 4; nj -= 4) {
+    const int tp = kFbWaves * nj * 16;
+    for (int tw = 16; tw <= 64; tw *= 2) {
+      const int th = tp / tw;
+      FusedBwdGeom c{};
+      c.TH = th; c.TW = tw; c.tw_shift = tw == 16 ? 4 : (tw == 32 ? 5 : 6);
+      c.HH = th + ey1 - ey0; c.HWD = tw + ex1 - ex0; c.ey0 = ey0; c.ex0 = ex0;
+      c.py = py; c.px = px; c.KS = KS; c.nj = nj;
+      if (fb_lds(c) > (size_t)kFbMaxLds) continue;
+      const double tiles = (double)((g.OH + th - 1) / th) * ((g.OW + tw - 1) / tw);
+      const double cost = tiles * ((double)c.HH * c.HWD * (C8y + C8x) + 0.25 * tp * (C8x + C8y));
+      if (cost < best * 0.999) {
+        best = cost;
+        found = true;
+        fg = c;
+      }
+    }
+  }
+  if (!found) return false;
+  fg.tiles_y = (g.OH + fg.TH - 1) / fg.TH;
+  fg.tiles_x = (g.OW + fg.TW - 1) / fg.TW;
+  fg.ntiles = (long)g.N * fg.tiles_y * fg.tiles_x <= (1L << 30) ? g.N * fg.tiles_y * fg.tiles_x : 0;
+  return fg.ntiles > 0;
+}
+
+int conv_bwd_fused_blocks(const ConvGeom& g) {
+  FusedBwdGeom fg;
+  if (!conv_bwd_fused_plan(g, fg)) return 0;
+  return std::min(fg.ntiles, kFusedBwdGrid);
+}
+
+int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
+  FusedBwdGeom fg;
+  if (!conv_bwd_fused_plan(g, fg)) return 8;
+  FusedBwdArgs a = a0;
+  a.N = g.N; a.H = g.IH; a.W = g.IW; a.Ci = g.Cgi; a.Co = g.Cgo; a.T = g.T;   // a.Kp: the dgrad packing's Kp
+  for (int t = 0; t < g.T; ++t) { a.dy[t] = g.dy[t]; a.dx[t] = g.dx[t]; }
+  const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
+  const size_t lds = fb_lds(fg);
+  const bool bwd = a.gy != nullptr, xpro = a.xc != nullptr, bne = a.bn_y != nullptr;
+#define FB_(NJ_, B_, X_, E_)                                                                                \
+  if (fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_) {                                                \
+    static bool lds_attr = false;                                                                            \
+    if (!lds_attr) {                                                                                         \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<NJ_, B_, X_, E_>),      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                      \
+      lds_attr = true;                                                                                       \
+    }                                                                                                        \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_>), dim3(grid), dim3(64 * kFbWaves), lds, s, a, fg); \
+    return 0;                                                                                                \
+  }
+#define FB4_(NJ_, B_) FB_(NJ_, B_, false, false) FB_(NJ_, B_, true, false) FB_(NJ_, B_, false, true) FB_(NJ_, B_, true, true)
+  FB4_(8, false) FB4_(8, true) FB4_(4, false) FB4_(4, true)
+#undef FB4_
+#undef FB_
+  return 8;
+}

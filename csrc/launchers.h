@@ -274,3 +274,38 @@ void comm_close(void* ptr);
 void comm_free(void* ptr);
 void oneshot_allreduce(const double* in, double* out, long n, const CommPeers& peers, int rank, int world, long cap,
                        unsigned long long* epoch, int* err, long long timeout, hipStream_t s);
+
+// conv_bwd.hip: fused data- + weight-gradient of a narrow stride-1 conv (one staging of dY and x per tile).
+// Geometry = the FORWARD conv (Gi = Go = 1, Cgi, Cgo <= 32, symmetric taps).  dY = bwd(dz, gy) when gy is set
+// (deferred BN-backward, gs/gk/grelu as ConvArgs::gy), else dz; x = relu?(xc scale/shift prologue) when xc is
+// set.  dxo <- dL/dx [N,H,W,Cgi]; bn_y/bn_coef/bn_relu/stat_part: the BN-backward partials epilogue (ConvArgs).
+// dw <- [conv_bwd_fused_blocks][Cgo][T*Cgi] fp32 slabs (summed by unpack_wgrad).  wd: the packed data-gradient
+// weights (ConvPlan.pack_dgrad), Kp = their row pitch.
+constexpr int kFusedBwdGrid = 512;   // persistent grid: 2 blocks on each of the 256 CUs
+struct FusedBwdArgs {
+  const uint16_t* dz;
+  const uint16_t* gy;
+  const float* gs;
+  const float* gk;
+  int grelu;
+  const uint16_t* x;
+  const float* xc;
+  int xrelu;
+  const uint16_t* wd;
+  int Kp;
+  uint16_t* dxo;
+  const uint16_t* bn_y;
+  const float* bn_coef;
+  int bn_relu;
+  float* stat_part;
+  float* dw;
+  int N, H, W, Ci, Co, T;
+  int dy[9], dx[9];
+};
+struct FusedBwdGeom {
+  int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, ntiles;
+  int py, px, KS, nj;
+};
+bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg);
+int conv_bwd_fused_blocks(const ConvGeom& g);   // 0: not eligible
+int conv_bwd_fused(const FusedBwdArgs& a, const ConvGeom& g, hipStream_t s);

@@ -141,11 +141,12 @@ class DeferredGrad:
 
 
 _DEFERRED = {}   # token data_ptr -> DeferredGrad (alive between a BN backward and its producers' backward)
-# env MSP_DEFER_DY=1 turns the deferral on.  Off by default: measured net-neutral on its own at bs320
-# (profiles/r04/kernels_deferdy_{on,off}_bs320.txt: bn_act_bwd_apply 73.6 -> 38.1 ms/step, but the halo
-# data- and weight-gradients each re-read y and are HBM-bound at ~4 TB/s: +41 ms/step, step +4 ms).  It
-# pays only where ONE kernel rebuilds dY for both the data- and the weight-gradient.
-DEFER_DY = os.environ.get('MSP_DEFER_DY', '0') == '1'
+# env MSP_DEFER_DY=0 turns the deferral off (A/B).  A deferred gradient pays only where ONE kernel rebuilds dY
+# for both the data- and the weight-gradient (ops.conv._fused_bwd, csrc/conv_bwd.hip); everywhere else the
+# consumer resolves it (the same apply pass as the materialised path).  Rebuilding it in the SEPARATE halo
+# data- and weight-gradient kernels measured net-neutral (profiles/r04/kernels_deferdy_{on,off}_bs320.txt:
+# bn_act_bwd_apply 73.6 -> 38.1 ms/step, but each kernel re-reads y: +41 ms/step).
+DEFER_DY = os.environ.get('MSP_DEFER_DY', '1') != '0'
 _DY_CONSUMERS = {'_ConvFnBackward', '_MultiConvFnBackward'}
 
 

@@ -16,6 +16,7 @@ Reference parity: ``nn.Conv2d`` / ``nn.ConvTranspose2d`` as used in ``models/mod
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -203,6 +204,54 @@ def _taps(tl):
     return [t[0] for t in tl], [t[1] for t in tl]
 
 
+# env MSP_FUSED_BWD=0: the narrow stride-1 convs run the separate data- and weight-gradient kernels (A/B)
+FUSED_BWD = os.environ.get('MSP_FUSED_BWD', '1') != '0'
+# env MSP_DEFER_DY_SEPARATE=1: a deferred BN data-gradient may also be rebuilt by the SEPARATE halo data- and
+# weight-gradient kernels (each re-reads y; measured net-neutral -- profiles/r04/kernels_deferdy_*): off, so
+# outside the fused backward a deferred gradient is resolved (= the apply pass of the materialised path)
+DEFER_SEPARATE = os.environ.get('MSP_DEFER_DY_SEPARATE', '0') == '1'
+
+
+def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
+    """Data- and weight-gradient of a narrow stride-1 single-group conv in ONE kernel (csrc/conv_bwd.hip):
+    dY (rebuilt from a deferred BN data-gradient when one arrives) and x (through the forward's deferred-BN
+    prologue) are staged once per tile; the BN epilogue of the data-gradient (BwdStatsHandle) runs in it too.
+    Returns (dxs, wgrads) or None when the shape is not eligible."""
+    if not (FUSED_BWD and need_dx and not plan.transposed and plan.stride == 1 and plan.Gi == 1 and plan.Go == 1
+            and plan.bias is None and plan.Cgi <= 32 and plan.Cgo <= 32 and 2 <= plan.T <= 9
+            and all(b.weight.requires_grad for b in plan.branches)):
+        return None
+    C = require()
+    n, ih, iw, oh, ow = shape
+    dims = plan.fwd_dims(n, ih, iw, oh, ow)
+    tdy, tdx = _taps(plan.taps_fwd)
+    nblk = C.conv_bwd_fused_blocks(dims, tdy, tdx)
+    if nblk <= 0:
+        return None
+    from .bn import claim_deferred, peek_deferred
+    d = peek_deferred(gys[0])
+    coefs, rmask = ctx.pro
+    xc = coefs[0] if coefs else None
+    wd, Kp_d = plan.pack_dgrad(dev)
+    dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
+    h = ctx.bn_handle
+    bne = h is not None and h.y is not None
+    part = torch.empty(nblk, 2, plan.Cgi, dtype=torch.float32, device=dev) if bne else None
+    dwp = torch.empty(nblk * plan.rows * plan.T * plan.Cip, dtype=torch.float32, device=dev)
+    C.conv_bwd_fused(d.dz if d is not None else gys[0],
+                     d.y if d is not None else None, d.stats if d is not None else None,
+                     d.coef if d is not None else None, bool(d.relu) if d is not None else False,
+                     xs[0], xc, bool(rmask & 1), wd, Kp_d, dxt,
+                     h.y if bne else None, h.stats if bne else None, bool(h.relu) if bne else False, part,
+                     dwp, dims, tdy, tdx)
+    if bne:
+        h.part = part
+    if d is not None:
+        claim_deferred(d)
+    need = [b.weight.requires_grad for b in plan.branches]
+    return [dxt], _unpack_slabs(plan, dwp, nblk, need)
+
+
 def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     """Deferred BN data-gradients among this launch's incoming gradient groups (``ops.bn.DeferredGrad``).
 
@@ -216,7 +265,7 @@ def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     if not any(d is not None for d in ds):
         return list(grads), None
     C = require()
-    ok = not plan.transposed and plan.stride == 1 and plan.bias is None
+    ok = DEFER_SEPARATE and not plan.transposed and plan.stride == 1 and plan.bias is None
     if ok and dgrad:
         ok = bool(C.conv_uses_halo(dims_d, taps_d[0], taps_d[1], False, True))
     if ok:
@@ -296,6 +345,13 @@ class _ConvFn(torch.autograd.Function):
         else:
             dy, dx = _taps(plan.taps_bwd)
             trans = plan.stride > 1
+        fused = _fused_bwd(ctx, plan, gys, xs, (n, ih, iw, oh, ow), need_dx, dev)
+        if fused is not None:
+            dxs, wgrads = fused
+            ctx.bn_handle = None
+            if plan.ready_hook is not None:
+                plan.ready_hook([b.weight for b in plan.branches])
+            return tuple([None, None, None, None, None] + dxs + wgrads)
         # deferred BN data-gradients: rebuilt in the staging of both launches below, or resolved here
         gys, bwd = _bwd_operands(gys, plan, dims_d, (dy, dx), plan.fwd_dims(n, ih, iw, oh, ow),
                                  _taps(plan.taps_fwd), dgrad=need_dx)
@@ -366,6 +422,15 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None):
     nrep = C.conv_wgrad_replicas(dims, dy, dx, False, bool(bk))   # split-K dW slabs, summed in fixed order
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
     C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask, **bk)
+    return _unpack_slabs(plan, dwp, nrep, need)
+
+
+def _unpack_slabs(plan: ConvPlan, dwp, nrep, need):
+    """dW of every branch from ``nrep`` split-K slabs [nrep][rows][T*Cip] (fixed-order sum, into the branch's
+    arena sink or a fresh fp32 tensor returned to autograd)."""
+    C = require()
+    KT = plan.T * plan.Cip
+    res = []
     cin_tot = plan.Gi * plan.ci_l
     for b, nd in zip(plan.branches, need):
         if not nd:

@@ -38,8 +38,17 @@ CASES = [
 ]
 
 
+MODES = [  # (deferred BN data-gradient, fused data+weight-gradient kernel, deferred dY in the separate kernels)
+    (True, False, True),     # the separate halo kernels' BN-backward prologue
+    (True, True, False),     # the fused backward consuming the deferred gradient (the default)
+    (False, True, False),    # the fused backward on a materialised dY
+]
+
+
+@pytest.mark.parametrize('mode', MODES)
 @pytest.mark.parametrize('case', CASES)
-def test_deferred_bn_data_gradient(gpu, case, monkeypatch):
+def test_deferred_bn_data_gradient(gpu, case, mode, monkeypatch):
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
     cin, co, (kh, kw), dil, n3, n1, (n, h, w), chain = case
     torch.manual_seed(5)
     convs = [nn.Conv2d(cin, co, (kh, kw), 1, (dil * (kh // 2), dil * (kw // 2)), (dil, dil), bias=False).to(gpu)
@@ -58,8 +67,10 @@ def test_deferred_bn_data_gradient(gpu, case, monkeypatch):
     gs = [to_fm_reference(_bf(torch.randn(n, co, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(9 + g))))
           for g in range(n3 + n1)]
     res, resolved = [], []
-    for defer in (False, True):
+    for defer, fused, separate in ((False, False, False), mode):
         monkeypatch.setattr(bnmod, 'DEFER_DY', defer)
+        monkeypatch.setattr(convmod, 'FUSED_BWD', fused)
+        monkeypatch.setattr(convmod, 'DEFER_SEPARATE', separate)
         for m in convs + bns + [bn1]:
             for p in m.parameters():
                 p.grad = None
@@ -100,7 +111,10 @@ def test_deferred_tokens_reach_the_halo_prologue(gpu, monkeypatch):
     calls = []
     orig = bnmod.resolve
 
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
     monkeypatch.setattr(bnmod, 'DEFER_DY', True)
+    monkeypatch.setattr(convmod, 'FUSED_BWD', False)
+    monkeypatch.setattr(convmod, 'DEFER_SEPARATE', True)
 
     def spy(g):
         calls.append(bnmod.peek_deferred(g) is not None)
@@ -120,3 +134,30 @@ def test_deferred_tokens_reach_the_halo_prologue(gpu, monkeypatch):
     z.backward(torch.randn_like(z))
     assert not any(calls), 'the single 17-channel 3x3 conv must consume the deferred gradient in its kernels'
     assert x.grad is not None and torch.isfinite(x.grad.float()).all()
+
+
+def test_fused_backward_runs_for_narrow_convs(gpu, monkeypatch):
+    """The 17-channel 3x3 chain conv takes the fused data+weight-gradient kernel (one launch, no separate
+    halo data-/weight-gradient launch) and consumes the deferred BN gradient without a resolve pass."""
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
+    monkeypatch.setattr(bnmod, 'DEFER_DY', True)
+    monkeypatch.setattr(convmod, 'FUSED_BWD', True)
+    calls = []
+    orig = convmod._fused_bwd
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r is not None)
+        return r
+    monkeypatch.setattr(convmod, '_fused_bwd', spy)
+    torch.manual_seed(2)
+    m = nn.Conv2d(17, 17, 3, 1, 2, 2, bias=False).to(gpu)
+    bnm = nn.BatchNorm2d(17).to(gpu)
+    plan = ConvPlan(3, 3, 17, 17, [Branch(m.weight, 0, 0, 9)], padding=(2, 2), dilation=(2, 2))
+    x = to_fm_reference(_bf(torch.randn(2, 17, 40, 48, device=gpu))).requires_grad_(True)
+    (y,), _ = conv(plan, [x])
+    z = materialize(bn_act([y], BNState.from_module(bnm), True, True, None, deferred=True, defer_bwd=True))
+    z.backward(torch.randn_like(z))
+    torch.cuda.synchronize()
+    assert calls == [True], calls
+    assert not bnmod._DEFERRED
