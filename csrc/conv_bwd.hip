@@ -27,11 +27,14 @@
 
 namespace {
 
-constexpr int kFbWaves = 4;
-constexpr int kFbLd = 8;          // staging vectors in flight per thread
+constexpr int kFbWaves = 4;       // compute waves: data- then weight-gradient of tile i
+constexpr int kFbProd = 4;        // staging waves: tile i + 1 into the other LDS buffer meanwhile
+constexpr int kFbThreads = 64 * (kFbWaves + kFbProd);
+constexpr int kFbLd = 16;         // staging vectors in flight per thread (the data-gradient accumulators are
+                                  // dead while staging: only the weight-gradient ones stay live)
 constexpr int kFbMaxKS = 24;      // data-gradient k-steps (T <= 9 taps x <= 4 slots / 4)
 constexpr int kFbMaxT = 9;
-constexpr int kFbMaxLds = 76 * 1024;
+constexpr int kFbMaxLds = 156 * 1024;  // two dY + x buffer pairs, the data-gradient weights, the BN partials
 constexpr int kFbSlack = 64;      // elements past each tile (the 24..31 channel over-read of the last pixel)
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -48,18 +51,21 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
 }
 
 template <int NJ, bool BWD, bool XPRO, bool BNE>
-__global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
+__global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
   extern __shared__ uint4 fb_smem[];
   constexpr int MI = 2;                       // 32 data-gradient rows (input channels <= 32)
   constexpr int NT = 3;                       // weight-gradient taps per wave (T <= 9 = 3 x 4 waves)
   constexpr int TP = kFbWaves * NJ * 16;      // pixels per tile
   constexpr int NCH = TP / 32;                // weight-gradient k chunks per tile
   const int hpx = fg.HH * fg.HWD;
-  uint16_t* tY = reinterpret_cast<uint16_t*>(fb_smem);
-  uint16_t* tX = tY + hpx * fg.py + kFbSlack;
-  float* s_stat = reinterpret_cast<float*>(tX + hpx * fg.px + kFbSlack);   // [waves][2][32]
+  const int pair = hpx * (fg.py + fg.px) + 2 * kFbSlack;   // elements of one dY + x buffer pair
+  uint16_t* const lds0 = reinterpret_cast<uint16_t*>(fb_smem);
+  const int wp = 32 * fg.KS + 8;                           // weight row pitch (elements; +16 B: bank spread)
+  uint16_t* const s_w = lds0 + 2 * pair;                   // [32 rows][wp] data-gradient weights, per block
+  float* s_stat = reinterpret_cast<float*>(s_w + 32 * wp);   // [waves][2][32]
   __shared__ float s_bt[BWD ? 5 * 32 : 1];    // dY rebuild table: scale, shift (+inf: no ReLU), k1, k2, k3
   __shared__ float s_xt[XPRO ? 3 * 32 : 1];   // x prologue: scale, shift, ReLU floor (0 / -inf)
+  __shared__ float s_bn[BNE ? 3 * 32 : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean
   __shared__ int s_ub[kFbMaxKS * 4];          // data-gradient unit -> dY tile offset
   __shared__ int s_wb[kFbMaxT];               // weight-gradient tap -> x tile offset (pixel units)
 
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
   const int Ci = a.Ci, Co = a.Co, T = a.T;
   const int C8y = Co >> 3, C8x = Ci >> 3;
   if constexpr (BWD) {
-    for (int c = tid; c < 32; c += 64 * kFbWaves) {
+    for (int c = tid; c < 32; c += kFbThreads) {
       const bool on = c < Co;
       s_bt[c] = on ? a.gs[c] : 0.f;
       s_bt[32 + c] = (on && a.grelu) ? a.gs[Co + c] : INFINITY;
@@ -78,14 +84,14 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
     }
   }
   if constexpr (XPRO) {
-    for (int c = tid; c < 32; c += 64 * kFbWaves) {
+    for (int c = tid; c < 32; c += kFbThreads) {
       const bool on = c < Ci;
       s_xt[c] = on ? a.xc[c] : 0.f;
       s_xt[32 + c] = on ? a.xc[Ci + c] : 0.f;
       s_xt[64 + c] = a.xrelu ? 0.f : -INFINITY;
     }
   }
-  for (int e = tid; e < fg.KS * 4; e += 64 * kFbWaves) {
+  for (int e = tid; e < fg.KS * 4; e += kFbThreads) {
     int ub = 0;
     if (e < T * C8y) {
       const int t = e / C8y, c8 = e - t * C8y;
@@ -95,8 +101,23 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
     s_ub[e] = ub;
   }
   if (tid < kFbMaxT) s_wb[tid] = tid < T ? (a.dy[tid] * fg.HWD + a.dx[tid]) : 0;
+  if constexpr (BNE) {
+    for (int c = tid; c < 32; c += kFbThreads) {
+      const bool on = c < Ci;
+      s_bn[c] = on ? a.bn_coef[c] : 0.f;
+      s_bn[32 + c] = (on && a.bn_relu) ? a.bn_coef[Ci + c] : INFINITY;
+      s_bn[64 + c] = on ? a.bn_coef[2 * Ci + c] : 0.f;
+    }
+  }
+  {   // the data-gradient weights stay resident: no global latency inside the k loop
+    const int rowv = 4 * fg.KS;   // uint4 per row
+    for (int e = tid; e < 32 * rowv; e += kFbThreads) {
+      const int r = e / rowv, k = e - r * rowv;
+      *reinterpret_cast<uint4*>(s_w + r * wp + 8 * k) = *reinterpret_cast<const uint4*>(a.wd + (long)r * a.Kp + 8 * k);
+    }
+  }
   if (BNE)
-    for (int c = tid; c < kFbWaves * 2 * 32; c += 64 * kFbWaves) s_stat[c] = 0.f;
+    for (int c = tid; c < kFbWaves * 2 * 32; c += kFbThreads) s_stat[c] = 0.f;
   __syncthreads();
 
   // data-gradient: the wave's NJ 16-pixel columns -> dY tile pixel offsets
@@ -127,21 +148,28 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
 
   const int per_img = fg.tiles_y * fg.tiles_x;
   const long img_px = (long)a.H * a.W;
-  for (int tt = blockIdx.x; tt < fg.ntiles; tt += gridDim.x) {
+  auto tile_origin = [&](int tt, int& ty0, int& tx0, long& imoff) {
     const int n = tt / per_img, trem = tt - n * per_img;
     const int tyi = trem / fg.tiles_x;
-    const int ty0 = tyi * fg.TH, tx0 = (trem - tyi * fg.tiles_x) * fg.TW;
-    const long imoff = (long)n * img_px;
-    if (tt != (int)blockIdx.x) __syncthreads();   // every wave is done with the previous tile's LDS
-    // ---- staging: dY = bwd(dz, y2) and x = prologue(y1), zero outside the image -------------------------
+    ty0 = tyi * fg.TH;
+    tx0 = (trem - tyi * fg.tiles_x) * fg.TW;
+    imoff = (long)n * img_px;
+  };
+  // staging of one tile by the staging waves (thread st of 64 * kFbProd) into the buffer pair tY / tX
+  auto stage = [&](int tt, uint16_t* tY, uint16_t* tX, int st) {
+    int ty0, tx0;
+    long imoff;
+    tile_origin(tt, ty0, tx0, imoff);
+    // staging: dY = bwd(dz, y2) and x = prologue(y1), zero outside the image -------------------------
     {
       const int totY = hpx * C8y, totX = hpx * C8x, tot = totY + totX;
-      for (int base = tid; base < tot; base += 64 * kFbWaves * kFbLd) {
-        uint4 v[kFbLd], w[kFbLd];
-        int dst[kFbLd], cc[kFbLd];
+      constexpr int LD = BWD ? (BNE ? 8 : 10) : kFbLd;   // two loads per dY vector when rebuilding it
+      for (int base = st; base < tot; base += 64 * kFbProd * LD) {
+        uint4 v[LD], w[LD];
+        int dst[LD], cc[LD];
 #pragma unroll
-        for (int u = 0; u < kFbLd; ++u) {
-          const int idx = base + u * 64 * kFbWaves;
+        for (int u = 0; u < LD; ++u) {
+          const int idx = base + u * 64 * kFbProd;
           v[u] = make_uint4(0, 0, 0, 0);
           w[u] = make_uint4(0, 0, 0, 0);
           dst[u] = -1;
@@ -150,8 +178,8 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
             const bool isy = idx < totY;
             const int e = isy ? idx : idx - totY;
             const int C8 = isy ? C8y : C8x;
-            const int hp = e / C8, c8 = e - hp * C8;
-            const int hy = hp / fg.HWD, hx = hp - hy * fg.HWD;
+            const int hp = fdiv(e, C8, isy ? fg.inv_c8y : fg.inv_c8x), c8 = e - hp * C8;
+            const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
             const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
             dst[u] = isy ? hp * fg.py + 8 * c8 : -2 - (hp * fg.px + 8 * c8);   // <= -2: an x-tile slot
             if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
@@ -167,7 +195,7 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
           }
         }
 #pragma unroll
-        for (int u = 0; u < kFbLd; ++u) {
+        for (int u = 0; u < LD; ++u) {
           if (dst[u] == -1) continue;
           uint4 val = v[u];
           if (dst[u] >= 0) {
@@ -187,28 +215,59 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
         }
       }
     }
-    __syncthreads();
+  };
+
+  const bool producer = wave >= kFbWaves;   // wave-uniform role
+  if (producer && (int)blockIdx.x < fg.ntiles) stage(blockIdx.x, lds0, lds0 + hpx * fg.py + kFbSlack, tid - 64 * kFbWaves);
+  __syncthreads();
+  int it = 0;
+  for (int tt = blockIdx.x; tt < fg.ntiles; tt += gridDim.x, ++it) {
+    uint16_t* const cur = lds0 + (it & 1) * pair;
+    if (producer) {
+      // tile i + 1 into the other pair (read by the compute waves during tile i - 1: released by the barrier)
+      const int nt = tt + gridDim.x;
+      uint16_t* const nxt = lds0 + ((it + 1) & 1) * pair;
+      if (nt < fg.ntiles) stage(nt, nxt, nxt + hpx * fg.py + kFbSlack, tid - 64 * kFbWaves);
+      __syncthreads();
+      continue;
+    }
+    int ty0, tx0;
+    long imoff;
+    tile_origin(tt, ty0, tx0, imoff);
+    const uint16_t* const tY = cur;
+    const uint16_t* const tX = cur + hpx * fg.py + kFbSlack;
 
     // ---- data-gradient: dz1 = conv(dY, W_d) (+ BN1 backward partials) -----------------------------------
     {
       const uint16_t* wrow[MI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) wrow[i] = a.wd + (long)(16 * i + lr) * a.Kp + 8 * lg;
+      for (int i = 0; i < MI; ++i) wrow[i] = s_w + (16 * i + lr) * wp + 8 * lg;
+      // BN1: this tile's y1 at the output pixels; the first row block's loads go out ahead of the k loop
+      // (their latency under the MFMAs), the second's ahead of the first block's epilogue
+      uint2 yy[MI][NJ];
+      auto pix = [&](int j) -> long {   // element offset of column j's output pixel (-1: outside the image)
+        const int p = (wave * NJ + j) * 16 + lr;
+        const int ty = ty0 + (p >> fg.tw_shift), tx = tx0 + (p & (fg.TW - 1));
+        return (ty < a.H && tx < a.W) ? (imoff + (long)ty * a.W + tx) * Ci : -1;
+      };
+      auto load_y = [&](int i) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const long pm = pix(j);
+          yy[i][j] = (pm >= 0 && 16 * i + 4 * lg < Ci) ? *reinterpret_cast<const uint2*>(a.bn_y + pm + 16 * i + 4 * lg)
+                                                       : make_uint2(0, 0);
+        }
+      };
+      if (BNE) load_y(0);
       f32x4_t acc[MI][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      uint4 A[MI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i]);
       for (int ks = 0; ks < fg.KS; ++ks) {
-        uint4 An[MI];
-        const bool more = ks + 1 < fg.KS;
-        if (more) {
+        uint4 A[MI];
 #pragma unroll
-          for (int i = 0; i < MI; ++i) An[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * (ks + 1));
-        }
+        for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * ks);
         const int ub = s_ub[4 * ks + lg];
         uint4 B[NJ];
 #pragma unroll
@@ -217,44 +276,33 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32(A[i], B[j], acc[i][j]);
-        if (more) {
-#pragma unroll
-          for (int i = 0; i < MI; ++i) A[i] = An[i];
-        }
       }
       // epilogue: dz1 (bf16, NHWC) for the in-image pixels and channels < Ci
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
+        if (BNE && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
         float sc[4], sh[4], mu[4];
         if (BNE) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            sc[r] = a.bn_coef[cb + r];
-            sh[r] = a.bn_relu ? a.bn_coef[Ci + cb + r] : INFINITY;
-            mu[r] = a.bn_coef[2 * Ci + cb + r];
+            sc[r] = s_bn[cb + r];
+            sh[r] = s_bn[32 + cb + r];
+            mu[r] = s_bn[64 + cb + r];
           }
         }
-        uint2 yy[NJ];
-        long pm[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const int p = (wave * NJ + j) * 16 + lr;
-          const int ty = ty0 + (p >> fg.tw_shift), tx = tx0 + (p & (fg.TW - 1));
-          pm[j] = (ty < a.H && tx < a.W) ? (imoff + (long)ty * a.W + tx) * Ci + cb : -1;
-          if (BNE) yy[j] = pm[j] >= 0 ? *reinterpret_cast<const uint2*>(a.bn_y + pm[j]) : make_uint2(0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          if (pm[j] < 0) continue;
+          const long pm = pix(j);
+          if (pm < 0) continue;
           const uint32_t lo = pack2(acc[i][j][0], acc[i][j][1]), hi = pack2(acc[i][j][2], acc[i][j][3]);
-          *reinterpret_cast<uint2*>(a.dxo + pm[j]) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(a.dxo + pm + cb) = make_uint2(lo, hi);
           if (BNE) {
             const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                  __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-            const float y4[4] = {__uint_as_float(yy[j].x << 16), __uint_as_float(yy[j].x & 0xffff0000u),
-                                 __uint_as_float(yy[j].y << 16), __uint_as_float(yy[j].y & 0xffff0000u)};
+            const float y4[4] = {__uint_as_float(yy[i][j].x << 16), __uint_as_float(yy[i][j].x & 0xffff0000u),
+                                 __uint_as_float(yy[i][j].y << 16), __uint_as_float(yy[i][j].y & 0xffff0000u)};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float gr = fmaf(y4[r], sc[r], sh[r]) > 0.f ? g4[r] : 0.f;
@@ -292,6 +340,7 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
         }
       }
     }
+    __syncthreads();   // tile i consumed, tile i + 1 staged
   }   // tile loop
 
   // ---- BN1 partials: this block's row -------------------------------------------------------------------
@@ -302,14 +351,14 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float s2 = row16_sum(cs[i][r]), q2 = row16_sum(cq[i][r]);
-        if (lr == 0 && cb + r < Ci) {
+        if (!producer && lr == 0 && cb + r < Ci) {
           s_stat[(wave * 2 + 0) * 32 + cb + r] = s2;
           s_stat[(wave * 2 + 1) * 32 + cb + r] = q2;
         }
       }
     }
     __syncthreads();
-    for (int c = tid; c < Ci; c += 64 * kFbWaves) {
+    for (int c = tid; c < Ci; c += kFbThreads) {
       float s2 = 0.f, q2 = 0.f;
 #pragma unroll
       for (int wv = 0; wv < kFbWaves; ++wv) { s2 += s_stat[(wv * 2 + 0) * 32 + c]; q2 += s_stat[(wv * 2 + 1) * 32 + c]; }
@@ -318,6 +367,7 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
     }
   }
   // ---- dW slab of this block: [Co][T * Ci], element (co, t*Ci + ci) -------------------------------------
+  if (producer) return;
   float* slab = a.dw + (long)blockIdx.x * Co * (T * Ci);
 #pragma unroll
   for (int m = 0; m < NT; ++m) {
@@ -338,8 +388,12 @@ __global__ __launch_bounds__(64 * kFbWaves, 2) void conv_bwd_fused_kernel(FusedB
   }
 }
 
+size_t fb_pair_lds(const FusedBwdGeom& fg) {
+  return ((size_t)fg.HH * fg.HWD * (fg.py + fg.px) + 2 * kFbSlack) * 2;
+}
+
 size_t fb_lds(const FusedBwdGeom& fg) {
-  return ((size_t)fg.HH * fg.HWD * (fg.py + fg.px) + 2 * kFbSlack) * 2 + (size_t)kFbWaves * 2 * 32 * 4;
+  return 2 * fb_pair_lds(fg) + (size_t)32 * (32 * fg.KS + 8) * 2 + (size_t)kFbWaves * 2 * 32 * 4;
 }
 
 }  // namespace
@@ -382,6 +436,9 @@ bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
     }
   }
   if (!found) return false;
+  fg.inv_c8y = 1.0f / (float)C8y;
+  fg.inv_c8x = 1.0f / (float)C8x;
+  fg.inv_hwd = 1.0f / (float)fg.HWD;
   fg.tiles_y = (g.OH + fg.TH - 1) / fg.TH;
   fg.tiles_x = (g.OW + fg.TW - 1) / fg.TW;
   fg.ntiles = (long)g.N * fg.tiles_y * fg.tiles_x <= (1L << 30) ? g.N * fg.tiles_y * fg.tiles_x : 0;
@@ -411,7 +468,7 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                      \
       lds_attr = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_>), dim3(grid), dim3(64 * kFbWaves), lds, s, a, fg); \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_>), dim3(grid), dim3(kFbThreads), lds, s, a, fg); \
     return 0;                                                                                                \
   }
 #define FB4_(NJ_, B_) FB_(NJ_, B_, false, false) FB_(NJ_, B_, true, false) FB_(NJ_, B_, false, true) FB_(NJ_, B_, true, true)

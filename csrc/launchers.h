@@ -281,7 +281,7 @@ void oneshot_allreduce(const double* in, double* out, long n, const CommPeers& p
 // set.  dxo <- dL/dx [N,H,W,Cgi]; bn_y/bn_coef/bn_relu/stat_part: the BN-backward partials epilogue (ConvArgs).
 // dw <- [conv_bwd_fused_blocks][Cgo][T*Cgi] fp32 slabs (summed by unpack_wgrad).  wd: the packed data-gradient
 // weights (ConvPlan.pack_dgrad), Kp = their row pitch.
-constexpr int kFusedBwdGrid = 512;   // persistent grid: 2 blocks on each of the 256 CUs
+constexpr int kFusedBwdGrid = 256;   // persistent grid: one (staging + compute waves) block per CU
 struct FusedBwdArgs {
   const uint16_t* dz;
   const uint16_t* gy;
@@ -305,6 +305,7 @@ struct FusedBwdArgs {
 struct FusedBwdGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, ntiles;
   int py, px, KS, nj;
+  float inv_c8y, inv_c8x, inv_hwd;   // fp32 reciprocals (fdiv) of the staging index math
 };
 bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg);
 int conv_bwd_fused_blocks(const ConvGeom& g);   // 0: not eligible
