@@ -890,6 +890,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_uses_halo", &conv_uses_halo_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"),
         py::arg("bwd") = false);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
+  m.def("conv_set_halo_split", [](int64_t mode) { conv_set_halo_split((int)mode); });
   m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });
   m.def("conv_gemm_force_cfg", [](int64_t c) { conv_gemm_force_cfg((int)c); });
   m.def("conv_gemm_num_cfgs", []() { return conv_gemm_num_cfgs(); });

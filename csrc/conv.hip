@@ -857,7 +857,18 @@ struct HaloGeom {
   int st_q, st_r, st_a, st_b;        // staging cursor step of 256 elements: 256 = st_q*C8 + st_r,
                                      // st_q = st_a*HWD + st_b (non-chunked: C8 = Cip/8)
   float inv_c8, inv_hwd, inv_cgi;   // fp32 reciprocals for fdiv (staging index math)
+  int split;                         // split-bank tile image (halo_phys): two copies, one per k-group parity
+  int tile_elems;                    // LDS elements of the tile image (both copies when split)
 };
+
+// Split-bank tile image.  CDNA4 services a ds_read_b128 in four 16-lane groups, each mixing lanes of two
+// MFMA k-groups: {0-3,12-15 | 20-27}, {4-11 | 16-19,28-31} (k-groups 0 | 1) and the same +32 (2 | 3).  With
+// one image the two k-groups read (tap, channel) units at unrelated offsets and collide (PMC: 0.23-0.41
+// bank-conflict rate).  Split: the tile is stored twice, copy h in the h-th 128-B half of every 256-B bank
+// row (logical 16-B slot s -> row s / 8, half h, column s % 8); k-groups of parity h read copy h.  A group's
+// 8 lanes per k-group read 8 consecutive pixels at an odd slot pitch -> 8 distinct columns of their half:
+// conflict-free for every tap offset, at twice the tile's LDS and staging stores.
+DEVI int halo_phys(int e, int smask) { return e + (e & smask); }   // smask = ~63 (split) or 0
 
 
 constexpr int kHaloMaxKS = 96;   // k-steps per channel chunk (4 (tap, 8-channel) units each)
@@ -909,7 +920,14 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
   }
   if (g.Gi > 1) __syncthreads();   // block-uniform; Gi == 1 staging never reads s_xp / s_yp
   // per-wave (sum, sum^2) rows after the tile: [kHaloWaves][2][rows] fp32
-  float* s_stat = reinterpret_cast<float*>(tile + hpx * hg.pitch);
+  float* s_stat = reinterpret_cast<float*>(tile + hg.tile_elems);
+  const int smask = hg.split ? ~63 : 0;                  // split-bank image (halo_phys)
+  const int hcopy = hg.split ? ((lg & 1) << 6) : 0;      // this lane's copy: k-group parity
+  auto st_tile = [&](int e, const uint4& val) {
+    uint4* tp = reinterpret_cast<uint4*>(tile + halo_phys(e, smask));
+    tp[0] = val;
+    if (hg.split) tp[8] = val;   // + 128 B: the other half of the bank row
+  };
   // deferred-BN prologue table after them (hg.xtab): per input channel scale, shift and the ReLU floor
   // (0 or -inf); groups without a prologue get the identity (exact on bf16 values)
   float* s_coef = s_stat + kHaloWaves * 2 * rows;
@@ -1029,7 +1047,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       if constexpr (BWD) {
         if (cc[u] >= 0) val = bwd8(val, yv[u], s_coef + cc[u], Cip);
       }
-      *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+      st_tile(dst[u], val);
     }
   };
   // Deferred-BN prologue as its own pass over the staged chunk (after the barrier that published it):
@@ -1041,7 +1059,8 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       const int hy = fdiv(hp, hg.HWD, hg.inv_hwd), hx = hp - __mul24(hy, hg.HWD);
       const int iy = ty0 + hg.ey0 + hy, ix = tx0 + hg.ex0 + hx;
       if ((unsigned)iy >= (unsigned)g.IH || (unsigned)ix >= (unsigned)g.IW) continue;
-      uint4* tp = reinterpret_cast<uint4*>(tile + __mul24(hp, hg.pitch) + c8 * 8);
+      const int te = __mul24(hp, hg.pitch) + c8 * 8;
+      const uint4* tp = reinterpret_cast<const uint4*>(tile + halo_phys(te, smask));
       const float* cp = s_coef + c0 + c8 * 8;
       const float4 s0 = *reinterpret_cast<const float4*>(cp), s1 = *reinterpret_cast<const float4*>(cp + 4);
       const float4 h0 = *reinterpret_cast<const float4*>(cp + Cip), h1 = *reinterpret_cast<const float4*>(cp + Cip + 4);
@@ -1053,7 +1072,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
       f[2] = fmaxf(fmaf(f[2], s0.z, h0.z), l0.z); f[3] = fmaxf(fmaf(f[3], s0.w, h0.w), l0.w);
       f[4] = fmaxf(fmaf(f[4], s1.x, h1.x), l1.x); f[5] = fmaxf(fmaf(f[5], s1.y, h1.y), l1.y);
       f[6] = fmaxf(fmaf(f[6], s1.z, h1.z), l1.z); f[7] = fmaxf(fmaf(f[7], s1.w, h1.w), l1.w);
-      *tp = pack8(f);
+      st_tile(te, pack8(f));
     }
   };
 
@@ -1134,7 +1153,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         f[6] = fmaxf(fmaf(f[6], s1.z, h1.z), l1.z); f[7] = fmaxf(fmaf(f[7], s1.w, h1.w), l1.w);
         val = pack8(f);
       }
-      *reinterpret_cast<uint4*>(tile + (pd[u] & 0xffff)) = val;
+      *reinterpret_cast<uint4*>(tile + (pd[u] & 0xffff)) = val;   // (PIPE: never split)
     }
   };
   if (PIPE) pipe_fetch(wgid);
@@ -1217,7 +1236,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
           if (dst[u] < 0) continue;
           uint4 val = v[u];
           if (cc[u] >= 0) val = bwd8(val, yv[u], s_coef + cc[u] * 8, Cip);
-          *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+          st_tile(dst[u], val);
         }
       } else if (!BNE && hg.xtab) {
 #pragma unroll
@@ -1239,12 +1258,12 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
             f[6] = fmaxf(fmaf(f[6], s1.z, h1.z), l1.z); f[7] = fmaxf(fmaf(f[7], s1.w, h1.w), l1.w);
             val = pack8(f);
           }
-          *reinterpret_cast<uint4*>(tile + dst[u]) = val;
+          st_tile(dst[u], val);
         }
       } else {
 #pragma unroll
         for (int u = 0; u < kHaloLd; ++u)
-          if (dst[u] >= 0) *reinterpret_cast<uint4*>(tile + dst[u]) = v[u];
+          if (dst[u] >= 0) st_tile(dst[u], v[u]);
       }
     }
     __syncthreads();
@@ -1297,7 +1316,7 @@ __global__ __launch_bounds__(64 * kHaloWaves, (CHUNKED || PIPE) ? 2 : ((MI <= 2 
         const int ub = s_ub[4 * ks + lg];
         uint4 B[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + pb[j] + ub);
+        for (int j = 0; j < NJ; ++j) B[j] = *reinterpret_cast<const uint4*>(tile + halo_phys(pb[j] + ub, smask) + hcopy);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1539,9 +1558,18 @@ static int conv_pick_wpx(const ConvGeom& g, int mi, int nj) {
 // whole (one chunk, LDS <= 64 KB) or -- single row group only -- in chunks of CC channels (CC | Cip, a
 // chunk's staging fits the kHaloLd registers per thread), widest CC first.
 static int halo_nj(int mi, bool pipe = false) { return (mi <= 2 && !pipe) ? 8 : 4; }
-static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows) {
-  return (size_t)HH * HWD * pitch * 2 + (size_t)kHaloWaves * 2 * rows * 4;
+static int halo_tile_elems(int HH, int HWD, int pitch, bool split) {
+  const int e = HH * HWD * pitch;
+  return split ? 2 * ((e + 63) / 64) * 64 : e;
 }
+static size_t halo_lds_bytes(int HH, int HWD, int pitch, int rows, bool split = false) {
+  return (size_t)halo_tile_elems(HH, HWD, pitch, split) * 2 + (size_t)kHaloWaves * 2 * rows * 4;
+}
+
+// split-bank image policy (halo_phys): 0 never, 1 (default) where it keeps the blocks per CU of the single
+// image, 2 wherever it fits the LDS cap (A/B: conv_set_halo_split)
+static int g_halo_split = 1;
+void conv_set_halo_split(int mode) { g_halo_split = mode; }
 
 // LDS cap of a halo tile + its stats rows + the prologue table.  Two blocks per CU hold up to ~76 KB of
 // dynamic LDS each (160 KB per CU minus the static tap tables); 64 KB measured 0.6 % slower per step
@@ -1630,6 +1658,17 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg, bool bwd =
       }
       hg.inv_hwd = 1.0f / (float)hg.HWD;
       hg.inv_cgi = 1.0f / (float)g.Cgi;
+      hg.split = 0;
+      if (!pipe && g_halo_split > 0) {
+        const size_t one = halo_lds_bytes(hg.HH, hg.HWD, pitch, rows) + tab + 2048;   // + static tables
+        const size_t two = halo_lds_bytes(hg.HH, hg.HWD, pitch, rows, true) + tab + 2048;
+        const int reg_blocks = pass == 1 ? 2 : ((mi <= 2 && nj <= 4) ? 4 : 3);   // conv_halo_kernel's bounds
+        const int per_cu = 160 * 1024;
+        const bool fits = two - 2048 <= halo_tile_cap();
+        const bool keeps = (int)(per_cu / two) >= std::min(reg_blocks, (int)(per_cu / one));
+        hg.split = fits && (g_halo_split == 2 || keeps) ? 1 : 0;
+      }
+      hg.tile_elems = halo_tile_elems(hg.HH, hg.HWD, pitch, hg.split != 0);
       return true;
     }
   }
@@ -1637,7 +1676,9 @@ static bool conv_halo_ok(const ConvGeom& g, bool trans, HaloGeom& hg, bool bwd =
   return false;
 }
 
-static size_t halo_lds(const HaloGeom& hg, int rows) { return halo_lds_bytes(hg.HH, hg.HWD, hg.pitch, rows); }
+static size_t halo_lds(const HaloGeom& hg, int rows) {
+  return halo_lds_bytes(hg.HH, hg.HWD, hg.pitch, rows, hg.split != 0);
+}
 
 static int g_halo_mode = -1;   // -1: from MSP_CONV_HALO (default on), 0: off, 1: on
 

@@ -84,6 +84,7 @@ int conv_wgrad_gemm_num_cfgs();
 int conv_pick_mi(int rows);
 int conv_rows_alloc(int rows);
 void conv_set_halo(int on);
+void conv_set_halo_split(int mode);   // 0 never, 1 occupancy-preserving (default), 2 wherever it fits
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
 // bwd: the launch carries a deferred BN-backward prologue (ConvArgs::gy): no PIPE variant, larger table
 bool conv_uses_halo(const ConvGeom& g, bool trans, bool bwd = false);

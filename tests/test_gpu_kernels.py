@@ -440,6 +440,39 @@ def test_conv_halo_matches_gather(gpu, case):
         C.conv_set_gemm(True)
 
 
+@pytest.mark.parametrize('case', HALO_CASES)
+def test_conv_halo_split_bank_image_is_bitwise(gpu, case):
+    """The split-bank tile image (two copies, one per k-group parity: csrc/conv.hip halo_phys) changes only
+    LDS addresses: forward, BN partials and data-gradient are bitwise those of the single image."""
+    from medical_segmentation_pytorch_amd.ops import _ext
+    C = _ext.require()
+    n, h, w, ci, co, (kh, kw), pad, dil, go = case
+    torch.manual_seed(4)
+    convs = [nn.Conv2d(ci, co, (kh, kw), 1, pad, dil, bias=False).to(gpu) for _ in range(go)]
+    plan = ConvPlan(kh, kw, ci, co, [Branch(c.weight, g, 0, kh * kw) for g, c in enumerate(convs)], padding=pad,
+                    dilation=dil, Go=go)
+    x = _bf(torch.randn(n, ci, h, w, device=gpu))
+    gs = [to_fm_reference(_bf(torch.randn(n, co, h, w, device=gpu, generator=torch.Generator(gpu).manual_seed(9 + i))))
+          for i in range(go)]
+    outs = []
+    C.conv_set_gemm(False)
+    try:
+        for mode in (0, 2):
+            C.conv_set_halo_split(mode)
+            xf = to_fm_reference(x).requires_grad_(True)
+            ys, part = conv(plan, [xf], want_stats=True)
+            torch.autograd.backward(ys, gs)
+            torch.cuda.synchronize()
+            outs.append(([y.clone() for y in ys], part.clone(), xf.grad.clone()))
+    finally:
+        C.conv_set_halo_split(1)
+        C.conv_set_gemm(True)
+    (y0, p0, d0), (y2, p2, d2) = outs
+    assert all(torch.equal(a, b) for a, b in zip(y0, y2))
+    assert torch.equal(p0, p2)
+    assert torch.equal(d0, d2)
+
+
 def _halo_vs_gather(gpu, case, C):
     n, h, w, ci, co, (kh, kw), pad, dil, go = case
     torch.manual_seed(4)

@@ -60,6 +60,8 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--miopen', action='store_true')
     ap.add_argument('--halo', type=int, default=1, help='1: halo-tiled stride-1 kernel where eligible, 0: gather only')
+    ap.add_argument('--split', type=int, default=1, help='halo split-bank tile image: 0 never, 1 occupancy-preserving '
+                    '(default), 2 wherever it fits (csrc/conv.hip halo_phys)')
     ap.add_argument('--only', default='', help='substring filter on layer names')
     ap.add_argument('--levels', default='', help='comma list of levels to run (e.g. 3,4,5,6)')
     ap.add_argument('--prologue', action='store_true',
@@ -69,6 +71,7 @@ def main():
     from medical_segmentation_pytorch_amd.ops import _ext
     C = _ext.require()
     C.conv_set_halo(bool(a.halo))
+    C.conv_set_halo_split(a.split)
     res = []
     tot = {'fwd': 0.0, 'dgrad': 0.0, 'wgrad': 0.0}
     for name, lvl, ci, co, k, s, p, d, groups in layers():
@@ -120,7 +123,7 @@ def main():
         print(f"{name:28s} fwd {t_f:7.3f} ms ({row['fwd_tflops']:6.1f} TF)  dgrad {t_d:7.3f} ({row['dgrad_tflops']:6.1f})"
               f"  wgrad {t_w:7.3f} ({row['wgrad_tflops']:6.1f})" +
               (f"  miopen-fwd {row['miopen_fwd_ms']:7.3f}" if a.miopen else ''), flush=True)
-    print(json.dumps({'batch': a.batch, 'size': a.size, 'halo': a.halo, 'layers': res, 'totals_ms': tot}))
+    print(json.dumps({'batch': a.batch, 'size': a.size, 'halo': a.halo, 'split': a.split, 'layers': res, 'totals_ms': tot}))
 
 
 if __name__ == '__main__':
