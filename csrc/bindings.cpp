@@ -307,6 +307,22 @@ void bn_act_apply_t(const at::Tensor& y, const at::Tensor& stats, const at::Tens
   bn_act_apply(bf(y), st, st + Cp, bf(z), P, Cp, relu ? 1 : 0, cur_stream());
 }
 
+void bn_add_act_t(const at::Tensor& y, const at::Tensor& sa, bool relu_a, const at::Tensor& x,
+                  const c10::optional<at::Tensor>& sb, bool relu_b, const at::Tensor& z, bool relu) {
+  CHECK_BF16(y); CHECK_BF16(x); CHECK_BF16(z); CHECK_F32(sa);
+  const int64_t Cp = y.size(-1), P = y.numel() / Cp;
+  TORCH_CHECK(Cp % 8 == 0 && x.numel() == P * Cp && z.numel() == P * Cp && sa.numel() == 4 * Cp, "bn_add_act shapes");
+  const float* a = f32(sa);
+  const float* b = nullptr;
+  if (sb.has_value() && sb->defined()) {
+    CHECK_F32(*sb);
+    TORCH_CHECK(sb->numel() == 4 * Cp, "bn_add_act: identity BN stats");
+    b = sb->data_ptr<float>();
+  }
+  bn_add_act(bf(y), a, a + Cp, relu_a ? 1 : 0, bf(x), b, b ? b + Cp : nullptr, relu_b ? 1 : 0, bf(z), P, (int)Cp,
+             relu ? 1 : 0, cur_stream());
+}
+
 void bn_act_bwd_partial_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& part,
                           int64_t P, int64_t Cp, bool relu) {
   CHECK_BF16(dz); CHECK_BF16(y); CHECK_F32(stats); CHECK_F32(part);
@@ -923,6 +939,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_reduce_bwd_finalize", &bn_reduce_bwd_finalize_t);
   m.def("bn_rf_chunks", [](int64_t Cp) { return bn_rf_chunks((int)Cp); });
   m.def("bn_act_apply", &bn_act_apply_t);
+  m.def("bn_add_act", &bn_add_act_t);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),
         py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("pscale") = 1.0);

@@ -256,6 +256,58 @@ __global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __
   }
 }
 
+// ResNet block tail in one pass: z = relu(o + r) with o = act_a(sa*y + ba) (the last BN of the block,
+// deferred) and r = act_b(sb*x + bb) (the downsample branch's BN, deferred) or the plain identity x
+// (sb == nullptr).  o and r are rounded to bf16 before the add, as their materialised tensors were:
+// bitwise the bn_act_apply (x2) + add_act chain, minus its intermediate tensors.
+__global__ __launch_bounds__(kBlock) void bn_add_act_kernel(const uint16_t* __restrict__ y,
+                                                            const float* __restrict__ sa,
+                                                            const float* __restrict__ ba, int relu_a,
+                                                            const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ sb,
+                                                            const float* __restrict__ bb, int relu_b,
+                                                            uint16_t* __restrict__ z, long P, int CG, int relu) {
+  const int R = kBlock / CG, tid = threadIdx.x, cg = tid % CG, r = tid / CG;
+  if (r >= R) return;
+  float a[8], b[8], c[8], d[8];
+  load8f(sa + 8 * cg, a);
+  load8f(ba + 8 * cg, b);
+  const bool defb = sb != nullptr;
+  if (defb) {
+    load8f(sb + 8 * cg, c);
+    load8f(bb + 8 * cg, d);
+  }
+  const float fa = relu_a ? 0.f : -INFINITY, fb = (defb && relu_b) ? 0.f : -INFINITY;
+  const long stride = (long)gridDim.x * R;
+  const long Cp = 8L * CG;
+  long p = (long)blockIdx.x * R + r;
+  for (; p < P; p += kUnroll * stride) {
+    uint4 in[kUnroll], iv[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      in[u] = q < P ? *reinterpret_cast<const uint4*>(y + q * Cp + 8 * cg) : make_uint4(0, 0, 0, 0);
+      iv[u] = q < P ? *reinterpret_cast<const uint4*>(x + q * Cp + 8 * cg) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long q = p + u * stride;
+      if (q >= P) break;
+      float v[8], w[8];
+      unpack8(in[u], v);
+      unpack8(iv[u], w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = bf2f(f2bf(fmaxf(fmaf(v[e], a[e], b[e]), fa)));
+        const float rr = defb ? bf2f(f2bf(fmaxf(fmaf(w[e], c[e], d[e]), fb))) : w[e];
+        const float t = o + rr;
+        v[e] = relu ? fmaxf(t, 0.f) : t;
+      }
+      *reinterpret_cast<uint4*>(z + q * Cp + 8 * cg) = pack8(v);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void bn_act_bwd_partial_kernel(
     const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, float* __restrict__ part, long P,
@@ -660,6 +712,12 @@ void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uin
                   int relu, hipStream_t s) {
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), 0, s, y, scale, shift, z, P,
                      Cp / 8, relu);
+}
+
+void bn_add_act(const uint16_t* y, const float* sa, const float* ba, int relu_a, const uint16_t* x, const float* sb,
+                const float* bb, int relu_b, uint16_t* z, long P, int Cp, int relu, hipStream_t s) {
+  hipLaunchKernelGGL(bn_add_act_kernel, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), 0, s, y, sa, ba, relu_a, x, sb, bb,
+                     relu_b, z, P, Cp / 8, relu);
 }
 
 void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

@@ -157,6 +157,9 @@ void bn_reduce_bwd_finalize(const float* part, long nblk, int C, int Cp, double*
                             float* coef, float pscale, hipStream_t s);
 void bn_act_apply(const uint16_t* y, const float* scale, const float* shift, uint16_t* z, long P, int Cp,
                   int relu, hipStream_t s);
+// z = relu(act_a(sa*y + ba) + (sb ? act_b(sb*x + bb) : x)): the ResNet block tail (bitwise the apply + add_act chain)
+void bn_add_act(const uint16_t* y, const float* sa, const float* ba, int relu_a, const uint16_t* x, const float* sb,
+                const float* bb, int relu_b, uint16_t* z, long P, int Cp, int relu, hipStream_t s);
 void bn_act_bwd_partial(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
                         const float* mean, float* part, long P, int Cp, int relu, hipStream_t s);
 void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const float* scale,

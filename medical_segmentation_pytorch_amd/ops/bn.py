@@ -301,6 +301,8 @@ def flush_pending():
     _FWD.flush()
     _BWD.flush()
     clear_deferred()
+    from .conv import check_parked_grads
+    check_parked_grads()
 
 
 def _world(group):

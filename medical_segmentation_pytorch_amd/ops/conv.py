@@ -284,6 +284,39 @@ def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     return gys, (gy, gs, gk, grelu, [d for d in ds if d is not None])
 
 
+# Identity-branch data-gradients waiting for the conv that shares their input (``ops.pool.res_tail``): a
+# ResNet identity block's input x feeds conv1 and the block tail.  The tail's backward parks dL/dx of the
+# identity path here (keyed by x's storage) instead of returning it; conv1's backward then accumulates its
+# data-gradient into it in the GEMM / halo epilogue (``accumulate=True``) and returns the sum -- no
+# autograd bf16 add of the two contributions.
+_GRAD_ACC = {}
+
+
+def park_input_grad(x, g):
+    """``g`` is (part of) dL/dx: the next conv backward whose input is ``x`` returns its dgrad + g."""
+    key = x.data_ptr()
+    assert key not in _GRAD_ACC, 'one parked identity gradient per tensor'
+    _GRAD_ACC[key] = (g, tuple(x.shape))
+
+
+def check_parked_grads():
+    """Step boundary: every parked identity gradient has been claimed (else a gradient was lost)."""
+    if _GRAD_ACC:
+        n = len(_GRAD_ACC)
+        _GRAD_ACC.clear()
+        raise RuntimeError(f'{n} parked identity gradient(s) never claimed by their conv')
+
+
+def _claim_parked(xs, nx):
+    if not _GRAD_ACC or nx != 1:
+        return None
+    ent = _GRAD_ACC.get(xs[0].data_ptr())
+    if ent is None or ent[1] != tuple(xs[0].shape):
+        return None
+    del _GRAD_ACC[xs[0].data_ptr()]
+    return ent[0]
+
+
 class _ConvFn(torch.autograd.Function):
     # pro = (coefs, relu mask): deferred-BN prologue of the input groups (ops.bn.Deferred); the same
     # prologue runs again in the weight-gradient staging, so z never exists in HBM
@@ -348,6 +381,9 @@ class _ConvFn(torch.autograd.Function):
         fused = _fused_bwd(ctx, plan, gys, xs, (n, ih, iw, oh, ow), need_dx, dev)
         if fused is not None:
             dxs, wgrads = fused
+            parked = _claim_parked(xs, ctx.nx) if need_dx else None
+            if parked is not None and dxs[0] is not None:
+                dxs[0].add_(parked)
             ctx.bn_handle = None
             if plan.ready_hook is not None:
                 plan.ready_hook([b.weight for b in plan.branches])
@@ -357,11 +393,18 @@ class _ConvFn(torch.autograd.Function):
                                  _taps(plan.taps_fwd), dgrad=need_dx)
         bk = {} if bwd is None else dict(gy=bwd[0], gs=bwd[1], gk=bwd[2], grelu=bwd[3])
         dxs = [None] * ctx.nx
+        parked = _claim_parked(xs, ctx.nx) if need_dx else None
+        # (the parked tensor may also be this conv's own output gradient: then the sum goes to a fresh tensor)
+        in_place = parked is not None and all(g.data_ptr() != parked.data_ptr() for g in gys)
         if need_dx:
             wd, Kp_d = plan.pack_dgrad(dev)
             dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
             h = ctx.bn_handle
-            if h is not None and h.y is not None and not trans:
+            if in_place and not trans and plan.Gi == 1 and (h is None or h.y is None):
+                # dL/dx = this dgrad + the parked identity-branch gradient, summed in the epilogue
+                C.conv_fwd(gys, wd, [parked], None, None, dims_d, dy, dx, False, accumulate=True, **bk)
+                dxs, parked = [parked], None
+            elif h is not None and h.y is not None and not trans:
                 # dL/dx is the BN output's gradient: emit the BN backward partials in the epilogue
                 nblk = C.conv_stat_blocks(dims_d, dy, dx, False, bwd is not None)
                 part = torch.empty(nblk, 2, plan.Gi * plan.Cgi, dtype=torch.float32, device=dev)
@@ -369,6 +412,8 @@ class _ConvFn(torch.autograd.Function):
                 h.part = part
             else:
                 C.conv_fwd(gys, wd, dxs, None, None, dims_d, dy, dx, trans, **bk)
+            if parked is not None:   # (a launch without the accumulate epilogue: one bf16 add)
+                dxs[0].add_(parked)
             ctx.bn_handle = None
         wgrads = _conv_wgrad(plan, gys, xs, (n, ih, iw, oh, ow), dev, ctx.pro, bk)
         if bwd is not None:

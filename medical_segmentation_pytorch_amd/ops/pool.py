@@ -5,14 +5,15 @@
   per element; the backward gathers (deterministic, no atomics).
 * :func:`up2_cat` -- smp ``UnetDecoderBlock``: ``cat([interpolate(x, 2, 'nearest'), skip], 1)`` written
   once into a dense channel range (the following conv then sees one ordinary input).
-* :func:`add_act` -- the ResNet block tail ``relu(bn(conv(x)) + identity)``.
+* :func:`add_act` -- the ResNet block tail ``relu(bn(conv(x)) + identity)`` on materialised inputs;
+  :func:`res_tail` -- the same from the deferred BN outputs in one pass (training).
 """
 from __future__ import annotations
 
 import torch
 
 from ._ext import require
-from .bn import need_grads
+from .bn import materialize, need_grads
 from .fm import cpad
 
 
@@ -86,6 +87,51 @@ class _AddAct(torch.autograd.Function):
         g = torch.empty_like(z)
         C.relu_bwd(dz.contiguous(), z, g)
         return g, g, None
+
+
+class _ResTail(torch.autograd.Function):
+    """relu(o + r): o a deferred BN output (the block's last BN), r the identity -- a plain tensor or the
+    deferred downsample BN -- in ONE pass (``bn_add_act``; no materialised o / r).  Backward: g = dz * (z > 0)
+    is the gradient of both o and r (the deferred aliases take dL/d(BN output)); with ``park`` the identity's
+    share is parked for conv1, which shares the block input x and adds it in its data-gradient epilogue
+    (``ops.conv.park_input_grad``) instead of autograd adding two bf16 tensors."""
+
+    @staticmethod
+    def forward(ctx, a_t, a_stats, a_relu, b_t, b_stats, b_relu, park):
+        C = require()
+        a_t, b_t = a_t.contiguous(), b_t.contiguous()
+        z = torch.empty_like(a_t)
+        C.bn_add_act(a_t, a_stats, a_relu, b_t, b_stats, b_relu, z, True)
+        ctx.save_for_backward(z)
+        ctx.park = park and b_stats is None
+        ctx.b_ref = b_t if ctx.park else None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        need_grads([dz])
+        C = require()
+        (z,) = ctx.saved_tensors
+        g = torch.empty_like(z)
+        C.relu_bwd(dz.contiguous(), z, g)
+        if ctx.park:
+            from .conv import park_input_grad
+            park_input_grad(ctx.b_ref, g)
+            ctx.b_ref = None
+            return g, None, None, None, None, None, None
+        return g, None, None, g, None, None, None
+
+
+def res_tail(o, idt, park_identity=False):
+    """ResNet block tail ``relu(o + idt)``: fused when ``o`` is a deferred BN output (training), else the
+    materialised add_act.  ``park_identity``: ``idt`` is the block input and conv1 (one of ours) reads it."""
+    from .bn import Deferred, need_stats
+    if not isinstance(o, Deferred):
+        return add_act(materialize(o), materialize(idt), relu=True)
+    need_stats([o, idt])
+    if isinstance(idt, Deferred):
+        return _ResTail.apply(o.t, o.stats, bool(o.relu), idt.t, idt.stats, bool(idt.relu), False)
+    return _ResTail.apply(o.t, o.stats, bool(o.relu), idt, None, False, bool(park_identity))
 
 
 def maxpool(x, k=3, s=2, p=1):

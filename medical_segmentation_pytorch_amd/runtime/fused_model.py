@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
-from ..ops.pool import add_act, maxpool, up2_cat
+from ..ops.pool import maxpool, res_tail, up2_cat
 from .fused_decoders import SmpDecoders, fused_decoder_kind
 
 
@@ -486,7 +486,8 @@ class FusedExecutor(SmpDecoders):
             o = self.conv_bn(blk.conv3, blk.bn3, o, training, relu=False)
         else:
             o = self.conv_bn(blk.conv2, blk.bn2, o, training, relu=False)
-        return add_act(materialize(o), materialize(idt), relu=True)
+        # one pass from the deferred BN outputs; an identity block parks the identity gradient for conv1
+        return res_tail(o, idt, park_identity=blk.downsample is None)
 
     def resnet_encoder(self, enc, images, training):
         """smp ResNet encoder stages 1..depth as NHWC bf16 feature maps (dilated output-stride-8/16

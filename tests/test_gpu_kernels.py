@@ -694,3 +694,78 @@ def test_ohem_in_captured_graph(gpu):
         ref.backward()
         assert abs(out.item() - ref.item()) < 1e-5, (scale, out.item(), ref.item())
         assert _rel(x.grad, xr.grad) < 1e-4
+
+
+@pytest.mark.parametrize('deferred_identity', [False, True])
+def test_res_tail_bitwise_and_parked_identity_gradient(gpu, deferred_identity):
+    """ResNet block tail in one pass (``bn_add_act``) is bitwise the materialise + add_act chain; its
+    backward parks the identity gradient for conv1, whose data-gradient epilogue adds it: dL/dx equals the
+    autograd sum of the two contributions (to one bf16 rounding)."""
+    from medical_segmentation_pytorch_amd.ops import pool
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
+    from medical_segmentation_pytorch_amd.ops.bn import Deferred, materialize
+    torch.manual_seed(3)
+    n, h, w, c = 2, 12, 20, 64
+    yd = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+    x0 = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+
+    def stats():
+        st = torch.zeros(4, c, device=gpu)
+        st[0].uniform_(0.5, 1.5)
+        st[1].uniform_(-0.5, 0.5)
+        return st
+    sa, sb = stats(), stats()
+    m = nn.Conv2d(c, c, 1, bias=False).to(gpu)
+    plan = ConvPlan(1, 1, c, c, [Branch(m.weight, 0, 0, 1)], padding=(0, 0))
+    dz = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+    res = []
+    for fused in (False, True):
+        m.weight.grad = None
+        x = x0.clone().requires_grad_(True)
+        (c1,), _ = conv(plan, [x])   # conv1 of the block reads the block input; the tail consumes its chain
+        t = c1 * 1.0   # (in a block, conv1's output gradient comes from bn1: never the tail's tensor)
+        o = Deferred(t, sa, False)
+        idt = Deferred(yd.clone().requires_grad_(True), sb, False) if deferred_identity else x
+        if fused:
+            z = pool.res_tail(o, idt, park_identity=not deferred_identity)
+        else:
+            z = pool.add_act(materialize(o), materialize(idt), relu=True)
+        t.retain_grad()
+        z.backward(dz)
+        torch.cuda.synchronize()
+        convmod.check_parked_grads()
+        res.append((z.detach().clone(), t.grad.clone(), x.grad.clone(), m.weight.grad.clone()))
+    (z0, t0, x0g, w0), (z1, t1, x1g, w1) = res
+    assert torch.equal(z0, z1)
+    assert torch.equal(t0, t1)
+    # the epilogue adds the parked gradient to the fp32 accumulator and rounds once (autograd rounds the
+    # dgrad to bf16, then adds): within a bf16 rounding, not bitwise
+    assert _rel(x1g, x0g) < 4e-3
+    assert torch.equal(w0, w1)
+
+
+def test_parked_gradient_aliasing_its_own_dy_is_not_overwritten(gpu):
+    """A parked identity gradient that is also the conv's own dY (conv output read by the tail directly)
+    must not be accumulated into in place: the weight gradient reads dY after the data-gradient."""
+    from medical_segmentation_pytorch_amd.ops import pool
+    from medical_segmentation_pytorch_amd.ops.bn import Deferred, materialize
+    torch.manual_seed(5)
+    n, h, w, c = 2, 8, 12, 64
+    x0 = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+    st = torch.zeros(4, c, device=gpu)
+    st[0] = 1.0
+    m = nn.Conv2d(c, c, 1, bias=False).to(gpu)
+    plan = ConvPlan(1, 1, c, c, [Branch(m.weight, 0, 0, 1)], padding=(0, 0))
+    dz = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+    res = []
+    for fused in (False, True):
+        m.weight.grad = None
+        x = x0.clone().requires_grad_(True)
+        (c1,), _ = conv(plan, [x])
+        o = Deferred(c1, st, False)
+        z = pool.res_tail(o, x, park_identity=True) if fused else pool.add_act(materialize(o), x, relu=True)
+        z.backward(dz)
+        torch.cuda.synchronize()
+        res.append((x.grad.clone(), m.weight.grad.clone()))
+    assert _rel(res[1][0], res[0][0]) < 4e-3
+    assert torch.equal(res[1][1], res[0][1])
