@@ -35,6 +35,8 @@ CASES = [
     (17, 17, (3, 3), 1, 1, 1, (2, 24, 32), False),     # Go = 2: 3x3 + 1x1 at the centre tap, both deferred
     (17, 17, (3, 3), 1, 5, 3, (2, 24, 32), False),     # DUCK fused-8: chunked data-gradient -> resolved
     (64, 64, (3, 3), 1, 1, 0, (2, 16, 16), False),     # >= 64 channels: GEMM kernels -> resolved
+    (17, 17, (3, 3), 1, 1, 0, (12, 128, 128), True),   # 384 tiles > the 256-block persistent grid: blocks
+                                                       # loop over tiles (the double-buffered staging)
 ]
 
 

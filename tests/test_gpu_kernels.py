@@ -769,3 +769,4 @@ def test_parked_gradient_aliasing_its_own_dy_is_not_overwritten(gpu):
         res.append((x.grad.clone(), m.weight.grad.clone()))
     assert _rel(res[1][0], res[0][0]) < 4e-3
     assert torch.equal(res[1][1], res[0][1])
+

@@ -35,21 +35,22 @@ def _pretrain(model, gpu, size, batch, steps):
     """A well-conditioned gradient oracle: at random init, training-mode DUCKNet / small ResNets amplify ANY
     bf16 rounding (PyTorch's own autocast reached only 0.15-0.27 mean grad cos vs fp32 on DUCKNet,
     profiles/r03/parity_probe_ducknet_train.log), so the weights are first trained ``steps`` Adam steps on
-    input-correlated synthetic labels (the fused training step itself, same batch shape)."""
-    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep
+    input-correlated synthetic labels.  The pretraining is EAGER fp32 on PyTorch's native kernels
+    (MIOpen off): the oracle weights do not depend on the fused engine under test, so a kernel change
+    cannot move the oracle itself (fused-step pretraining did: autocast mean cos 0.83-0.94 between builds)."""
     g = torch.Generator().manual_seed(7)
-    xs = torch.empty(batch, 3, size, size, device=gpu)
-    ys = torch.empty(batch, size, size, dtype=torch.long, device=gpu)
-
-    def feed(x, y):
-        x.copy_(torch.randn(batch, 3, size, size, generator=g).to(gpu))
-        y.copy_((F.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long())
-    step = FusedStep(model, xs, ys, optimizer='adam', lr=1e-3, use_graph=False, feed=feed, total_steps=steps + 1,
-                     pct_start=0.1)
-    for _ in range(steps):
-        step()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=1e-3, total_steps=steps + 1, pct_start=0.1)
+    with torch.backends.cudnn.flags(enabled=False):
+        for _ in range(steps):
+            x = torch.randn(batch, 3, size, size, generator=g).to(gpu)
+            y = (F.avg_pool2d(x[:, :1], 9, 1, 4)[:, 0] > 0).long()
+            opt.zero_grad(set_to_none=True)
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+            sched.step()
     torch.cuda.synchronize()
-    for p in model.parameters():   # (the arena grad views of the pretraining engine)
+    for p in model.parameters():
         p.grad = None
     return model
 
@@ -63,7 +64,8 @@ ILL_CONDITIONED = 128 * 8   # size * batch of the two bottleneck-ResNet cases (s
 # after 100 or 300 pretraining steps, at 64 px / batch 2 and at 128 px / batch 8 alike (its layer2/3 BN
 # parameters at 0.2-0.4) -- the fused engine matches autocast there to 0.001 (0.5615 vs 0.5610, 0.6473 vs
 # 0.6463); for them the test asserts that parity, not the absolute 0.9 (ILL_CONDITIONED below).
-MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64, 4),
+# (DUCKNet at 256 px: at 128 px autocast itself only reaches 0.83-0.86 -- its stage 4-5 BNs see 16x16 / 8x8 maps)
+MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 256, 4), (lambda: UNet(2, 3, 32), 64, 4),
                                                  (lambda: _smp_unet('resnet18'), 64, 4),
                                                  (lambda: _smp_unet('resnet50'), 128, 8, 100),
                                                  # grouped 3x3 (MIOpen channels-last) between fused ops
@@ -71,7 +73,7 @@ MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 128, 4), (lambda: UNet(2, 3, 32), 64,
                                                  # fully fused decoders (runtime/fused_decoders.py)
                                                  (lambda: _smp('UnetPlusPlus', 'resnet18'), 64, 4),
                                                  (lambda: _smp('FPN', 'resnet18'), 64, 4),
-                                                 (lambda: _smp('DeepLabV3Plus', 'resnet18'), 64, 4),
+                                                 (lambda: _smp('DeepLabV3Plus', 'resnet18'), 128, 4),
                                                  # output stride 8: at 64 px the dilation-4 layer4 sees
                                                  # 8x8 maps (mostly padding taps) and even bf16 autocast
                                                  # only reaches grad cos ~0.92 vs fp32 -- 128 px is stable
@@ -127,8 +129,8 @@ def test_fused_matches_eager(gpu, model_fn, size, batch, steps):
             assert p.grad is None or not p.grad.any()
             continue
         assert p.grad is not None
-        if q.grad.abs().sum() > 0:
-            cf.append(_cos(p.grad, q.grad))
+        if q.grad.abs().sum() > 0 and q.grad.numel() > 1:   # (a 1-element "cosine" is only a sign test:
+            cf.append(_cos(p.grad, q.grad))                   # PAN's 1-channel FPA BNs -- not scored)
             cb.append(_cos(r.grad, q.grad))
             names.append(name)
     # Parameters whose exact gradient is ~0 -- a conv bias feeding a training BatchNorm, whose mean the BN

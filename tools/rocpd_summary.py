@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 ``*_results.db`` (rocpd SQLite) into a per-kernel time table.
 
-Usage: python tools/rocpd_summary.py path/to/results.db [--top 40] [--steps N] [--group]
+Usage: python tools/rocpd_summary.py path/to/results.db [--top 40] [--steps N] [--group] [--window]
 ``--group`` buckets kernels into families (conv fwd / dgrad / wgrad / BN / elementwise ...).
+``--window``: only the last ``--steps`` steady-state steps, marker to marker (the once-per-step fused
+optimizer kernel, ``--marker``) -- excludes warmup / graph-capture work (e.g. the setup copies).
 """
 import argparse
 import collections
@@ -27,9 +29,16 @@ def main():
     ap.add_argument('--top', type=int, default=40)
     ap.add_argument('--steps', type=int, default=1)
     ap.add_argument('--group', action='store_true')
+    ap.add_argument('--window', action='store_true')
+    ap.add_argument('--marker', default=r'adam_kernel|sgd_kernel|Adam')
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
-    rows = db.execute('select name, start, end from kernels').fetchall()
+    rows = db.execute('select name, start, end from kernels order by start').fetchall()
+    if a.window:
+        marks = [i for i, r in enumerate(rows) if re.search(a.marker, r[0])]
+        if len(marks) < a.steps + 1:
+            raise SystemExit(f'--window: marker found {len(marks)} times, need {a.steps + 1}')
+        rows = rows[marks[-a.steps - 1] + 1:marks[-1] + 1]
     tot = collections.defaultdict(float)
     cnt = collections.Counter()
     for name, s, e in rows:
