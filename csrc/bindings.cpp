@@ -535,7 +535,10 @@ void aug_batch_t(const at::Tensor& images, const at::Tensor& masks, const at::Te
   TORCH_CHECK(ip.is_cuda() && ip.scalar_type() == at::kInt && ip.is_contiguous());
   TORCH_CHECK(out.dim() == 4 && out.size(1) == 3, "out must be [B, 3, H, W]");
   const int B = out.size(0), H = out.size(2), W = out.size(3);
-  TORCH_CHECK(ip.numel() == (int64_t)B * kAugIParams && fp.numel() == (int64_t)B * 4 && mean.numel() >= B);
+  // mean: [B] floats, then (8-B aligned) the fp64 slice partials of the gray mean
+  const int64_t poff = ((int64_t)B + 1) / 2 * 2;
+  TORCH_CHECK(ip.numel() == (int64_t)B * kAugIParams && fp.numel() == (int64_t)B * 4 &&
+              mean.numel() >= poff + 2 * (int64_t)aug_gray_scratch_doubles(B), "aug: mean [B + gray partials]");
   TORCH_CHECK(work.numel() == (int64_t)B * H * W * 3 && mask_out.numel() == (int64_t)B * H * W);
   TORCH_CHECK(meta.dim() == 2 && meta.size(1) == 4 && norm_mean.size() == 3 && norm_std.size() == 3);
   auto s = cur_stream();
@@ -545,7 +548,7 @@ void aug_batch_t(const at::Tensor& images, const at::Tensor& masks, const at::Te
     const int st = (int)stages[k];
     TORCH_CHECK(st >= 0 && st < 4);
     if (std::find(contrast_stages.begin(), contrast_stages.end(), stages[k]) != contrast_stages.end())
-      aug_gray_mean(f32(work), f32(mean), B, H * W, s);
+      aug_gray_mean(f32(work), f32(mean), reinterpret_cast<double*>(f32(mean) + poff), B, H * W, s);
     aug_color(f32(work), ip.data_ptr<int>(), f32(fp), f32(mean), B, H * W, st, s);
   }
   const float m3[3] = {(float)norm_mean[0], (float)norm_mean[1], (float)norm_mean[2]};
@@ -940,6 +943,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_rf_chunks", [](int64_t Cp) { return bn_rf_chunks((int)Cp); });
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_add_act", &bn_add_act_t);
+  m.def("aug_gray_scratch_doubles", &aug_gray_scratch_doubles);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),
         py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("pscale") = 1.0);

@@ -196,7 +196,8 @@ void relu_bwd(const uint16_t* dz, const uint16_t* z, uint16_t* g, long n_elem, h
 constexpr int kAugIParams = 14;
 void aug_geometry(const uint8_t* images, const uint8_t* masks, const int64_t* meta, const int* ip, float* work,
                   int64_t* mask_out, int B, int CH, int CW, hipStream_t s);
-void aug_gray_mean(const float* work, float* mean, int B, int HW, hipStream_t s);
+int aug_gray_scratch_doubles(int B);   // fp64 partials aug_gray_mean needs
+void aug_gray_mean(const float* work, float* mean, double* part, int B, int HW, hipStream_t s);
 void aug_color(float* work, const int* ip, const float* fp, const float* mean, int B, int HW, int stage,
                hipStream_t s);
 void aug_finalize(const float* work, const int* ip, float* out, int B, int HW, const float* mean3, const float* std3,

@@ -80,7 +80,7 @@ class DeviceAugLoader:
 
     def __init__(self, dataset, batch_size, device, sampler=None, shuffle=True, drop_last=True, seed=0,
                  binary_float=False, data=None, aug=None):
-        require()
+        C = require()
         self.dataset = dataset
         self.data = data if data is not None else DeviceDataset(dataset, device)
         self.batch_size = batch_size
@@ -102,7 +102,9 @@ class DeviceAugLoader:
         ch, cw = aug.crop
         B = batch_size
         self.work = torch.empty(B * ch * cw * 3, dtype=torch.float32, device=device)
-        self.mean = torch.empty(B, dtype=torch.float32, device=device)
+        # [B] per-sample gray means + (8-B aligned) the fp64 slice partials of their reduction
+        self.mean = torch.empty((B + 1) // 2 * 2 + 2 * C.aug_gray_scratch_doubles(B), dtype=torch.float32,
+                                device=device)
         self.norm_mean = [float(v) for v in aug.mean]
         self.norm_std = [float(v) for v in aug.std]
         self.device = device
