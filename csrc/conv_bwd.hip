@@ -30,6 +30,9 @@ namespace {
 constexpr int kFbWaves = 4;       // compute waves: data- then weight-gradient of tile i
 constexpr int kFbProd = 4;        // staging waves: tile i + 1 into the other LDS buffer meanwhile
 constexpr int kFbThreads = 64 * (kFbWaves + kFbProd);
+#ifndef FB_LD_BNE
+#define FB_LD_BNE 8   // (12 / 16 spill: 4.37 / 4.70 ms vs 3.47 ms, tools/dev/fused_bwd_bench.py)
+#endif
 constexpr int kFbLd = 16;         // staging vectors in flight per thread (the data-gradient accumulators are
                                   // dead while staging: only the weight-gradient ones stay live)
 constexpr int kFbMaxKS = 24;      // data-gradient k-steps (T <= 9 taps x <= 4 slots / 4)
@@ -65,7 +68,9 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
   float* s_stat = reinterpret_cast<float*>(s_w + 32 * wp);   // [waves][2][32]
   __shared__ float s_bt[BWD ? 5 * 32 : 1];    // dY rebuild table: scale, shift (+inf: no ReLU), k1, k2, k3
   __shared__ float s_xt[XPRO ? 3 * 32 : 1];   // x prologue: scale, shift, ReLU floor (0 / -inf)
-  __shared__ float s_bn[BNE ? 3 * 32 : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean
+  __shared__ float s_bn[BNE ? 5 * 32 : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean,
+                                              // and (lds_y) 1 / prologue scale, -shift / scale - mean
+  __shared__ int s_ldsy;
   __shared__ int s_ub[kFbMaxKS * 4];          // data-gradient unit -> dY tile offset
   __shared__ int s_wb[kFbMaxT];               // weight-gradient tap -> x tile offset (pixel units)
 
@@ -101,12 +106,26 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     s_ub[e] = ub;
   }
   if (tid < kFbMaxT) s_wb[tid] = tid < T ? (a.dy[tid] * fg.HWD + a.dx[tid]) : 0;
+  // lds_y: the BN epilogue's y1 is this conv's own input (the chain case: x = y1 through the BN1 prologue),
+  // so y1 at the output pixels is rebuilt from the staged x tile instead of a global load in the epilogue
+  // (whose latency, twice per tile, was the critical path of the compute waves: with the MFMA loops knocked
+  // out the kernel still took 87 % of its time).  For t = sc*y1 + sh: ReLU mask = x > 0, y1 - mean =
+  // x / sc - sh / sc - mean (x = bf16(t): the rounding of the stored activation).  Needs sc != 0.
+  if (tid == 0) s_ldsy = (BNE && XPRO && (const void*)a.bn_y == (const void*)a.x) ? 1 : 0;
+  __syncthreads();
   if constexpr (BNE) {
     for (int c = tid; c < 32; c += kFbThreads) {
       const bool on = c < Ci;
       s_bn[c] = on ? a.bn_coef[c] : 0.f;
       s_bn[32 + c] = (on && a.bn_relu) ? a.bn_coef[Ci + c] : INFINITY;
       s_bn[64 + c] = on ? a.bn_coef[2 * Ci + c] : 0.f;
+      if constexpr (XPRO) {
+        const float sc = on ? a.xc[c] : 1.f, sh = on ? a.xc[Ci + c] : 0.f;
+        const float inv = 1.f / sc;
+        s_bn[96 + c] = inv;
+        s_bn[128 + c] = on ? fmaf(-sh, inv, -a.bn_coef[2 * Ci + c]) : 0.f;
+        if (!(sc != 0.f) || !isfinite(inv)) s_ldsy = 0;   // (benign race: every writer stores 0)
+      }
     }
   }
   {   // the data-gradient weights stay resident: no global latency inside the k loop
@@ -163,7 +182,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     // staging: dY = bwd(dz, y2) and x = prologue(y1), zero outside the image -------------------------
     {
       const int totY = hpx * C8y, totX = hpx * C8x, tot = totY + totX;
-      constexpr int LD = BWD ? (BNE ? 8 : 10) : kFbLd;   // two loads per dY vector when rebuilding it
+      constexpr int LD = BWD ? (BNE ? FB_LD_BNE : 10) : kFbLd;   // two loads per dY vector when rebuilding it
       for (int base = st; base < tot; base += 64 * kFbProd * LD) {
         uint4 v[LD], w[LD];
         int dst[LD], cc[LD];
@@ -184,12 +203,14 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
             dst[u] = isy ? hp * fg.py + 8 * c8 : -2 - (hp * fg.px + 8 * c8);   // <= -2: an x-tile slot
             if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
               const long pix = imoff + iy * a.W + ix;
+#ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
               if (isy) {
                 v[u] = fb_ldg4(a.dz + pix * Co + 8 * c8);
                 if (BWD) w[u] = fb_ldg4(a.gy + pix * Co + 8 * c8);
               } else {
                 v[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
               }
+#endif
               cc[u] = 8 * c8;
             }
           }
@@ -258,13 +279,18 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
                                                        : make_uint2(0, 0);
         }
       };
-      if (BNE) load_y(0);
+      const bool lds_y = BNE && XPRO && s_ldsy != 0;   // block-uniform
+      if (BNE && !lds_y) load_y(0);
       f32x4_t acc[MI][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#ifdef FB_KO_DGRAD
+      for (int ks = 0; ks < 0; ++ks) {
+#else
       for (int ks = 0; ks < fg.KS; ++ks) {
+#endif
         uint4 A[MI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) A[i] = *reinterpret_cast<const uint4*>(wrow[i] + 32 * ks);
@@ -280,16 +306,16 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       // epilogue: dz1 (bf16, NHWC) for the in-image pixels and channels < Ci
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        if (BNE && i + 1 < MI) load_y(i + 1);
+        if (BNE && !lds_y && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
         float sc[4], sh[4], mu[4];
         if (BNE) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            sc[r] = s_bn[cb + r];
+            sc[r] = lds_y ? s_bn[96 + cb + r] : s_bn[cb + r];
             sh[r] = s_bn[32 + cb + r];
-            mu[r] = s_bn[64 + cb + r];
+            mu[r] = lds_y ? s_bn[128 + cb + r] : s_bn[64 + cb + r];
           }
         }
 #pragma unroll
@@ -301,13 +327,27 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
           if (BNE) {
             const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                  __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-            const float y4[4] = {__uint_as_float(yy[i][j].x << 16), __uint_as_float(yy[i][j].x & 0xffff0000u),
-                                 __uint_as_float(yy[i][j].y << 16), __uint_as_float(yy[i][j].y & 0xffff0000u)};
+            if (lds_y) {   // y1 from the staged x tile (this output pixel's halo slot)
+              const int p = (wave * NJ + j) * 16 + lr;
+              const int hp = ((p >> fg.tw_shift) - fg.ey0) * fg.HWD + ((p & (fg.TW - 1)) - fg.ex0);
+              const uint2 xv = *reinterpret_cast<const uint2*>(tX + hp * fg.px + cb);
+              const float x4[4] = {__uint_as_float(xv.x << 16), __uint_as_float(xv.x & 0xffff0000u),
+                                   __uint_as_float(xv.y << 16), __uint_as_float(xv.y & 0xffff0000u)};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float gr = fmaf(y4[r], sc[r], sh[r]) > 0.f ? g4[r] : 0.f;
-              cs[i][r] += gr;
-              cq[i][r] += gr * (y4[r] - mu[r]);
+              for (int r = 0; r < 4; ++r) {
+                const float gr = (!a.bn_relu || x4[r] > 0.f) ? g4[r] : 0.f;
+                cs[i][r] += gr;
+                cq[i][r] += gr * fmaf(x4[r], sc[r], mu[r]);
+              }
+            } else {
+              const float y4[4] = {__uint_as_float(yy[i][j].x << 16), __uint_as_float(yy[i][j].x & 0xffff0000u),
+                                   __uint_as_float(yy[i][j].y << 16), __uint_as_float(yy[i][j].y & 0xffff0000u)};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float gr = fmaf(y4[r], sc[r], sh[r]) > 0.f ? g4[r] : 0.f;
+                cs[i][r] += gr;
+                cq[i][r] += gr * (y4[r] - mu[r]);
+              }
             }
           }
         }
@@ -315,8 +355,12 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     }
 
     // ---- weight-gradient: accw[m][i][j] += dY[chunk][co block i]^T x[chunk + tap][ci block j] ----------
+#ifdef FB_KO_WGRAD
+    for (int s = 0; s < 0; ++s) {
+#else
 #pragma unroll 2
     for (int s = 0; s < NCH; ++s) {
+#endif
       const int hlo = halo_pix(32 * s + plo), hhi = halo_pix(32 * s + phi);
       uint4 fa[2];
 #pragma unroll
