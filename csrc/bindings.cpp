@@ -787,6 +787,59 @@ void dwconv_wgrad_t(const at::Tensor& x, const at::Tensor& dyv, const at::Tensor
   TORCH_CHECK(rc == 0, "dwconv_wgrad: no instantiation");
 }
 
+// ---- gconv.hip: grouped convolution (NHWC bf16, fp32 weights [T][C][CG]) -------------------------------
+static void gconv_check(const at::Tensor& x, const at::Tensor& y, int64_t CG, const std::vector<int64_t>& dy,
+                        const std::vector<int64_t>& dx) {
+  CHECK_BF16(x); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3), "gconv: NHWC maps");
+  TORCH_CHECK(x.size(3) % 8 == 0 && x.size(3) % CG == 0, "gconv: C % 8 == 0 and C % CG == 0");
+  TORCH_CHECK(CG == 1 || CG == 2 || CG == 4 || CG == 8 || CG == 16 || CG == 32 || CG == 64, "gconv: CG");
+  TORCH_CHECK(dy.size() == dx.size() && !dy.empty() && (int)dy.size() <= kMaxTaps, "gconv: taps");
+}
+
+void gconv_fwd_t(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t CG, int64_t stride,
+                 std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  gconv_check(x, y, CG, dy, dx);
+  CHECK_F32(w);
+  const int C = x.size(3), T = dy.size();
+  TORCH_CHECK(w.numel() == (int64_t)T * C * CG, "gconv: w [T][C][CG]");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = gconv_fwd(bf(x), f32(w), bf(y), x.size(0), x.size(1), x.size(2), y.size(1), y.size(2), C, CG, stride, T,
+                           ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "gconv_fwd: no instantiation");
+}
+
+void gconv_dgrad_t(const at::Tensor& g, const at::Tensor& w, const at::Tensor& dxo, int64_t CG, int64_t stride,
+                   std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  gconv_check(dxo, g, CG, dy, dx);
+  CHECK_F32(w);
+  const int C = dxo.size(3), T = dy.size();
+  TORCH_CHECK(w.numel() == (int64_t)T * C * CG, "gconv: w [T][C][CG]");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = gconv_dgrad(bf(g), f32(w), bf(dxo), dxo.size(0), dxo.size(1), dxo.size(2), g.size(1), g.size(2), C, CG,
+                             stride, T, ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "gconv_dgrad: no instantiation");
+}
+
+int64_t gconv_wgrad_slices_t(int64_t P, int64_t C, int64_t CG, int64_t T) { return gconv_wgrad_slices(P, C, CG, T); }
+
+void gconv_wgrad_t(const at::Tensor& x, const at::Tensor& g, const at::Tensor& part, int64_t CG, int64_t stride,
+                   std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  gconv_check(x, g, CG, dy, dx);
+  CHECK_F32(part);
+  const int C = x.size(3), T = dy.size();
+  const int64_t nib = CG >= 8 ? CG / 8 : 1;
+  const int64_t row = (int64_t)T * (C / 8) * nib * 64;
+  TORCH_CHECK(part.numel() % row == 0, "gconv_wgrad: part [S][T*C/8*nib][64]");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = gconv_wgrad(bf(x), bf(g), f32(part), (int)(part.numel() / row), x.size(0), x.size(1), x.size(2),
+                             g.size(1), g.size(2), C, CG, stride, T, ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "gconv_wgrad: no instantiation");
+}
+
 void colsum_t(const at::Tensor& part, const at::Tensor& out, bool accum) {
   CHECK_F32(part); CHECK_F32(out);
   const int64_t ncol = out.numel();
@@ -943,6 +996,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_rf_chunks", [](int64_t Cp) { return bn_rf_chunks((int)Cp); });
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_add_act", &bn_add_act_t);
+  m.def("gconv_fwd", &gconv_fwd_t);
+  m.def("gconv_dgrad", &gconv_dgrad_t);
+  m.def("gconv_wgrad_slices", &gconv_wgrad_slices_t);
+  m.def("gconv_wgrad", &gconv_wgrad_t);
   m.def("aug_gray_scratch_doubles", &aug_gray_scratch_doubles);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),

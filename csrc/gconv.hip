@@ -1,0 +1,242 @@
+// Grouped convolution (ResNeXt's grouped 3x3, torchvision ``Bottleneck.conv2`` with groups = 32) on NHWC
+// bf16, fp32 accumulation -- forward, data-gradient and weight-gradient.
+//
+// Reference: models/__init__.py:8-10 (smp encoders incl. resnext50_32x4d; SURVEY §2 "encoders").  Until
+// round 4 this was the one conv of the fused graph that ran on MIOpen's channels-last grouped kernels.
+//
+// A group has CG = C / groups channels in and out (ResNeXt 32x4d: 4, 8, 16, 32 on layers 1-4), so per
+// output channel the reduction is only CG x taps (36..288) long: too short for an MFMA tile, and the
+// block-diagonal weight would waste groups-fold MFMA work as a dense GEMM.  These kernels are direct VALU
+// convolutions instead, memory-shaped like the depthwise kernels (decoder.hip):
+//   fwd / dgrad : a thread owns 8 consecutive channels of one pixel (one 16-B vector out); threads of a
+//                 wave share the channel block and walk 64 consecutive pixels, so the weight reads are
+//                 wave-uniform (broadcast) and the activation reads are one 16-B vector per lane per tap.
+//                 CG <= 8: the 8 channels' groups are exactly the 8 input channels of the same block (one
+//                 vector per tap); CG > 8: CG / 8 vectors of the group per tap.
+//   wgrad       : a thread owns (tap, 8 output channels, 8 input channels of their group) = 64 fp32
+//                 accumulators over a slice of the pixels; lanes are consecutive channel blocks of the
+//                 same pixel (coalesced); per-slice partials [S][combos][64] are summed in slice order by
+//                 colsum (bitwise deterministic).
+// Weights are repacked fp32 [T][C][CG] (w[t][co][cil] = W[co][cil][kh][kw]).
+#include <algorithm>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+constexpr int kBlock = 256;
+
+struct GTaps { int T; int dy[kMaxTaps]; int dx[kMaxTaps]; };
+
+int grid_for(long n) {
+  long b = (n + kBlock - 1) / kBlock;
+  if (b > (1L << 20)) b = 1L << 20;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+// y[n, oy, ox, co] = sum_t sum_cil w[t][co][cil] * x[n, oy*s + dy_t, ox*s + dx_t, group(co)*CG + cil]
+template <int CG>
+__global__ __launch_bounds__(kBlock) void gconv_fwd_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                           uint16_t* __restrict__ y, int N, int IH, int IW, int OH,
+                                                           int OW, int C, int stride, GTaps tp) {
+  const long P = (long)N * OH * OW;
+  const long total = P * (C >> 3);
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int cb = (int)(i / P);      // channel block (wave-uniform for P % 64 == 0)
+    const long p = i - (long)cb * P;
+    const int ox = (int)(p % OW);
+    const long q = p / OW;
+    const int oy = (int)(q % OH);
+    const long n = q / OH;
+    const int co0 = 8 * cb;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const uint16_t* xn = x + n * IH * IW * C;
+    for (int t = 0; t < tp.T; ++t) {
+      const int iy = oy * stride + tp.dy[t], ix = ox * stride + tp.dx[t];
+      if ((unsigned)iy >= (unsigned)IH || (unsigned)ix >= (unsigned)IW) continue;
+      const uint16_t* xp = xn + ((long)iy * IW + ix) * C;
+      const float* wt = w + ((long)t * C + co0) * CG;
+      if constexpr (CG <= 8) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(xp + co0), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int gb = (e / CG) * CG;
+#pragma unroll
+          for (int k = 0; k < CG; ++k) acc[e] = fmaf(wt[e * CG + k], v[gb + k], acc[e]);
+        }
+      } else {
+        const int g0 = (co0 / CG) * CG;
+#pragma unroll
+        for (int vb = 0; vb < CG / 8; ++vb) {
+          float v[8];
+          unpack8(*reinterpret_cast<const uint4*>(xp + g0 + 8 * vb), v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[e] = fmaf(wt[e * CG + 8 * vb + k], v[k], acc[e]);
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(y + p * C + co0) = pack8(acc);
+  }
+}
+
+// dx[n, iy, ix, ci] = sum_t sum_{co in group(ci)} w[t][co][ci - g0] * dy[n, (iy - dy_t)/s, (ix - dx_t)/s, co]
+template <int CG>
+__global__ __launch_bounds__(kBlock) void gconv_dgrad_kernel(const uint16_t* __restrict__ dy, const float* __restrict__ w,
+                                                             uint16_t* __restrict__ dx, int N, int IH, int IW, int OH,
+                                                             int OW, int C, int stride, GTaps tp) {
+  const long P = (long)N * IH * IW;
+  const long total = P * (C >> 3);
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long)gridDim.x * kBlock) {
+    const int cb = (int)(i / P);
+    const long p = i - (long)cb * P;
+    const int ix = (int)(p % IW);
+    const long q = p / IW;
+    const int iy = (int)(q % IH);
+    const long n = q / IH;
+    const int ci0 = 8 * cb;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const uint16_t* dn = dy + n * OH * OW * C;
+    for (int t = 0; t < tp.T; ++t) {
+      const int ry = iy - tp.dy[t], rx = ix - tp.dx[t];
+      if (ry < 0 || rx < 0) continue;
+      const int oy = ry / stride, ox = rx / stride;
+      if (oy * stride != ry || ox * stride != rx || oy >= OH || ox >= OW) continue;
+      const uint16_t* gp = dn + ((long)oy * OW + ox) * C;
+      const float* wt = w + (long)t * C * CG;
+      if constexpr (CG <= 8) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(gp + ci0), v);   // the same 8-channel block of outputs
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int gb = (e / CG) * CG;
+#pragma unroll
+          for (int k = 0; k < CG; ++k) acc[e] = fmaf(wt[(long)(ci0 + gb + k) * CG + (e - gb)], v[gb + k], acc[e]);
+        }
+      } else {
+        const int g0 = (ci0 / CG) * CG, el = ci0 - g0;
+#pragma unroll
+        for (int vb = 0; vb < CG / 8; ++vb) {
+          float v[8];
+          unpack8(*reinterpret_cast<const uint4*>(gp + g0 + 8 * vb), v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float* wr = wt + (long)(g0 + 8 * vb + k) * CG + el;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(wr[e], v[k], acc[e]);
+          }
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + p * C + ci0) = pack8(acc);
+  }
+}
+
+// part[s][combo][64]: combo = (t, co block ob, input block ib of the group) -> acc[e][k] = sum over slice s
+// of dy[p, 8*ob + e] * x[p*s + off_t, g0 + 8*ib + k] (CG < 8: k < CG, the input channels of e's group)
+template <int CG>
+__global__ __launch_bounds__(kBlock) void gconv_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                             float* __restrict__ part, int N, int IH, int IW, int OH,
+                                                             int OW, int C, int stride, GTaps tp, int nslice) {
+  constexpr int NIB = CG >= 8 ? CG / 8 : 1;
+  const int nob = C >> 3;
+  const int ncombo = tp.T * nob * NIB;
+  const int combo = blockIdx.x * kBlock + threadIdx.x;
+  const int s = blockIdx.y;
+  if (combo >= ncombo) return;
+  const int t = combo / (nob * NIB);
+  const int r = combo - t * nob * NIB;
+  const int ib = r / nob, ob = r - ib * nob;   // lanes: consecutive output blocks (coalesced channel reads)
+  const int co0 = 8 * ob;
+  const int g0 = (co0 / CG) * CG;
+  const int xc0 = CG >= 8 ? g0 + 8 * ib : co0;   // CG < 8: the 8-channel block holding e's groups
+  float acc[8][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[e][k] = 0.f;
+  const long P = (long)N * OH * OW;
+  const long per = (P + nslice - 1) / nslice;
+  const long p0 = (long)s * per, p1 = p0 + per < P ? p0 + per : P;
+  for (long p = p0; p < p1; ++p) {
+    const int ox = (int)(p % OW);
+    const long q = p / OW;
+    const int oy = (int)(q % OH);
+    const long n = q / OH;
+    const int iy = oy * stride + tp.dy[t], ix = ox * stride + tp.dx[t];
+    if ((unsigned)iy >= (unsigned)IH || (unsigned)ix >= (unsigned)IW) continue;
+    float g[8], v[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + p * C + co0), g);
+    unpack8(*reinterpret_cast<const uint4*>(x + ((n * IH + iy) * IW + ix) * C + xc0), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[e][k] = fmaf(g[e], v[k], acc[e][k]);
+  }
+  float* o = part + ((long)s * ncombo + combo) * 64;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; k += 4)
+      *reinterpret_cast<float4*>(o + e * 8 + k) = make_float4(acc[e][k], acc[e][k + 1], acc[e][k + 2], acc[e][k + 3]);
+}
+
+GTaps make_taps(int T, const int* dyv, const int* dxv) {
+  GTaps tp{};
+  tp.T = T;
+  for (int t = 0; t < T; ++t) { tp.dy[t] = dyv[t]; tp.dx[t] = dxv[t]; }
+  return tp;
+}
+}  // namespace
+
+int gconv_wgrad_slices(long P, int C, int CG, int T) {
+  const int nib = CG >= 8 ? CG / 8 : 1;
+  const long combos = (long)T * (C / 8) * nib;
+  const long cblocks = (combos + kBlock - 1) / kBlock;
+  long s = (2048 + cblocks - 1) / cblocks;            // ~2048 blocks
+  s = std::min(s, std::max(1L, P / 256));             // >= 256 pixels per slice
+  return (int)std::max(1L, std::min(s, 1024L));
+}
+
+#define GC_DISPATCH_(KERN, ...)                                                                            \
+  switch (CG) {                                                                                           \
+    case 1: hipLaunchKernelGGL(KERN<1>, __VA_ARGS__); return 0;                                           \
+    case 2: hipLaunchKernelGGL(KERN<2>, __VA_ARGS__); return 0;                                           \
+    case 4: hipLaunchKernelGGL(KERN<4>, __VA_ARGS__); return 0;                                           \
+    case 8: hipLaunchKernelGGL(KERN<8>, __VA_ARGS__); return 0;                                           \
+    case 16: hipLaunchKernelGGL(KERN<16>, __VA_ARGS__); return 0;                                         \
+    case 32: hipLaunchKernelGGL(KERN<32>, __VA_ARGS__); return 0;                                         \
+    case 64: hipLaunchKernelGGL(KERN<64>, __VA_ARGS__); return 0;                                         \
+  }                                                                                                       \
+  return 1;
+
+int gconv_fwd(const uint16_t* x, const float* w, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C, int CG,
+              int stride, int T, const int* dyv, const int* dxv, hipStream_t s) {
+  const GTaps tp = make_taps(T, dyv, dxv);
+  const dim3 grid(grid_for((long)N * OH * OW * (C / 8)));
+  GC_DISPATCH_(gconv_fwd_kernel, grid, dim3(kBlock), 0, s, x, w, y, N, IH, IW, OH, OW, C, stride, tp)
+}
+
+int gconv_dgrad(const uint16_t* dy, const float* w, uint16_t* dx, int N, int IH, int IW, int OH, int OW, int C, int CG,
+                int stride, int T, const int* dyv, const int* dxv, hipStream_t s) {
+  const GTaps tp = make_taps(T, dyv, dxv);
+  const dim3 grid(grid_for((long)N * IH * IW * (C / 8)));
+  GC_DISPATCH_(gconv_dgrad_kernel, grid, dim3(kBlock), 0, s, dy, w, dx, N, IH, IW, OH, OW, C, stride, tp)
+}
+
+int gconv_wgrad(const uint16_t* x, const uint16_t* dy, float* part, int nslice, int N, int IH, int IW, int OH, int OW,
+                int C, int CG, int stride, int T, const int* dyv, const int* dxv, hipStream_t s) {
+  const GTaps tp = make_taps(T, dyv, dxv);
+  const int nib = CG >= 8 ? CG / 8 : 1;
+  const int combos = T * (C / 8) * nib;
+  const dim3 grid((unsigned)((combos + kBlock - 1) / kBlock), (unsigned)nslice);
+  GC_DISPATCH_(gconv_wgrad_kernel, grid, dim3(kBlock), 0, s, x, dy, part, N, IH, IW, OH, OW, C, stride, tp, nslice)
+}
+#undef GC_DISPATCH_

@@ -315,3 +315,13 @@ struct FusedBwdGeom {
 bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg);
 int conv_bwd_fused_blocks(const ConvGeom& g);   // 0: not eligible
 int conv_bwd_fused(const FusedBwdArgs& a, const ConvGeom& g, hipStream_t s);
+
+// gconv.hip: grouped convolution (ResNeXt grouped 3x3), NHWC bf16, fp32 weights repacked [T][C][CG]
+int gconv_fwd(const uint16_t* x, const float* w, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C, int CG,
+              int stride, int T, const int* dyv, const int* dxv, hipStream_t s);
+int gconv_dgrad(const uint16_t* dy, const float* w, uint16_t* dx, int N, int IH, int IW, int OH, int OW, int C, int CG,
+                int stride, int T, const int* dyv, const int* dxv, hipStream_t s);
+int gconv_wgrad_slices(long P, int C, int CG, int T);
+// part [nslice][T * C/8 * max(1, CG/8)][64] fp32 (summed over slices by colsum)
+int gconv_wgrad(const uint16_t* x, const uint16_t* dy, float* part, int nslice, int N, int IH, int IW, int OH, int OW,
+                int C, int CG, int stride, int T, const int* dyv, const int* dxv, hipStream_t s);

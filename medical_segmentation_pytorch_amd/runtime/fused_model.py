@@ -23,11 +23,11 @@ import os
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
 from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
+from ..ops.gconv import gconv
 from ..ops.pool import maxpool, res_tail, up2_cat
 from .fused_decoders import SmpDecoders, fused_decoder_kind
 
@@ -461,17 +461,13 @@ class FusedExecutor(SmpDecoders):
                             single)
 
     def grouped_conv_bn(self, conv_mod, bn_mod, x, training, relu):
-        """Grouped 3x3 conv (ResNeXt ``conv2``, ``groups=32``) inside the fused graph: the NHWC bf16
-        feature map IS a channels-last NCHW tensor (widths are multiples of 8), so the conv runs on
-        MIOpen's channels-last grouped kernels with no layout copy, between fused ops on both sides
-        (the 1x1 convs around it -- most of a ResNeXt block's FLOPs -- stay on the HIP kernels).  Its BN
-        takes the statistics pass (no conv epilogue) and never parks its backward exchange: the
-        data-gradient goes to an autograd op, not to one of ours."""
+        """Grouped 3x3 conv (ResNeXt ``conv2``, ``groups=32``) on the HIP grouped-conv kernels
+        (``ops.gconv``, csrc/gconv.hip: direct VALU convolutions -- a group's reduction is only 36-288 long);
+        until round 4 it ran on MIOpen's channels-last kernels.  Its BN takes the statistics pass (no conv
+        epilogue) and never parks its backward exchange: the data-gradient goes to this op's own backward."""
         z = materialize(x)
         assert z.shape[-1] == conv_mod.in_channels, 'grouped conv input must be unpadded (C % 8 == 0)'
-        y = F.conv2d(z.permute(0, 3, 1, 2), conv_mod.weight.to(torch.bfloat16), None, conv_mod.stride,
-                     conv_mod.padding, conv_mod.dilation, conv_mod.groups)
-        y = y.permute(0, 2, 3, 1).contiguous()   # a view when MIOpen returns channels-last
+        y = gconv(z, conv_mod)
         return bn_act([y], self.bn(bn_mod), relu, training, deferred=_DEFER_BN)
 
     def resnet_block(self, blk, x, training):

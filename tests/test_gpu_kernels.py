@@ -770,3 +770,27 @@ def test_parked_gradient_aliasing_its_own_dy_is_not_overwritten(gpu):
     assert _rel(res[1][0], res[0][0]) < 4e-3
     assert torch.equal(res[1][1], res[0][1])
 
+
+
+@pytest.mark.parametrize('c,groups,stride', [(128, 32, 1), (64, 32, 2), (256, 32, 1), (512, 32, 2), (1024, 32, 1),
+                                             (64, 8, 1), (48, 48, 1)])
+def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
+    """HIP grouped 3x3 (csrc/gconv.hip; ResNeXt conv2, CG = 4..32 channels per group, stride 1 / 2) vs the
+    fp32 PyTorch conv on the same bf16 inputs: output, input gradient and weight gradient."""
+    from medical_segmentation_pytorch_amd.ops.gconv import gconv
+    torch.manual_seed(8)
+    n, h, w = 2, 14, 18
+    m = nn.Conv2d(c, c, 3, stride, 1, groups=groups, bias=False).to(gpu)
+    x = torch.randn(n, h, w, c, device=gpu).to(torch.bfloat16)
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, stride, 1, 1, groups)
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    ref.backward(g.float())
+    xf = x.clone().requires_grad_(True)
+    y = gconv(xf, m)
+    y.backward(g.permute(0, 2, 3, 1).contiguous())
+    assert y.shape == (n, ref.shape[2], ref.shape[3], c)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+    assert _rel(xf.grad.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert _rel(m.weight.grad, wr.grad) < 1e-3
