@@ -19,8 +19,6 @@ What is fused relative to the module graph (reference ``models/ducknet.py``, ``m
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
@@ -467,7 +465,7 @@ class FusedExecutor(SmpDecoders):
         epilogue) and never parks its backward exchange: the data-gradient goes to this op's own backward."""
         z = materialize(x)
         assert z.shape[-1] == conv_mod.in_channels, 'grouped conv input must be unpadded (C % 8 == 0)'
-        y = gconv(z, conv_mod)
+        y = gconv(z, conv_mod)   # (smp-Unet ResNeXt50 bs64: 1196 img/s vs 361 on MIOpen, profiles/r04/)
         return bn_act([y], self.bn(bn_mod), relu, training, deferred=_DEFER_BN)
 
     def resnet_block(self, blk, x, training):
