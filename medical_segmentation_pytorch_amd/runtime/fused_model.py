@@ -19,6 +19,8 @@ What is fused relative to the module graph (reference ``models/ducknet.py``, ``m
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
