@@ -899,7 +899,9 @@ void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy,
                       const at::Tensor& dxo, const c10::optional<at::Tensor>& bn_y,
                       const c10::optional<at::Tensor>& bn_coef, bool bn_relu,
                       const c10::optional<at::Tensor>& stat_part, const at::Tensor& dw, std::vector<int64_t> dims,
-                      std::vector<int64_t> dy, std::vector<int64_t> dx) {
+                      std::vector<int64_t> dy, std::vector<int64_t> dx, const c10::optional<at::Tensor>& dz2,
+                      const c10::optional<at::Tensor>& gy2, const c10::optional<at::Tensor>& gs2,
+                      const c10::optional<at::Tensor>& gk2, bool grelu2, int64_t t1) {
   ConvGeom g = make_geom(dims, dy, dx);
   const int64_t nblk = conv_bwd_fused_blocks(g);
   TORCH_CHECK(nblk > 0, "conv_bwd_fused: shape not eligible");
@@ -908,10 +910,24 @@ void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy,
   CHECK_BF16(x); TORCH_CHECK(x.numel() == nx, "x numel");
   CHECK_BF16(dxo); TORCH_CHECK(dxo.numel() == nx, "dx numel");
   CHECK_BF16(wd);
-  TORCH_CHECK(Kp_d % 32 == 0 && Kp_d >= g.T * g.Cgo && wd.numel() >= 32 * Kp_d, "packed dgrad weights");
-  CHECK_F32(dw); TORCH_CHECK(dw.numel() == nblk * g.Cgo * g.T * g.Cgi, "dw slabs numel");
+  TORCH_CHECK(Kp_d % 32 == 0 && Kp_d >= g.T * g.Go * g.Cgo && wd.numel() >= 32 * Kp_d, "packed dgrad weights");
+  CHECK_F32(dw); TORCH_CHECK(dw.numel() == nblk * g.Go * g.Cgo * g.T * g.Cgi, "dw slabs numel");
   FusedBwdArgs a{};
   a.dz = bf(dz);
+  a.t1 = (int)t1;
+  if (g.Go == 2) {
+    TORCH_CHECK(dz2.has_value() && dz2->defined(), "conv_bwd_fused: Go == 2 needs dz2");
+    CHECK_BF16(*dz2); TORCH_CHECK(dz2->numel() == ny, "dz2 numel");
+    a.dz2 = bf(*dz2);
+    if (gy2.has_value() && gy2->defined()) {
+      CHECK_BF16(*gy2); TORCH_CHECK(gy2->numel() == ny, "gy2 numel");
+      TORCH_CHECK(gs2.has_value() && gk2.has_value(), "gy2 needs gs2 and gk2");
+      CHECK_F32(*gs2); CHECK_F32(*gk2);
+      TORCH_CHECK(gs2->numel() >= 2 * g.Cgo && gk2->numel() >= 3 * g.Cgo, "gs2 [4][C], gk2 [3][C]");
+      a.gy2 = bf(*gy2); a.gs2 = gs2->data_ptr<float>(); a.gk2 = gk2->data_ptr<float>();
+    }
+    a.grelu2 = grelu2 ? 1 : 0;
+  }
   if (gy.has_value() && gy->defined()) {
     CHECK_BF16(*gy); TORCH_CHECK(gy->numel() == ny, "gy numel");
     TORCH_CHECK(gs.has_value() && gk.has_value(), "gy needs gs and gk");
@@ -1060,7 +1076,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_wgrad", &dwconv_wgrad_t);
   m.def("colsum", &colsum_t);
   m.def("conv_bwd_fused_blocks", &conv_bwd_fused_blocks_t);
-  m.def("conv_bwd_fused", &conv_bwd_fused_t);
+  m.def("conv_bwd_fused", &conv_bwd_fused_t, py::arg("dz"), py::arg("gy"), py::arg("gs"), py::arg("gk"),
+        py::arg("grelu"), py::arg("x"), py::arg("xc"), py::arg("xrelu"), py::arg("wd"), py::arg("Kp_d"), py::arg("dxo"),
+        py::arg("bn_y"), py::arg("bn_coef"), py::arg("bn_relu"), py::arg("stat_part"), py::arg("dw"), py::arg("dims"),
+        py::arg("dy"), py::arg("dx"), py::arg("dz2") = py::none(), py::arg("gy2") = py::none(),
+        py::arg("gs2") = py::none(), py::arg("gk2") = py::none(), py::arg("grelu2") = false, py::arg("t1") = -1);
   m.def("comm_buffer_bytes", &comm_buffer_bytes);
   m.def("comm_alloc", &comm_alloc_t);
   m.def("comm_open", &comm_open_t);

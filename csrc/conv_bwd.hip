@@ -53,7 +53,7 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <int NJ, bool BWD, bool XPRO, bool BNE>
+template <int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false>
 __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
   extern __shared__ uint4 fb_smem[];
   constexpr int MI = 2;                       // 32 data-gradient rows (input channels <= 32)
@@ -66,7 +66,8 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
   const int wp = 32 * fg.KS + 8;                           // weight row pitch (elements; +16 B: bank spread)
   uint16_t* const s_w = lds0 + 2 * pair;                   // [32 rows][wp] data-gradient weights, per block
   float* s_stat = reinterpret_cast<float*>(s_w + 32 * wp);   // [waves][2][32]
-  __shared__ float s_bt[BWD ? 5 * 32 : 1];    // dY rebuild table: scale, shift (+inf: no ReLU), k1, k2, k3
+  __shared__ float s_bt[BWD ? 5 * 64 : 1];    // dY rebuild table (stacked groups): scale, shift (+inf: no
+                                              // ReLU), k1, k2, k3
   __shared__ float s_xt[XPRO ? 3 * 32 : 1];   // x prologue: scale, shift, ReLU floor (0 / -inf)
   __shared__ float s_bn[BNE ? 5 * 32 : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean,
                                               // and (lds_y) 1 / prologue scale, -shift / scale - mean
@@ -77,15 +78,21 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int Ci = a.Ci, Co = a.Co, T = a.T;
-  const int C8y = Co >> 3, C8x = Ci >> 3;
+  constexpr int Go = GO2 ? 2 : 1;
+  const int C8g = Co >> 3, C8y = Go * C8g, C8x = Ci >> 3;   // dY: Go groups of Co channels, stacked
+  const int nU0 = T * C8g, nU = nU0 + (Go == 2 ? C8g : 0);   // data-gradient K units (tap, 8 channels)
+  const int nWU = T + (Go == 2 ? 1 : 0);                     // weight-gradient (group, tap) units
   if constexpr (BWD) {
-    for (int c = tid; c < 32; c += kFbThreads) {
-      const bool on = c < Co;
-      s_bt[c] = on ? a.gs[c] : 0.f;
-      s_bt[32 + c] = (on && a.grelu) ? a.gs[Co + c] : INFINITY;
-      s_bt[64 + c] = on ? a.gk[c] : 0.f;
-      s_bt[96 + c] = on ? a.gk[Co + c] : 0.f;
-      s_bt[128 + c] = on ? a.gk[2 * Co + c] : 0.f;
+    for (int c = tid; c < 64; c += kFbThreads) {
+      const int g = c >= Co ? 1 : 0, cl = c - g * Co;
+      const float* gs = g ? a.gs2 : a.gs;
+      const float* gk = g ? a.gk2 : a.gk;
+      const bool on = c < Go * Co && (g ? a.gy2 : a.gy) != nullptr;
+      s_bt[c] = on ? gs[cl] : 0.f;
+      s_bt[64 + c] = (on && (g ? a.grelu2 : a.grelu)) ? gs[Co + cl] : INFINITY;
+      s_bt[128 + c] = on ? gk[cl] : 0.f;
+      s_bt[192 + c] = on ? gk[Co + cl] : 0.f;
+      s_bt[256 + c] = on ? gk[2 * Co + cl] : 0.f;
     }
   }
   if constexpr (XPRO) {
@@ -96,10 +103,16 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       s_xt[64 + c] = a.xrelu ? 0.f : -INFINITY;
     }
   }
+  // unit e -> (tap t, stacked 8-channel slot c8): group 0 over every tap, then group 1 at its one tap t1
+  auto unit = [&](int e, int& t, int& c8) {
+    if (e < nU0) { t = e / C8g; c8 = e - t * C8g; }
+    else { t = a.t1; c8 = C8g + (e - nU0); }
+  };
   for (int e = tid; e < fg.KS * 4; e += kFbThreads) {
     int ub = 0;
-    if (e < T * C8y) {
-      const int t = e / C8y, c8 = e - t * C8y;
+    if (e < nU) {
+      int t, c8;
+      unit(e, t, c8);
       // data-gradient taps = the negated forward taps
       ub = ((-a.dy[t] - fg.ey0) * fg.HWD + (-a.dx[t] - fg.ex0)) * fg.py + 8 * c8;
     }
@@ -128,11 +141,17 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       }
     }
   }
-  {   // the data-gradient weights stay resident: no global latency inside the k loop
+  {   // the data-gradient weights stay resident, in unit order: no global latency inside the k loop
     const int rowv = 4 * fg.KS;   // uint4 per row
     for (int e = tid; e < 32 * rowv; e += kFbThreads) {
-      const int r = e / rowv, k = e - r * rowv;
-      *reinterpret_cast<uint4*>(s_w + r * wp + 8 * k) = *reinterpret_cast<const uint4*>(a.wd + (long)r * a.Kp + 8 * k);
+      const int r = e / rowv, u = e - r * rowv;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (u < nU) {
+        int t, c8;
+        unit(u, t, c8);   // packed dgrad weights: k = t * (Go*Co) + stacked channel
+        v = *reinterpret_cast<const uint4*>(a.wd + (long)r * a.Kp + t * (Go * Co) + 8 * c8);
+      }
+      *reinterpret_cast<uint4*>(s_w + r * wp + 8 * u) = v;
     }
   }
   if (BNE)
@@ -203,15 +222,21 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
             dst[u] = isy ? hp * fg.py + 8 * c8 : -2 - (hp * fg.px + 8 * c8);   // <= -2: an x-tile slot
             if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
               const long pix = imoff + iy * a.W + ix;
+              cc[u] = 8 * c8;
 #ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
               if (isy) {
-                v[u] = fb_ldg4(a.dz + pix * Co + 8 * c8);
-                if (BWD) w[u] = fb_ldg4(a.gy + pix * Co + 8 * c8);
+                const bool g2 = GO2 && c8 >= C8g;   // (a select of two kernarg pointers, not an indexed load)
+                const int cl = 8 * (c8 - (g2 ? C8g : 0));
+                v[u] = fb_ldg4((g2 ? a.dz2 : a.dz) + pix * Co + cl);
+                if (BWD) {
+                  const uint16_t* yp = g2 ? a.gy2 : a.gy;
+                  if (!GO2 || yp != nullptr) w[u] = fb_ldg4(yp + pix * Co + cl);
+                  else cc[u] = -1;   // a plain gradient group: stored as loaded
+                }
               } else {
                 v[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
               }
 #endif
-              cc[u] = 8 * c8;
             }
           }
         }
@@ -220,7 +245,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
           if (dst[u] == -1) continue;
           uint4 val = v[u];
           if (dst[u] >= 0) {
-            if (BWD && cc[u] >= 0) val = bwd8(val, w[u], s_bt + cc[u], 32);
+            if (BWD && cc[u] >= 0) val = bwd8(val, w[u], s_bt + cc[u], 64);
             *reinterpret_cast<uint4*>(tY + dst[u]) = val;
           } else {
             if (XPRO && cc[u] >= 0) {
@@ -371,8 +396,18 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       }
 #pragma unroll
       for (int m = 0; m < NT; ++m) {
-        const int t = wave + kFbWaves * m;
-        if (t >= T) break;   // wave-uniform
+        const int u = wave + kFbWaves * m;   // (group, tap) unit: group 0's taps, then group 1's tap t1
+        if (u >= nWU) break;   // wave-uniform
+        const bool g2 = GO2 && u >= T;
+        const int t = g2 ? a.t1 : u;
+        if (g2) {   // the second group's dY columns; its unit is the wave's last, so fa is overwritten
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const uint2 lo = fb_tr_read(tY + hlo * fg.py + Co + 16 * i + 4 * p4);
+            const uint2 hi = fb_tr_read(tY + hhi * fg.py + Co + 16 * i + 4 * p4);
+            fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          }
+        }
         const int sw = s_wb[t];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -410,13 +445,14 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       a.stat_part[((long)blockIdx.x * 2 + 1) * Ci + c] = q2;
     }
   }
-  // ---- dW slab of this block: [Co][T * Ci], element (co, t*Ci + ci) -------------------------------------
+  // ---- dW slab of this block: [Go*Co][T * Ci], element (g*Co + co, t*Ci + ci) ----------------------------
   if (producer) return;
-  float* slab = a.dw + (long)blockIdx.x * Co * (T * Ci);
+  float* slab = a.dw + (long)blockIdx.x * (Go * Co) * (T * Ci);
 #pragma unroll
   for (int m = 0; m < NT; ++m) {
-    const int t = wave + kFbWaves * m;
-    if (t >= T) break;
+    const int u = wave + kFbWaves * m;
+    if (u >= nWU) break;
+    const int g = (GO2 && u >= T) ? 1 : 0, t = g ? a.t1 : u;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -426,7 +462,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = 16 * i + 4 * lg + r;
-          if (co < Co) slab[(long)co * (T * Ci) + t * Ci + ci] = accw[m][i][j][r];
+          if (co < Co) slab[(long)(g * Co + co) * (T * Ci) + t * Ci + ci] = accw[m][i][j][r];
         }
       }
   }
@@ -445,7 +481,8 @@ size_t fb_lds(const FusedBwdGeom& fg) {
 // Plan: eligible shapes and the tile geometry (0 = not eligible).  Symmetric tap sets only (3x3 with any
 // dilation, 1x7 / 7x1): the dY halo of the data-gradient and the x halo of the weight-gradient coincide.
 bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
-  if (g.stride != 1 || g.Gi != 1 || g.Go != 1 || g.OH != g.IH || g.OW != g.IW) return false;
+  // Go == 2: the ResidualBlock's 3x3 + 1x1 pair (the 1x1 at one tap of the 3x3's grid, FusedBwdArgs::t1)
+  if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > 2 || g.OH != g.IH || g.OW != g.IW) return false;
   if (g.Cgi > 32 || g.Cgo > 32 || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2) return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
   for (int t = 0; t < g.T; ++t) {
@@ -455,9 +492,9 @@ bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
     ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
-  const int C8y = g.Cgo / 8, C8x = g.Cgi / 8;
+  const int C8g = g.Cgo / 8, C8y = g.Go * C8g, C8x = g.Cgi / 8;
   const int py = 8 * ((C8y & 1) ? C8y : C8y + 1), px = 8 * ((C8x & 1) ? C8x : C8x + 1);
-  const int KS = (g.T * C8y + 3) / 4;
+  const int KS = (g.T * C8g + (g.Go == 2 ? C8g : 0) + 3) / 4;
   if (KS > kFbMaxKS) return false;
   double best = 1e30;
   bool found = false;
@@ -500,23 +537,28 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   if (!conv_bwd_fused_plan(g, fg)) return 8;
   FusedBwdArgs a = a0;
   a.N = g.N; a.H = g.IH; a.W = g.IW; a.Ci = g.Cgi; a.Co = g.Cgo; a.T = g.T;   // a.Kp: the dgrad packing's Kp
+  a.Go = g.Go;
+  if (g.Go == 2 && (a.dz2 == nullptr || a.t1 < 0 || a.t1 >= g.T)) return 8;
+  if ((a.gy != nullptr) != (a.gs != nullptr) || (a.gy2 != nullptr) != (a.gs2 != nullptr)) return 8;
   for (int t = 0; t < g.T; ++t) { a.dy[t] = g.dy[t]; a.dx[t] = g.dx[t]; }
   const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
   const size_t lds = fb_lds(fg);
-  const bool bwd = a.gy != nullptr, xpro = a.xc != nullptr, bne = a.bn_y != nullptr;
-#define FB_(NJ_, B_, X_, E_)                                                                                \
-  if (fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_) {                                                \
+  const bool bwd = a.gy != nullptr || a.gy2 != nullptr, xpro = a.xc != nullptr, bne = a.bn_y != nullptr;
+#define FB_(NJ_, B_, X_, E_, G_)                                                                            \
+  if (fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_ && (g.Go == 2) == G_) {                           \
     static bool lds_attr = false;                                                                            \
     if (!lds_attr) {                                                                                         \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<NJ_, B_, X_, E_>),      \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<NJ_, B_, X_, E_, G_>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                      \
       lds_attr = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_>), dim3(grid), dim3(kFbThreads), lds, s, a, fg); \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_, G_>), dim3(grid), dim3(kFbThreads), lds, s, a, fg); \
     return 0;                                                                                                \
   }
-#define FB4_(NJ_, B_) FB_(NJ_, B_, false, false) FB_(NJ_, B_, true, false) FB_(NJ_, B_, false, true) FB_(NJ_, B_, true, true)
-  FB4_(8, false) FB4_(8, true) FB4_(4, false) FB4_(4, true)
+#define FB4_(NJ_, B_, G_) FB_(NJ_, B_, false, false, G_) FB_(NJ_, B_, true, false, G_) FB_(NJ_, B_, false, true, G_) \
+                          FB_(NJ_, B_, true, true, G_)
+  FB4_(8, false, false) FB4_(8, true, false) FB4_(4, false, false) FB4_(4, true, false)
+  FB4_(8, false, true) FB4_(8, true, true) FB4_(4, false, true) FB4_(4, true, true)
 #undef FB4_
 #undef FB_
   return 8;

@@ -293,6 +293,14 @@ struct FusedBwdArgs {
   const float* gs;
   const float* gk;
   int grelu;
+  // Go == 2: a second output group (the ResidualBlock's 1x1 shortcut riding in the 3x3's launch) with its
+  // own dY (rebuilt from its own deferred BN gradient when gy2 != nullptr) at the single forward tap t1
+  int Go, t1;
+  const uint16_t* dz2;
+  const uint16_t* gy2;
+  const float* gs2;
+  const float* gk2;
+  int grelu2;
   const uint16_t* x;
   const float* xc;
   int xrelu;

@@ -217,10 +217,16 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
     dY (rebuilt from a deferred BN data-gradient when one arrives) and x (through the forward's deferred-BN
     prologue) are staged once per tile; the BN epilogue of the data-gradient (BwdStatsHandle) runs in it too.
     Returns (dxs, wgrads) or None when the shape is not eligible."""
-    if not (FUSED_BWD and need_dx and not plan.transposed and plan.stride == 1 and plan.Gi == 1 and plan.Go == 1
+    if not (FUSED_BWD and need_dx and not plan.transposed and plan.stride == 1 and plan.Gi == 1 and plan.Go <= 2
             and plan.bias is None and plan.Cgi <= 32 and plan.Cgo <= 32 and 2 <= plan.T <= 9
             and all(b.weight.requires_grad for b in plan.branches)):
         return None
+    t1 = -1
+    if plan.Go == 2:   # the ResidualBlock pair: group 0 over the full tap grid, group 1 (the 1x1) at one tap
+        b0, b1 = sorted(plan.branches, key=lambda b: b.out_group)
+        if len(plan.branches) != 2 or b0.t_base != 0 or b0.T != plan.T or b1.T != 1:
+            return None
+        t1 = b1.t_base
     C = require()
     n, ih, iw, oh, ow = shape
     dims = plan.fwd_dims(n, ih, iw, oh, ow)
@@ -230,6 +236,7 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
         return None
     from .bn import claim_deferred, peek_deferred
     d = peek_deferred(gys[0])
+    d2 = peek_deferred(gys[1]) if plan.Go == 2 else None
     coefs, rmask = ctx.pro
     xc = coefs[0] if coefs else None
     wd, Kp_d = plan.pack_dgrad(dev)
@@ -243,11 +250,16 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
                      d.coef if d is not None else None, bool(d.relu) if d is not None else False,
                      xs[0], xc, bool(rmask & 1), wd, Kp_d, dxt,
                      h.y if bne else None, h.stats if bne else None, bool(h.relu) if bne else False, part,
-                     dwp, dims, tdy, tdx)
+                     dwp, dims, tdy, tdx,
+                     dz2=(d2.dz if d2 is not None else gys[1]) if plan.Go == 2 else None,
+                     gy2=d2.y if d2 is not None else None, gs2=d2.stats if d2 is not None else None,
+                     gk2=d2.coef if d2 is not None else None, grelu2=bool(d2.relu) if d2 is not None else False,
+                     t1=t1)
     if bne:
         h.part = part
-    if d is not None:
-        claim_deferred(d)
+    for dd in (d, d2):
+        if dd is not None:
+            claim_deferred(dd)
     need = [b.weight.requires_grad for b in plan.branches]
     return [dxt], _unpack_slabs(plan, dwp, nblk, need)
 

@@ -37,6 +37,8 @@ CASES = [
     (64, 64, (3, 3), 1, 1, 0, (2, 16, 16), False),     # >= 64 channels: GEMM kernels -> resolved
     (17, 17, (3, 3), 1, 1, 0, (12, 128, 128), True),   # 384 tiles > the 256-block persistent grid: blocks
                                                        # loop over tiles (the double-buffered staging)
+    (17, 17, (3, 3), 1, 1, 1, (12, 128, 128), True),   # the Go = 2 fused backward (3x3 + centre 1x1), multi-tile
+    (17, 17, (3, 3), 2, 1, 1, (2, 40, 56), True),      # Go = 2, dilation 2
 ]
 
 
@@ -136,6 +138,35 @@ def test_deferred_tokens_reach_the_halo_prologue(gpu, monkeypatch):
     z.backward(torch.randn_like(z))
     assert not any(calls), 'the single 17-channel 3x3 conv must consume the deferred gradient in its kernels'
     assert x.grad is not None and torch.isfinite(x.grad.float()).all()
+
+
+def test_fused_backward_runs_for_the_residual_pair(gpu, monkeypatch):
+    """The ResidualBlock's 3x3 + 1x1 pair (Go = 2, the 1x1 at the centre tap) takes the fused backward and
+    consumes both deferred BN gradients."""
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
+    monkeypatch.setattr(bnmod, 'DEFER_DY', True)
+    monkeypatch.setattr(convmod, 'FUSED_BWD', True)
+    calls = []
+    orig = convmod._fused_bwd
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r is not None)
+        return r
+    monkeypatch.setattr(convmod, '_fused_bwd', spy)
+    torch.manual_seed(3)
+    m3 = nn.Conv2d(17, 17, 3, 1, 1, bias=False).to(gpu)
+    m1 = nn.Conv2d(17, 17, 1, bias=False).to(gpu)
+    bns = [nn.BatchNorm2d(17).to(gpu) for _ in range(2)]
+    plan = ConvPlan(3, 3, 17, 17, [Branch(m3.weight, 0, 0, 9), Branch(m1.weight, 1, 4, 1)], padding=(1, 1), Go=2)
+    x = to_fm_reference(_bf(torch.randn(2, 17, 40, 48, device=gpu))).requires_grad_(True)
+    ys, _ = conv(plan, [x])
+    zs = [materialize(bn_act([y], BNState.from_module(b), True, True, None, deferred=True, defer_bwd=True))
+          for y, b in zip(ys, bns)]
+    torch.autograd.backward(zs, [torch.randn_like(z) for z in zs])
+    torch.cuda.synchronize()
+    assert calls == [True], calls
+    assert not bnmod._DEFERRED
 
 
 def test_fused_backward_runs_for_narrow_convs(gpu, monkeypatch):
