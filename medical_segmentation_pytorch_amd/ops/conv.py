@@ -277,7 +277,11 @@ def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     if not any(d is not None for d in ds):
         return list(grads), None
     C = require()
-    ok = DEFER_SEPARATE and not plan.transposed and plan.stride == 1 and plan.bias is None
+    # Without a data-gradient launch (the first conv: its input is the image) the weight-gradient is dY's
+    # only reader: rebuilding dY there reads (dz, y) once instead of the apply pass's read dz, y + write dy
+    # + the weight-gradient's read dy -- 2 passes instead of 4, a win even where the halo kernels' re-read
+    # of y made deferral neutral (DEFER_SEPARATE).
+    ok = (DEFER_SEPARATE or not dgrad) and not plan.transposed and plan.stride == 1 and plan.bias is None
     if ok and dgrad:
         ok = bool(C.conv_uses_halo(dims_d, taps_d[0], taps_d[1], False, True))
     if ok:

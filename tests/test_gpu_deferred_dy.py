@@ -194,3 +194,43 @@ def test_fused_backward_runs_for_narrow_convs(gpu, monkeypatch):
     torch.cuda.synchronize()
     assert calls == [True], calls
     assert not bnmod._DEFERRED
+
+
+@pytest.mark.parametrize('go', [1, 8])
+def test_deferred_dy_without_data_gradient(gpu, go, monkeypatch):
+    """The first conv (input = the image, no data-gradient): the deferred BN gradients go straight into
+    the halo weight-gradient's staging (no apply pass) and the weight gradients match the materialised path."""
+    from medical_segmentation_pytorch_amd.ops import conv as convmod
+    calls = []
+    orig = bnmod.resolve
+
+    def spy(g):
+        calls.append(bnmod.peek_deferred(g) is not None)
+        return orig(g)
+    torch.manual_seed(4)
+    convs = [nn.Conv2d(3, 17, 3, 1, 1, bias=False).to(gpu) for _ in range(go)]
+    bns = [nn.BatchNorm2d(17).to(gpu) for _ in range(go)]
+    plan = ConvPlan(3, 3, 3, 17, [Branch(m.weight, g, 0, 9) for g, m in enumerate(convs)], padding=(1, 1), Go=go)
+    x = to_fm_reference(_bf(torch.randn(2, 3, 40, 56, device=gpu)))
+    gs = [to_fm_reference(_bf(torch.randn(2, 17, 40, 56, device=gpu, generator=torch.Generator(gpu).manual_seed(9 + g))))
+          for g in range(go)]
+    res = []
+    for defer in (False, True):
+        monkeypatch.setattr(bnmod, 'DEFER_DY', defer)
+        monkeypatch.setattr(bnmod, 'resolve', spy if defer else orig)
+        for m in convs:
+            m.weight.grad = None
+        state = [{k: v.clone() for k, v in b.state_dict().items()} for b in bns]
+        ys, _ = conv(plan, [x])
+        zs = [materialize(bn_act([y], BNState.from_module(b), True, True, None, deferred=True, defer_bwd=True))
+              for y, b in zip(ys, bns)]
+        torch.autograd.backward(zs, gs)
+        torch.cuda.synchronize()
+        res.append([m.weight.grad.clone() for m in convs])
+        for b, sd in zip(bns, state):
+            b.load_state_dict(sd)
+        bnmod.clear_deferred()
+    for a, b in zip(res[1], res[0]):
+        assert _rel(a, b) < 1e-3
+    assert not any(calls), 'no apply pass: the weight-gradient staging rebuilds dY'
+    assert convmod is not None
