@@ -787,6 +787,18 @@ void dwconv_wgrad_t(const at::Tensor& x, const at::Tensor& dyv, const at::Tensor
   TORCH_CHECK(rc == 0, "dwconv_wgrad: no instantiation");
 }
 
+void relu6_t(const at::Tensor& x, const at::Tensor& y) {
+  CHECK_BF16(x); CHECK_BF16(y);
+  TORCH_CHECK(x.numel() == y.numel() && x.numel() % 8 == 0, "relu6: same numel, multiple of 8");
+  relu6(bf(x), bf(y), x.numel(), cur_stream());
+}
+
+void relu6_bwd_t(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx) {
+  CHECK_BF16(dy); CHECK_BF16(y); CHECK_BF16(dx);
+  TORCH_CHECK(dy.numel() == y.numel() && dx.numel() == y.numel() && y.numel() % 8 == 0, "relu6_bwd: shapes");
+  relu6_bwd(bf(dy), bf(y), bf(dx), y.numel(), cur_stream());
+}
+
 // ---- gconv.hip: grouped convolution (NHWC bf16, fp32 weights [T][C][CG]) -------------------------------
 static void gconv_check(const at::Tensor& x, const at::Tensor& y, int64_t CG, const std::vector<int64_t>& dy,
                         const std::vector<int64_t>& dx) {
@@ -1013,6 +1025,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_apply", &bn_act_apply_t);
   m.def("bn_add_act", &bn_add_act_t);
   m.def("gconv_fwd", &gconv_fwd_t);
+  m.def("relu6", &relu6_t);
+  m.def("relu6_bwd", &relu6_bwd_t);
   m.def("gconv_dgrad", &gconv_dgrad_t);
   m.def("gconv_wgrad_slices", &gconv_wgrad_slices_t);
   m.def("gconv_wgrad", &gconv_wgrad_t);

@@ -104,6 +104,30 @@ DEVI uint4 load_vec(const Ptrs& in, int j, long i, int CG) {
   return v;
 }
 
+// ReLU6 (MobileNetV2): y = min(max(x, 0), 6); backward dx = dy where 0 < y < 6 (hardtanh's mask, from the output)
+__global__ __launch_bounds__(kBlock) void relu6_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       long nvec) {
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + i * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e], 0.f), 6.f);
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void relu6_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                           uint16_t* __restrict__ dx, long nvec) {
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
+    float g[8], v[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + i * 8), g);
+    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (v[e] > 0.f && v[e] < 6.f) ? g[e] : 0.f;
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(g);
+  }
+}
+
 __global__ void add_n_kernel(Ptrs in, int k, uint16_t* __restrict__ out, long nvec, int CG) {
   for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
     float a[8];
@@ -144,6 +168,14 @@ void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, in
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s) {
   const long total = (long)N * h * w * (Cp / 8);
   hipLaunchKernelGGL(pool2_sum_kernel, dim3(grid_for(total)), dim3(kBlock), 0, s, g, out, N, h, w, Cp);
+}
+
+void relu6(const uint16_t* x, uint16_t* y, long n_elem, hipStream_t s) {
+  hipLaunchKernelGGL(relu6_kernel, dim3(grid_for(n_elem / 8)), dim3(kBlock), 0, s, x, y, n_elem / 8);
+}
+
+void relu6_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n_elem, hipStream_t s) {
+  hipLaunchKernelGGL(relu6_bwd_kernel, dim3(grid_for(n_elem / 8)), dim3(kBlock), 0, s, dy, y, dx, n_elem / 8);
 }
 
 void add_n(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,

@@ -176,6 +176,8 @@ void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, in
              const float* lc, int lrelu, const float* sc, int srelu, hipStream_t s);
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s);
 // coefs (nullable): deferred-BN prologue per input (ld = Cp, the channel width of every input)
+void relu6(const uint16_t* x, uint16_t* y, long n_elem, hipStream_t s);   // min(max(x, 0), 6)
+void relu6_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n_elem, hipStream_t s);
 void add_n(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
            long n_elem, int Cp, hipStream_t s);
 void scale_f32(float* x, const float* scalar, float mult, long n, hipStream_t s);

@@ -115,3 +115,28 @@ def add_n(*xs):
         return materialize(xs[0])
     ts, coefs, mask = split_inputs(xs)
     return _AddN.apply((coefs, mask), *ts)
+
+
+class _ReLU6(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C = require()
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        C.relu6(x, y)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        (y,) = ctx.saved_tensors
+        dx = torch.empty_like(y)
+        C.relu6_bwd(g.contiguous(), y, dx)
+        return dx
+
+
+def relu6(x):
+    """``nn.ReLU6`` (MobileNetV2) on an NHWC bf16 map (a ``ops.bn.Deferred`` input is materialised first)."""
+    from .bn import materialize
+    return _ReLU6.apply(materialize(x))

@@ -86,10 +86,15 @@ class SmpDecoders:
         """SegmentationHead: conv (+bias) -> NCHW fp32 logits -> optional bilinear upsampling (align_corners,
         nn.UpsamplingBilinear2d) on the C-channel logits."""
         head = model.segmentation_head
-        logits = self.head(head[0], x, head[0].out_channels)
         if isinstance(head[1], nn.UpsamplingBilinear2d):
-            logits = F.interpolate(logits, scale_factor=head[1].scale_factor, mode='bilinear', align_corners=True)
-        return logits
+            # the upsampling runs on the NHWC bf16 logits (ops.decoder.resize_bilinear, csrc/decoder.hip)
+            # before the one NCHW fp32 conversion: no fp32 NCHW map at 4-8x the head's resolution
+            plan = self.plan_conv(head[0])
+            (y,), _ = conv(plan, [x], want_stats=False)
+            sf = head[1].scale_factor
+            sf = sf[0] if isinstance(sf, (tuple, list)) else sf
+            return from_fm(resize_bilinear(y, scale_factor=float(sf), align_corners=True), head[0].out_channels)
+        return self.head(head[0], x, head[0].out_channels)
 
     # -- Unet++ (smp UnetPlusPlusDecoder) ---------------------------------------------------------------
     def _unet_block(self, blk, x, cx, skips, training):

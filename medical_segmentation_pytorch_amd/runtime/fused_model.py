@@ -26,7 +26,7 @@ import torch.nn as nn
 
 from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
 from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
-from ..ops.elementwise import add_n, from_fm, to_fm, up2_add
+from ..ops.elementwise import add_n, from_fm, relu6, to_fm, up2_add
 from ..ops.gconv import gconv
 from ..ops.pool import maxpool, res_tail, up2_cat
 from .fused_decoders import SmpDecoders, fused_decoder_kind
@@ -520,9 +520,55 @@ class FusedExecutor(SmpDecoders):
             out = model.segmentation_head(model.decoder(*nchw))
         return out.float()
 
+    # -- smp Unet with a MobileNetV2 encoder (reference models/backbone.py:39-57, models/__init__.py:23-25) ----
+    def conv_bn_relu6(self, conv_mod, bn_mod, x, training, act=True):
+        """conv -> BN (-> ReLU6): convs on the implicit-GEMM / halo kernels, depthwise ones on the grouped
+        kernels (csrc/gconv.hip, stride 1 or 2); ReLU6 is its own pass (``ops.elementwise.relu6``) on the
+        materialised BN output.  Without ``act`` the BN output stays deferred (the block's add loads it)."""
+        if conv_mod.groups != 1:
+            y = gconv(materialize(x), conv_mod)
+            z = bn_act([y], self.bn(bn_mod), False, training, deferred=_DEFER_BN)
+        else:
+            plan = self.plan_conv(conv_mod)
+            (y,), part = self._conv(plan, [x], training)
+            z = self._bn_out([y], self.bn(bn_mod), False, training, (part, plan.rows, 0) if training else None)
+        return relu6(z) if act else z
+
+    def inverted_residual(self, blk, x, training):
+        """torchvision InvertedResidual: [1x1 expand-BN-ReLU6] -> 3x3 depthwise-BN-ReLU6 -> 1x1 project-BN
+        (+ x when stride 1 and in == out: one add pass that applies the project BN while loading)."""
+        layers = list(blk.conv)
+        h = x
+        k = 0
+        if len(layers) == 8:   # expand
+            h = self.conv_bn_relu6(layers[0], layers[1], h, training)
+            k = 3
+        h = self.conv_bn_relu6(layers[k], layers[k + 1], h, training)
+        o = self.conv_bn_relu6(layers[k + 3], layers[k + 4], h, training, act=False)
+        return add_n(x, o) if blk.use_res else materialize(o)
+
+    def mobilenet_encoder(self, enc, images, training):
+        x = to_fm(images)
+        feats = []
+        for stage in enc.get_stages()[1:enc._depth + 1]:
+            for m in stage:
+                if isinstance(m, nn.Sequential):   # stem conv / last 1x1: conv-BN-ReLU6
+                    x = self.conv_bn_relu6(m[0], m[1], x, training)
+                else:
+                    x = self.inverted_residual(m, x, training)
+            feats.append(x)
+        return feats
+
+    def mobilenet_unet(self, model, images, training):
+        feats = self.mobilenet_encoder(model.encoder, images, training)
+        return self.unet_decode(model, feats, training)
+
     def resnet_unet(self, model, images, training):
+        return self.unet_decode(model, self.resnet_encoder(model.encoder, images, training), training)
+
+    def unet_decode(self, model, feats, training):
+        """smp UnetDecoder + head over the encoder's stage features (nearest up2 + skip concat, 2 x cba)."""
         enc, dec = model.encoder, model.decoder
-        feats = self.resnet_encoder(enc, images, training)
         chans = list(enc.out_channels[1:])
         skips, skip_ch = feats[:-1][::-1], chans[:-1][::-1]
         x, cx = feats[-1], chans[-1]
@@ -553,6 +599,8 @@ class FusedExecutor(SmpDecoders):
             return self.unet(model, images, training)
         if _is_resnet_unet(model):
             return self.resnet_unet(model, images, training)
+        if _is_mobilenet_unet(model):
+            return self.mobilenet_unet(model, images, training)
         if _is_resnet_smp(model):
             kind = fused_decoder_kind(model)   # Unet++ / Linknet / FPN / DeepLabV3(+) / PSPNet: fully fused
             if kind is not None and _FUSED_DECODERS:
@@ -601,5 +649,20 @@ def eager_parts(model):
     return ['decoder', 'segmentation_head']
 
 
+def _is_mobilenet_unet(model) -> bool:
+    """smp ``Unet`` over the MobileNetV2 encoder (stride 32, BatchNorm decoder blocks, no head upsampling)."""
+    from ..models.smp import MobileNetV2Encoder, SegmentationModel, UnetDecoder
+    if not isinstance(model, SegmentationModel):
+        return False
+    enc, dec = getattr(model, 'encoder', None), getattr(model, 'decoder', None)
+    if not isinstance(enc, MobileNetV2Encoder) or not isinstance(dec, UnetDecoder) or enc._depth != 5:
+        return False
+    if any(_pair(m.dilation) != (1, 1) for m in enc.modules() if isinstance(m, nn.Conv2d)):
+        return False
+    if not isinstance(model.segmentation_head[1], nn.Identity):
+        return False
+    return all(isinstance(b.conv1[1], nn.BatchNorm2d) for b in dec.blocks)
+
+
 def supports(model) -> bool:
-    return type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_smp(model)
+    return type(model).__name__ in ('DuckNet', 'UNet') or _is_resnet_smp(model) or _is_mobilenet_unet(model)

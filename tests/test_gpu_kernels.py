@@ -794,3 +794,19 @@ def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
     assert _rel(xf.grad.permute(0, 3, 1, 2), xr.grad) < 1e-2
     assert _rel(m.weight.grad, wr.grad) < 1e-3
+
+
+def test_relu6_forward_backward(gpu):
+    """ReLU6 on the HIP elementwise kernels (MobileNetV2) vs torch's hardtanh: bitwise on bf16."""
+    from medical_segmentation_pytorch_amd.ops.elementwise import relu6
+    torch.manual_seed(2)
+    x = (torch.randn(2, 8, 9, 16, device=gpu) * 5).to(torch.bfloat16)
+    g = torch.randn_like(x)
+    xr = x.clone().requires_grad_(True)
+    ref = F.relu6(xr)
+    ref.backward(g)
+    xf = x.clone().requires_grad_(True)
+    y = relu6(xf)
+    y.backward(g)
+    assert torch.equal(y, ref)
+    assert torch.equal(xf.grad, xr.grad)

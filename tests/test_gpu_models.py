@@ -56,20 +56,24 @@ def _pretrain(model, gpu, size, batch, steps):
 
 
 ORACLE_STEPS = 300
-ILL_CONDITIONED = 128 * 8   # size * batch of the two bottleneck-ResNet cases (see MODEL_CASES)
+ILL = 'ill'   # MODEL_CASES flag: autocast-bf16 itself is ill-conditioned there -- assert parity with it only
 
 
 # (model, size, batch[, pretraining steps]).  The bottleneck ResNet-50 / ResNeXt-50 encoders are the one
 # family this oracle does not condition: autocast-bf16 itself stays at mean grad cos 0.56 / 0.65 vs fp32
 # after 100 or 300 pretraining steps, at 64 px / batch 2 and at 128 px / batch 8 alike (its layer2/3 BN
 # parameters at 0.2-0.4) -- the fused engine matches autocast there to 0.001 (0.5615 vs 0.5610, 0.6473 vs
-# 0.6463); for them the test asserts that parity, not the absolute 0.9 (ILL_CONDITIONED below).
-# (DUCKNet at 256 px: at 128 px autocast itself only reaches 0.83-0.86 -- its stage 4-5 BNs see 16x16 / 8x8 maps)
-MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 256, 4), (lambda: UNet(2, 3, 32), 64, 4),
+# 0.6463); for them the test asserts that parity, not the absolute 0.9 (the ILL flag).
+# (DUCKNet at 256 px, batch 8: at 128 px / batch 4 autocast itself only reaches 0.83-0.86, at 256 / 4 0.87 --
+# its stage 4-5 BNs normalise 8x8 / 16x16 maps)
+MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 256, 8), (lambda: UNet(2, 3, 32), 64, 4),
                                                  (lambda: _smp_unet('resnet18'), 64, 4),
-                                                 (lambda: _smp_unet('resnet50'), 128, 8, 100),
-                                                 # grouped 3x3 (MIOpen channels-last) between fused ops
-                                                 (lambda: _smp_unet('resnext50_32x4d'), 128, 8, 100),
+                                                 # MobileNetV2 (ReLU6, depthwise 3x3 on csrc/gconv.hip)
+                                                 # (ill-conditioned like the bottleneck ResNets: autocast 0.69)
+                                                 (lambda: _smp_unet('mobilenet_v2'), 128, 4, ORACLE_STEPS, ILL),
+                                                 (lambda: _smp_unet('resnet50'), 128, 8, 100, ILL),
+                                                 # grouped 3x3 (csrc/gconv.hip) between fused ops
+                                                 (lambda: _smp_unet('resnext50_32x4d'), 128, 8, 100, ILL),
                                                  # fully fused decoders (runtime/fused_decoders.py)
                                                  (lambda: _smp('UnetPlusPlus', 'resnet18'), 64, 4),
                                                  (lambda: _smp('FPN', 'resnet18'), 64, 4),
@@ -88,9 +92,9 @@ MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 256, 4), (lambda: UNet(2, 3, 32), 64,
                                                  (lambda: _smp('MAnet', 'resnet18'), 64, 4)]
 
 
-@pytest.mark.parametrize('model_fn,size,batch,steps', [c if len(c) == 4 else c + (ORACLE_STEPS,)
-                                                       for c in MODEL_CASES])
-def test_fused_matches_eager(gpu, model_fn, size, batch, steps):
+@pytest.mark.parametrize('model_fn,size,batch,steps,flag', [(c + (ORACLE_STEPS, None))[:5] if len(c) == 3 else
+                                                            (c + (None,))[:5] for c in MODEL_CASES])
+def test_fused_matches_eager(gpu, model_fn, size, batch, steps, flag):
     """The fused bf16 executor must be as close to fp32 eager as PyTorch's own bf16 autocast is -- measured
     on a well-conditioned oracle (pretrained weights, see _pretrain): autocast-bf16 must itself reach mean
     grad cos > 0.9 vs fp32 there, the fused mean must be within 0.03 of it and every parameter > 0.8."""
@@ -143,7 +147,7 @@ def test_fused_matches_eager(gpu, model_fn, size, batch, steps):
     print(f'grad cos mean: fused {mf:.4f} autocast-bf16 {mb:.4f} over {len(kept)} params ({len(noise)} noise-only: '
           f'{noise[:4]}); min fused {min(a for a, _, _ in kept):.4f} bf16 {min(b for _, b, _ in kept):.4f}')
     print('worst parameters (fused, autocast-bf16, name):', [(round(a, 3), round(b, 3), n) for a, b, n in sorted(kept)[:4]])
-    if size * batch != ILL_CONDITIONED:
+    if flag != ILL:
         assert mb > 0.9, f'oracle not well conditioned (autocast-bf16 vs fp32 mean grad cos {mb:.3f}): train longer'
     assert mf > mb - 0.03, (mf, mb)
     # per parameter: > 0.8 wherever the oracle itself is (autocast-bf16 > 0.9), and never far below autocast
