@@ -773,7 +773,7 @@ def test_parked_gradient_aliasing_its_own_dy_is_not_overwritten(gpu):
 
 
 @pytest.mark.parametrize('c,groups,stride', [(128, 32, 1), (64, 32, 2), (256, 32, 1), (512, 32, 2), (1024, 32, 1),
-                                             (64, 8, 1), (48, 48, 1)])
+                                             (64, 8, 1), (48, 48, 1), (192, 192, 2), (96, 96, 2), (96, 96, 1)])
 def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
     """HIP grouped 3x3 (csrc/gconv.hip; ResNeXt conv2, CG = 4..32 channels per group, stride 1 / 2) vs the
     fp32 PyTorch conv on the same bf16 inputs: output, input gradient and weight gradient."""
