@@ -88,7 +88,7 @@ MODEL_CASES = [(lambda: DuckNet(2, 3, 17), 256, 8), (lambda: UNet(2, 3, 32), 64,
                                                  (lambda: _smp('Linknet', 'resnet18'), 64, 4),
                                                  # (PAN's FPA block pools the stride-16 map to 1/8: at 128 px its
                                                  # 1-channel BNs normalise 1x1 maps over 4 values -- 256 px)
-                                                 (lambda: _smp('PAN', 'resnet18'), 256, 4),
+                                                 (lambda: _smp('PAN', 'resnet18'), 256, 8),
                                                  (lambda: _smp('MAnet', 'resnet18'), 64, 4)]
 
 
