@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       // data-gradient taps = the negated forward taps
       ub = ((-a.dy[t] - fg.ey0) * fg.HWD + (-a.dx[t] - fg.ex0)) * fg.py + 8 * c8;
     } else {
-      ub = 8 * (-1 - u);   // padding unit: an in-tile slot of the wanted bank residue (zero weights)
+      ub = 0;   // padding unit (zero weights): slot 0 of the lane's own pixel -- always staged, never garbage
     }
     s_ub[e] = ub;
   }
@@ -475,8 +475,9 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
 // K-unit order of the data-gradient: positions 4ks + {0, 1} and 4ks + {2, 3} are the two k-groups that one
 // ds_read_b128 lane group mixes (MI355X_MICROARCH §LDS); a pair whose dY tile offsets are equal in 16-B slots
 // mod 16 covers the 16 slots of a 256-B bank row exactly once (16 consecutive pixels at an odd slot pitch).
-// Greedy: each pair takes the first free unit and a free unit of the same residue, else a padding unit
-// (zero weights, any in-tile slot: given that residue), else any free unit.
+// Greedy: each pair takes the first free unit and a free unit of the same residue, else any free unit, else
+// a padding unit (zero weights; it reads slot 0 of the lane's pixel: an offset chosen for its bank residue
+// could land on a never-staged padding slot, and 0 x NaN garbage is NaN).
 void fb_unit_order(FusedBwdArgs& a, const FusedBwdGeom& fg) {
   const int C8g = a.Co / 8, nU0 = a.T * C8g, nU = nU0 + (a.Go == 2 ? C8g : 0), n = 4 * fg.KS;
   int res[96];
@@ -487,7 +488,6 @@ void fb_unit_order(FusedBwdArgs& a, const FusedBwdGeom& fg) {
     const int ub = ((-a.dy[t] - fg.ey0) * fg.HWD + (-a.dx[t] - fg.ex0)) * fg.py + 8 * c8;
     res[u] = (ub / 8) & 15;
   }
-  int npad = n - nU;
   int pos = 0;
   for (int first = 0; pos < n; ) {
     while (first < nU && used[first]) ++first;
@@ -503,9 +503,6 @@ void fb_unit_order(FusedBwdArgs& a, const FusedBwdGeom& fg) {
     if (mate >= 0) {
       used[mate] = true;
       a.uperm[pos++] = (short)mate;
-    } else if (npad > 0) {
-      --npad;
-      a.uperm[pos++] = (short)(-1 - res[first]);
     } else {
       int u = first + 1;
       while (u < nU && used[u]) ++u;

@@ -316,8 +316,7 @@ struct FusedBwdArgs {
   float* dw;
   int N, H, W, Ci, Co, T;
   int dy[9], dx[9];
-  // data-gradient K-unit order (set by conv_bwd_fused): unit index, or -1 - r for a zero-weight padding unit
-  // read at 16-B slot r.  Paired k-groups (0/1, 2/3) share a ds_read_b128 lane group: units paired with
+  // data-gradient K-unit order (set by conv_bwd_fused): unit index, or -1 for a zero-weight padding unit.  Paired k-groups (0/1, 2/3) share a ds_read_b128 lane group: units paired with
   // equal slot offsets mod 16 read conflict-free.
   short uperm[96];
 };

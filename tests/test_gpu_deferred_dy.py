@@ -38,6 +38,8 @@ CASES = [
     (17, 17, (3, 3), 1, 1, 0, (12, 128, 128), True),   # 384 tiles > the 256-block persistent grid: blocks
                                                        # loop over tiles (the double-buffered staging)
     (17, 17, (3, 3), 1, 1, 1, (12, 128, 128), True),   # the Go = 2 fused backward (3x3 + centre 1x1), multi-tile
+    (16, 16, (3, 3), 1, 1, 0, (4, 64, 96), True),      # 16 channels: 2 slots of a 3-slot pixel pitch (the third
+                                                       # never staged: no K unit may read it)
     (17, 17, (3, 3), 2, 1, 1, (2, 40, 56), True),      # Go = 2, dilation 2
 ]
 
