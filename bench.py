@@ -142,6 +142,8 @@ def comm_evidence(step, args, dist, step_ms, device):
     bnmod.COMM['instrument'] = True
     bnmod.COMM['works'] = []
     ex0 = bnmod.EXCHANGES[0]
+    from medical_segmentation_pytorch_amd.runtime import comm as ipc_comm
+    ipc_comm.wait_stats(reset=True)
     sync()
     dist.barrier()
     t0 = time.perf_counter()
@@ -150,8 +152,9 @@ def comm_evidence(step, args, dist, step_ms, device):
     sync()
     out['instrumented_step_ms'] = round((time.perf_counter() - t0) / n * 1e3, 3)
     out['syncbn_exchanges_per_step'] = (bnmod.EXCHANGES[0] - ex0) / n
-    from medical_segmentation_pytorch_amd.runtime import comm as ipc_comm
     out['syncbn_exchange_path'] = ipc_comm.describe()
+    # IPC path: per exchange, the spin before the last peer's flag (rank skew) vs the rest (transport)
+    out['syncbn_ipc_wait'] = ipc_comm.wait_stats(reset=True) or None
     durs = []
     for _, w in bnmod.COMM['works']:
         try:

@@ -881,7 +881,8 @@ void comm_allreduce_t(const at::Tensor& in, const at::Tensor& out, const std::ve
                       int64_t cap, const at::Tensor& epoch, const at::Tensor& err, double timeout_s) {
   CHECK_DEV(in); CHECK_DEV(out); CHECK_I64(epoch); CHECK_DEV(err);
   TORCH_CHECK(in.scalar_type() == at::kDouble && out.scalar_type() == at::kDouble, "comm_allreduce: fp64 rows");
-  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1 && epoch.numel() >= 1, "comm_allreduce: state");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1 && epoch.numel() >= 1 && epoch.is_contiguous(),
+              "comm_allreduce: state");
   const int world = (int)peers.size();
   TORCH_CHECK(world >= 1 && world <= kCommMaxRanks && rank >= 0 && rank < world, "comm_allreduce: bad rank/world");
   TORCH_CHECK(in.numel() == out.numel() && in.numel() <= cap, "comm_allreduce: ", in.numel(),
@@ -896,8 +897,8 @@ void comm_allreduce_t(const at::Tensor& in, const at::Tensor& out, const std::ve
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
   const long long ticks = (long long)(timeout_s * (khz > 0 ? khz : 100000) * 1000.0);
   oneshot_allreduce(in.data_ptr<double>(), out.data_ptr<double>(), in.numel(), pt, (int)rank, world, cap,
-                    reinterpret_cast<unsigned long long*>(epoch.data_ptr<int64_t>()), err.data_ptr<int>(), ticks,
-                    cur_stream());
+                    reinterpret_cast<unsigned long long*>(epoch.data_ptr<int64_t>()), (int)epoch.numel(),
+                    err.data_ptr<int>(), ticks, cur_stream());
 }
 
 // ---- conv_bwd.hip: fused data- + weight-gradient of a narrow stride-1 conv ---------------------------
@@ -1102,4 +1103,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("comm_free", [](int64_t p) { comm_free(reinterpret_cast<void*>(p)); });
   m.def("comm_allreduce", &comm_allreduce_t);
   m.def("comm_max_ranks", []() { return kCommMaxRanks; });
+  m.def("comm_wall_clock_khz", []() {
+    int dev = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    return (int64_t)(khz > 0 ? khz : 100000);
+  });
 }

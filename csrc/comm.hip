@@ -37,17 +37,22 @@ DEVI unsigned long long ld_sys(const unsigned long long* p) {
   return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kCommBlock) void oneshot_allreduce_kernel(const double* __restrict__ in,
-                                                                       double* __restrict__ out, long n,
+// ``in`` and ``out`` may alias (the engine reduces in place): every load of ``in`` happens in step 1, before
+// the barrier that precedes the first store to ``out`` in step 4.
+// ``epoch`` = the state row: [0] epoch, and with ``nstate`` >= 4 the wait instrumentation [1] sum of the
+// per-exchange spin time before the last peer's flag arrived (wall-clock ticks), [2] exchanges, [3] the max.
+__global__ __launch_bounds__(kCommBlock) void oneshot_allreduce_kernel(const double* in, double* out, long n,
                                                                        CommPeers peers, int rank, int world,
                                                                        long cap, unsigned long long* epoch,
-                                                                       int* err, long long timeout) {
+                                                                       int nstate, int* err, long long timeout) {
   __shared__ unsigned long long s_e;
   __shared__ int s_fail;
+  __shared__ unsigned int s_wait;
   const int tid = threadIdx.x;
   if (tid == 0) {
     s_e = epoch[0] + 1ull;
     s_fail = 0;
+    s_wait = 0u;
   }
   __syncthreads();
   const unsigned long long e = s_e;
@@ -70,13 +75,16 @@ __global__ __launch_bounds__(kCommBlock) void oneshot_allreduce_kernel(const dou
   if (tid < world) {
     const unsigned long long* f = reinterpret_cast<const unsigned long long*>(peers.buf[rank]) + tid;
     const long long t0 = wall_clock64();
+    long long t1 = t0;
     while (__hip_atomic_load(const_cast<unsigned long long*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (wall_clock64() - t0 > timeout) {
+      t1 = wall_clock64();
+      if (t1 - t0 > timeout) {
         s_fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    atomicMax(&s_wait, (unsigned int)min(t1 - t0, 0x7fffffffLL));   // LDS atomic
   }
   __syncthreads();
   // 4. reduce in rank order (system-scope loads: the slots were written by other agents)
@@ -89,6 +97,11 @@ __global__ __launch_bounds__(kCommBlock) void oneshot_allreduce_kernel(const dou
   }
   if (tid == 0) {
     epoch[0] = e;
+    if (nstate >= 4) {   // (this kernel is the only writer of the row: plain vector read-modify-write)
+      epoch[1] += s_wait;
+      epoch[2] += 1ull;
+      epoch[3] = max(epoch[3], (unsigned long long)s_wait);
+    }
     if (fail) atomicAdd(err, 1);
   }
 }
@@ -118,7 +131,7 @@ void comm_close(void* ptr) { (void)hipIpcCloseMemHandle(ptr); }
 void comm_free(void* ptr) { (void)hipFree(ptr); }
 
 void oneshot_allreduce(const double* in, double* out, long n, const CommPeers& peers, int rank, int world, long cap,
-                       unsigned long long* epoch, int* err, long long timeout, hipStream_t s) {
+                       unsigned long long* epoch, int nstate, int* err, long long timeout, hipStream_t s) {
   hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(1), dim3(kCommBlock), 0, s, in, out, n, peers, rank, world, cap,
-                     epoch, err, timeout);
+                     epoch, nstate, err, timeout);
 }

@@ -30,7 +30,12 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 DEVI f32x16_t mfma32(const uint4& a, const uint4& b, f32x16_t c) {
+#ifdef GK_KO_MFMA   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
+  c[0] += __uint_as_float(a.x ^ b.y);
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+#endif
 }
 
 // 64 zero bytes in global memory: the DMA source of every padding / out-of-range vector
@@ -42,6 +47,9 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 // the software pipeline.  Here the pipeline's own counted vmcnt waits + barriers order the DMAs
 // against the reads; nothing else in the main loop touches the vector-memory counter.
 DEVI void glds16(const void* src, uint32_t lds) {
+#ifdef GK_KO_DMA
+  return;
+#endif
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
@@ -233,9 +241,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
     for (int s = 0; s < 4; ++s) {
       uint4 af[FM], bfr[FN];
 #pragma unroll
+#ifdef GK_KO_LDS
+      for (int i = 0; i < FM; ++i) af[i] = make_uint4(kt + i, s, lane, 0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = make_uint4(kt, j + s, 0, lane);
+#else
       for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const uint4*>(cur + a_row0 + i * 32 * kRowB + soff[s]);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(cur + b_row0 + j * 32 * kRowB + soff[s]);
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -29,7 +29,12 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
 
 DEVI f32x16_t mfma32(const uint4& a, const uint4& b, f32x16_t c) {
+#ifdef GK_KO_MFMA   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
+  c[0] += __uint_as_float(a.x ^ b.y);
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+#endif
 }
 
 __device__ __attribute__((aligned(64))) uint4 g_wg_zero_page[4];
@@ -37,12 +42,18 @@ __device__ __attribute__((aligned(64))) uint4 g_wg_zero_page[4];
 // LDS-DMA, 16 B per lane (see conv_gemm.hip glds16: inline asm keeps the compiler from draining the
 // pipeline before every ds_read)
 DEVI void glds16(const void* src, uint32_t lds) {
+#ifdef GK_KO_DMA
+  return;
+#endif
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
 
 DEVI uint2 tr_read(const uint8_t* p) {
+#ifdef GK_KO_LDS
+  return make_uint2((uint32_t)(uintptr_t)p, 1u);
+#endif
   s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t __attribute__((address_space(3)))*)(p));
   union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
 }

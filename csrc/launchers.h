@@ -280,7 +280,7 @@ int comm_open(const void* handle64, void** ptr);
 void comm_close(void* ptr);
 void comm_free(void* ptr);
 void oneshot_allreduce(const double* in, double* out, long n, const CommPeers& peers, int rank, int world, long cap,
-                       unsigned long long* epoch, int* err, long long timeout, hipStream_t s);
+                       unsigned long long* epoch, int nstate, int* err, long long timeout, hipStream_t s);
 
 // conv_bwd.hip: fused data- + weight-gradient of a narrow stride-1 conv (one staging of dY and x per tile).
 // Geometry = the FORWARD conv (Gi = Go = 1, Cgi, Cgo <= 32, symmetric taps).  dY = bwd(dz, gy) when gy is set

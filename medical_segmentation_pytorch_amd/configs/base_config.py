@@ -126,8 +126,9 @@ class BaseConfig:
         self.lr_scale = 'reference'    # lr vs batch: 'reference' (x gpu_num) | 'sqrt' | 'linear' in
                                        # global_batch / lr_ref_batch (utils/optimizer.lr_batch_factor)
         self.lr_ref_batch = 16         # the batch base_lr is tuned for (MyConfig train_bs)
-        self.syncbn_comm = 'auto'      # SyncBN statistic exchange: 'auto' (IPC peer-memory kernel on one node,
-                                       # RCCL otherwise) | 'ipc' | 'rccl'  (env MSP_SYNCBN_COMM overrides)
+        self.syncbn_comm = 'rccl'      # SyncBN statistic exchange: 'rccl' | 'auto' (IPC peer-memory kernel on one
+                                       # node after a self-test, RCCL otherwise) | 'ipc'  (env MSP_SYNCBN_COMM
+                                       # overrides; IPC is opt-in until a cross-GPU run of it is recorded)
         self.gpu_augment = True        # run augmentation on the GPU over an HBM-resident dataset
         self.dist_backend = None       # None -> 'nccl' (RCCL) on GPU, 'gloo' on CPU
         self.log_interval = 50         # device-side loss accumulation, host sync every N iters

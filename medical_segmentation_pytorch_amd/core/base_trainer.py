@@ -128,6 +128,11 @@ class BaseTrainer:
                         self.save_ckpt(config, save_best=True)
             if self.main_rank and config.save_ckpt:
                 self.save_ckpt(config)
+            if config.DDP and config.save_ckpt:
+                # rank 0 alone wrote checkpoints: the others wait here, not inside the next epoch's first
+                # collective (a SyncBN exchange would count the skew against its deadline)
+                from ..utils.parallel import get_group
+                torch.distributed.barrier(group=get_group(config))
         if config.use_tb and self.main_rank and self.writer is not None:
             self.writer.flush()
             self.writer.close()

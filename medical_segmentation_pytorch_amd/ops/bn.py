@@ -188,8 +188,15 @@ def resolve(g):
 
 
 def clear_deferred():
-    """Step boundary: drop every token (all have been claimed or resolved by the end of backward)."""
+    """Step boundary: drop every token.  All of them must have been claimed or resolved by the end of
+    backward; a token still unresolved means its gradient reached a node that neither rebuilt nor wrote
+    it (e.g. an autograd accumulation with another gradient): that gradient was garbage, so raise (the
+    mirror of ``ops.conv.check_parked_grads``)."""
+    lost = sum(1 for d in _DEFERRED.values() if not d.done)
     _DEFERRED.clear()
+    if lost:
+        raise RuntimeError(f'{lost} deferred BN data-gradient(s) were never claimed by their producing conv nor '
+                           'resolved: a deferred BN output had a consumer outside the fused backward')
 
 
 def _dy_deferrable(ts):

@@ -10,11 +10,22 @@ for all flags in its own buffer and sums the slots in rank order (bitwise-identi
 rank).  No host round trip, no proxy thread, and the kernel is hipGraph-capturable (the epoch counter
 lives in device memory).
 
-Policy (``config.syncbn_comm`` / env ``MSP_SYNCBN_COMM``): ``'auto'`` (default) uses it for GPU process
-groups of a single-node job, after a self-test exchange of known values succeeded on every rank (all
-ranks agree, so a failure anywhere falls back everywhere); ``'rccl'`` forces the RCCL path; ``'ipc'``
-requires the IPC path (errors if it cannot be set up).  Rows larger than the buffer capacity and every
-multi-node group go through RCCL.
+Policy (``config.syncbn_comm`` / env ``MSP_SYNCBN_COMM``): ``'rccl'`` (default) keeps every exchange on
+RCCL; ``'auto'`` uses the IPC kernel for GPU process groups of a single-node job, after a self-test exchange
+of known values succeeded on every rank (all ranks agree, so a failure anywhere falls back everywhere);
+``'ipc'`` requires the IPC path (errors if it cannot be set up).  Rows larger than the buffer capacity and
+every multi-node group go through RCCL.  The IPC path is opt-in until a cross-GPU run of it is on record
+(it has only run as several processes sharing one GPU): a stalled exchange there ends in NaN and a fatal
+:func:`check`, where RCCL would wait up to the process-group timeout.
+
+Timeout: a peer that has not arrived after ``timeout_s`` (env ``MSP_SYNCBN_IPC_TIMEOUT`` seconds, else
+``config.dist_timeout_min``, else 30 minutes -- the process-group default) makes the exchange return NaN
+and count an error, so rank skew from host-side work (checkpoint writing on rank 0, validation) is
+waited out like RCCL would, and only a dead peer turns into the named error.
+
+Instrumentation: the kernel accumulates, per exchange, how long it spun before the LAST peer's flag
+arrived (:meth:`IpcAllReduce.wait_stats`): on an xGMI node that separates rank skew (long waits) from
+transport latency (the remaining exchange time).
 """
 from __future__ import annotations
 
@@ -27,7 +38,18 @@ import torch.distributed as dist
 
 from ..ops._ext import require
 
-POLICY = {'mode': os.environ.get('MSP_SYNCBN_COMM', 'auto')}
+POLICY = {'mode': os.environ.get('MSP_SYNCBN_COMM', 'rccl'), 'timeout_s': None}
+
+
+def default_timeout_s(config=None) -> float:
+    """Exchange deadline: env MSP_SYNCBN_IPC_TIMEOUT (s) > ``config.dist_timeout_min`` > 30 min."""
+    env = os.environ.get('MSP_SYNCBN_IPC_TIMEOUT')
+    if env:
+        return float(env)
+    if POLICY.get('timeout_s'):
+        return float(POLICY['timeout_s'])
+    minutes = getattr(config, 'dist_timeout_min', None) if config is not None else None
+    return float(minutes) * 60.0 if minutes else 1800.0
 _COMMS: Dict[object, Optional['IpcAllReduce']] = {}
 _LOG = []
 
@@ -35,7 +57,7 @@ _LOG = []
 class IpcAllReduce:
     """In-place SUM all-reduce of small fp64 rows over the ranks of ``group`` (one node)."""
 
-    def __init__(self, group, device, cap=32768, timeout_s=30.0):
+    def __init__(self, group, device, cap=32768, timeout_s=None):
         C = require()
         self.group = group
         self.world = dist.get_world_size(group)
@@ -43,7 +65,7 @@ class IpcAllReduce:
         if self.world > C.comm_max_ranks():
             raise ValueError(f'IPC all-reduce supports up to {C.comm_max_ranks()} ranks')
         self.cap = int(cap)
-        self.timeout_s = float(timeout_s)
+        self.timeout_s = float(timeout_s) if timeout_s is not None else default_timeout_s()
         self.device = device
         self.own, handle, self.opened, self.peers = 0, None, [], []
         try:   # a local failure must not skip the collective below (the other ranks are waiting in it)
@@ -63,7 +85,8 @@ class IpcAllReduce:
                     p = C.comm_open(h)
                     self.opened.append(p)
                     self.peers.append(p)
-        self.epoch = torch.zeros(1, dtype=torch.int64, device=device)
+        # [epoch, sum of last-flag wait ticks, exchanges, max wait ticks] (csrc/comm.hip)
+        self.epoch = torch.zeros(4, dtype=torch.int64, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.calls = 0
         atexit.register(self.close)
@@ -76,6 +99,17 @@ class IpcAllReduce:
     def fits(self, buf: torch.Tensor) -> bool:
         return (buf.dtype == torch.float64 and buf.is_contiguous() and buf.numel() <= self.cap
                 and buf.device == self.epoch.device)
+
+    def wait_stats(self, reset=False):
+        """(exchanges, mean / max spin before the last peer's flag, in us) since the last reset (host sync)."""
+        st = self.epoch[1:4].tolist()
+        khz = require().comm_wall_clock_khz()
+        n = st[1]
+        res = {'exchanges': n, 'wait_us_mean': (st[0] / n / khz * 1e3) if n else None,
+               'wait_us_max': st[2] / khz * 1e3 if n else None}
+        if reset:
+            self.epoch[1:4].zero_()
+        return res
 
     def errors(self) -> int:
         """Exchanges that timed out waiting for a peer (host sync)."""
@@ -159,6 +193,11 @@ def lookup(group) -> Optional[IpcAllReduce]:
 
 def active() -> bool:
     return any(c is not None for c in _COMMS.values())
+
+
+def wait_stats(reset=False):
+    """Per attached IPC communicator: :meth:`IpcAllReduce.wait_stats` (empty when every group is on RCCL)."""
+    return [c.wait_stats(reset) for c in _COMMS.values() if c is not None]
 
 
 def check():

@@ -117,7 +117,8 @@ def parallel_model(config, model, rank, device, optimizer=None):
             optimizer.attach_bucketer(bucketer)
         from ..runtime import comm as ipc_comm
         from ..runtime.engine import stat_group
-        ipc_comm.POLICY['mode'] = os.environ.get('MSP_SYNCBN_COMM', getattr(config, 'syncbn_comm', 'auto'))
+        ipc_comm.POLICY['mode'] = os.environ.get('MSP_SYNCBN_COMM', getattr(config, 'syncbn_comm', 'rccl'))
+        ipc_comm.POLICY['timeout_s'] = ipc_comm.default_timeout_s(config)
         from ..runtime.fused_model import eager_parts
         if group is not None and config.synBN:
             # modules that run eagerly inside the fused model (smp decoders over a fused encoder): torch
