@@ -165,9 +165,11 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
   const float* gsp[kMaxGroups];
   const float* gkp[kMaxGroups];
   const bool bwd = fill_bwd(gy, gs, gk, g.Go, (int64_t)g.N * g.OH * g.OW * g.Cgo, g.Cgo, gyp, gsp, gkp);
-  TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans, bwd), "dw numel mismatch (replicas)");
   const float* cf[kMaxGroups];
   fill_coefs(xc, g.Gi, std::vector<int64_t>(g.Gi, g.Cgi), cf);
+  bool pro = false;
+  for (int i = 0; i < g.Gi; ++i) pro |= cf[i] != nullptr;
+  TORCH_CHECK(dw.numel() == one * conv_wgrad_replicas(g, trans, bwd, pro), "dw numel mismatch (replicas)");
   TORCH_CHECK(!trans || xc.empty(), "no BN prologue on transposed weight-gradients");
   const int rc = conv_wgrad(pd.data(), px.data(), f32(dw), g, trans, cf, (unsigned)xrelu, cur_stream(), gyp, gsp, gkp,
                             (unsigned)grelu);
@@ -175,8 +177,8 @@ void conv_wgrad_t(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs, const
 }
 
 int64_t conv_wgrad_replicas_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
-                              bool bwd) {
-  return conv_wgrad_replicas(make_geom(dims, dy, dx), trans, bwd);
+                              bool bwd, bool pro) {
+  return conv_wgrad_replicas(make_geom(dims, dy, dx), trans, bwd, pro);
 }
 
 bool conv_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans, bool bwd) {
@@ -971,6 +973,8 @@ void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy,
 
 }  // namespace
 
+extern "C" const char* msp_sources_sha();   // build/csrc/sources_sha.cpp (generated by csrc/build.py)
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for medical_segmentation_pytorch_amd";
   m.def("conv_fwd", &conv_fwd, py::arg("xs"), py::arg("wp"), py::arg("ys"), py::arg("bias"), py::arg("stat_part"),
@@ -1010,7 +1014,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("T"), py::arg("Cpk"), py::arg("Ktot"), py::arg("t_base"), py::arg("c_base"), py::arg("s_row"),
         py::arg("s_ch"), py::arg("accumulate"), py::arg("nrep") = 1, py::arg("rep_stride") = 0);
   m.def("conv_wgrad_replicas", &conv_wgrad_replicas_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"),
-        py::arg("bwd") = false);
+        py::arg("bwd") = false, py::arg("pro") = false);
   m.def("pack_batch", &pack_batch_t);
   m.def("pack_per_block", &pack_per_block);
   m.def("bn_partial_blocks", [](int64_t P, int64_t Cp) { return bn_partial_blocks(P, Cp); });
@@ -1103,6 +1107,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("comm_free", [](int64_t p) { comm_free(reinterpret_cast<void*>(p)); });
   m.def("comm_allreduce", &comm_allreduce_t);
   m.def("comm_max_ranks", []() { return kCommMaxRanks; });
+  m.def("sources_sha", []() { return std::string(msp_sources_sha()); });
   m.def("comm_wall_clock_khz", []() {
     int dev = 0, khz = 0;
     (void)hipGetDevice(&dev);

@@ -1527,7 +1527,9 @@ int conv_pick_mi(int rows) {
 int conv_rows_alloc(int rows) {
   int r = 0;
   for (int mi = 1; mi <= 4; ++mi) r = std::max(r, cdiv(rows, 16 * mi) * 16 * mi);
-  return r;
+  // + one zero row of slack: the LDS-tiled GEMM's last K stage reads up to 32 elements past Kp of the
+  // last real row (conv_gemm.hip stage(): times a zero B operand, but it must stay inside the buffer)
+  return r + 1;
 }
 
 // PIPE (persistent, next tile prefetched in registers) runs the MI 3 / NJ 4 row groups of thin-halo 3x3
@@ -1936,8 +1938,8 @@ static bool wgrad_use_gemm(const ConvGeom& g, bool trans) {
   return g.Cgi >= 64 || g.stride > 1 || g.T == 1 || trans || !wgrad_halo_ok(g, tl);
 }
 
-int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd) {
-  if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm_replicas(g);
+int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd, bool pro) {
+  if (wgrad_use_gemm(g, trans)) return conv_wgrad_gemm_replicas(g, pro);
   return (int)wgrad_plan(g, trans, bwd).nsplit;
 }
 

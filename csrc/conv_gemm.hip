@@ -77,25 +77,33 @@ DEVI void kpos_advance(KPos& p, int by, int Cgi, int Gi) {
   }
 }
 
-constexpr int kBK = 64;          // k per stage
-constexpr int kRowB = kBK * 2;   // bytes per staged row
-
 struct GemmGeom {
   long M, OHW;
   int n_co, nk;
 };
 
-template <int WM, int WN, int FM, int FN, int NS>
+// BK = k per stage (64 or 32): one staged row (co or pixel) is BK bf16 = ROWB bytes, one DMA instruction
+// (64 lanes x 16 B) fills RPI rows.  BK 32 halves the bytes per stage, so the same LDS holds twice the
+// stages in flight (the round-5 knock-outs showed the BK-64 kernel bound by LDS-DMA latency at one stage
+// in flight, profiles/r05/gemm_knockouts_bs320.txt).
+template <int WM, int WN, int FM, int FN, int NS, int BK>
 struct GemmCfg {
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int TCO = 32 * WM * FM, TPX = 32 * WN * FN;
-  static constexpr int A_BYTES = TCO * kRowB, B_BYTES = TPX * kRowB, STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_INS = TCO / 8 / NW, B_INS = TPX / 8 / NW;   // DMA instructions per wave per stage
+  static constexpr int ROWB = BK * 2, SLOTS = BK / 8, RPI = 1024 / ROWB;
+  static constexpr int A_BYTES = TCO * ROWB, B_BYTES = TPX * ROWB, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_INS = TCO / RPI / NW, B_INS = TPX / RPI / NW;   // DMA instructions per wave per stage
   // (the epilogue's stats scratch reuses the stages)
   static constexpr int LDS = NS * STAGE;
-  static_assert(TCO % (8 * NW) == 0 && TPX % (8 * NW) == 0, "tile rows must split evenly over the waves");
+  static_assert(BK == 64 || BK == 32, "stage width");
+  static_assert(TCO % (RPI * NW) == 0 && TPX % (RPI * NW) == 0, "tile rows must split evenly over the waves");
   static_assert(2 * WN * TCO * 4 <= NS * STAGE, "stats scratch must fit in the staging LDS");
-  static_assert(NS >= 2 && NS <= 4 && 2 * (A_INS + B_INS) < 64, "pipeline depth / vmcnt range");
+  static_assert(NS >= 2 && NS <= 5 && (NS - 2) * (A_INS + B_INS) < 64, "pipeline depth / vmcnt range");
+  static_assert(NW % 2 == 0, "one logical k slot per lane across the wave's DMA instructions");
+  // XOR swizzle of the 16-B slots of a row (source side of the DMA, undone by the fragment reads): the 16
+  // rows of a ds_read_b128 lane group land on 16 distinct bank slots.  BK 64: 128-B rows, slot ^= (row >> 1)
+  // & 7; BK 32: 64-B rows (four per 256-B bank row), slot ^= (row >> 2) & 3.
+  static DEVI int swz(int row) { return BK == 64 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
 };
 
 // Regular tap grid (every conv this path takes): tap t = (r, c), r = t / kw, c = t % kw, offset
@@ -104,9 +112,10 @@ struct GemmCfg {
 // between two LDS-DMAs makes the compiler drain every DMA in flight (vmcnt(0)) before it.
 struct TapGrid { int kw, y0, ys, x0, xs; };
 
-template <int WM, int WN, int FM, int FN, int NS, bool BNE>
+template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, GemmGeom gg, TapGrid tg) {
-  using C = GemmCfg<WM, WN, FM, FN, NS>;
+  using C = GemmCfg<WM, WN, FM, FN, NS, BK>;
+  constexpr int kRowB = C::ROWB, RPI = C::RPI;
   const ConvGeom& g = a.g;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -125,89 +134,97 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   const int rows = g.Go * g.Cgo;
   const int Cgi = g.Cgi, Gi = g.Gi;
   const int IHW = g.IH * g.IW;
-  const uint16_t* x0p = a.x[0];
 
-  // ---- DMA roles: instruction j of this wave fills tile rows 8*(j*NW + wave) .. +7; lane -> row
-  // (lane >> 3), physical 16-B slot (lane & 7) = logical slot ^ ((row >> 1) & 7)
+  // ---- DMA roles: instruction j of this wave fills tile rows RPI*(j*NW + wave) .. +RPI-1; lane -> row
+  // lane / SLOTS, physical 16-B slot lane % SLOTS = logical slot ^ swz(row).  With NW even, swz(row) does
+  // not depend on j, so a lane's LOGICAL slot ls -- its k offset 8*ls inside the stage -- is the same for
+  // every instruction j of the wave.
+  const int ls = (lane % C::SLOTS) ^ C::swz(RPI * wave + lane / C::SLOTS);
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page);
+  // A (packed weights): a fixed row pointer per instruction; the stage adds its k base.  Rows past the
+  // layer read row 0 (their outputs are never stored) and the K tail of the last stage reads past Kp into
+  // the next row / the allocation's slack (packed_weight_slack): finite values times a zero B operand.
   const uint16_t* a_src[C::A_INS];
-  int a_k[C::A_INS];
 #pragma unroll
   for (int j = 0; j < C::A_INS; ++j) {
-    const int row = 8 * (j * C::NW + wave) + (lane >> 3);
-    const int ls = (lane & 7) ^ ((row >> 1) & 7);
-    const int co = co0 + row;
-    a_k[j] = co < rows ? 8 * ls : 1 << 30;   // rows past the layer read the zero page
+    const int co = co0 + RPI * (j * C::NW + wave) + lane / C::SLOTS;
     a_src[j] = a.w + (long)(co < rows ? co : 0) * g.Kp + 8 * ls;
   }
-  // B (im2col) lanes: output pixel -> (image base, oh*stride, ow*stride); k position -> tap (tr, tc),
-  // input group gi, channel cl, advanced by 64 per stage with register arithmetic only
-  int b_pn[C::B_INS], b_ph[C::B_INS], b_pw[C::B_INS], b_tr[C::B_INS], b_tc[C::B_INS], b_gi[C::B_INS], b_cl[C::B_INS];
+  // B (im2col of the input): per instruction the pixel's input origin (element offset, taps excluded) and
+  // a bitmask of the taps that land inside the image -- both fixed for the whole K walk.
+  long b_pix[C::B_INS];
+  uint32_t b_vm[C::B_INS];
 #pragma unroll
   for (int j = 0; j < C::B_INS; ++j) {
-    const int row = 8 * (j * C::NW + wave) + (lane >> 3);
-    const int ls = (lane & 7) ^ ((row >> 1) & 7);
-    const long m = px0 + row;
+    const long m = px0 + RPI * (j * C::NW + wave) + lane / C::SLOTS;
+    b_pix[j] = 0;
+    b_vm[j] = 0u;
     if (m < gg.M) {
       const int n = (int)(m / gg.OHW);
       const int r = (int)(m - (long)n * gg.OHW);
       const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
-      b_pn[j] = n * IHW;
-      b_ph[j] = oh * g.stride + tg.y0;
-      b_pw[j] = ow * g.stride + tg.x0;
-    } else {
-      b_pn[j] = -1; b_ph[j] = 0; b_pw[j] = 0;
+      const int ih0 = oh * g.stride, iw0 = ow * g.stride;
+      b_pix[j] = ((long)n * IHW + (long)ih0 * g.IW + iw0) * Cgi;
+      uint32_t vm = 0u;
+      int tr = 0, tc = 0;
+      for (int t = 0; t < g.T; ++t) {
+        const int ih = ih0 + tg.y0 + tr * tg.ys, iw = iw0 + tg.x0 + tc * tg.xs;
+        if ((unsigned)ih < (unsigned)g.IH && (unsigned)iw < (unsigned)g.IW) vm |= 1u << t;
+        if (++tc == tg.kw) { tc = 0; ++tr; }
+      }
+      b_vm[j] = vm;
     }
-    const int Cip = Gi * Cgi, k = 8 * ls;
-    const int t = k / Cip, rem = k - (k / Cip) * Cip;
-    b_tr[j] = t / tg.kw;
-    b_tc[j] = t - (t / tg.kw) * tg.kw;
-    b_gi[j] = rem / Cgi;
-    b_cl[j] = rem - (rem / Cgi) * Cgi;
   }
-  const int kh = g.T / tg.kw;
+  // K walk, uniform (SGPRs): the stage's first k = (tap t0 = (tr0, tc0), group g0, channel cl0); toff0 = the
+  // element offset of tap t0 from the pixel origin.  Cgi >= 64 >= the stage width, so the slots of a row
+  // cross at most one (group | tap) boundary: a lane at slot ls >= (Cgi - cl0) / 8 is in the next one.
+  const long dcol = (long)tg.xs * Cgi, drow = ((long)tg.ys * g.IW - (long)tg.kw * tg.xs) * Cgi;
+  int t0 = 0, tr0 = 0, tc0 = 0, g0 = 0, cl0 = 0;
+  long toff0 = ((long)tg.y0 * g.IW + tg.x0) * Cgi;
+  auto gptr = [&](int q) {   // group pointer from the kernel arguments (scalars), no memory read
+    const uint16_t* xb = a.x[0];
+#pragma unroll
+    for (int u = 1; u < kMaxGroups; ++u) xb = q == u ? a.x[u] : xb;
+    return xb;
+  };
 
   auto stage = [&](int kt, uint32_t sb) {
-    const int kb = kt * kBK;
+    const int kb = kt * BK;
 #pragma unroll
-    for (int j = 0; j < C::A_INS; ++j) {
-      const bool ok = kb + a_k[j] < g.Kp;
-      glds16(ok ? (const void*)(a_src[j] + kb) : (const void*)zero, sb + (8 * (j * C::NW + wave)) * kRowB);
+    for (int j = 0; j < C::A_INS; ++j) glds16(a_src[j] + kb, sb + (RPI * (j * C::NW + wave)) * kRowB);
+    // the (group | tap) after the current one
+    int g1 = g0 + 1, t1 = t0, tr1 = tr0, tc1 = tc0;
+    long toff1 = toff0;
+    if (g1 == Gi) {
+      g1 = 0;
+      ++t1;
+      toff1 += dcol;
+      if (++tc1 == tg.kw) { tc1 = 0; ++tr1; toff1 += drow; }
     }
+    const int rem0 = Cgi - cl0;
+    const bool nx = 8 * ls >= rem0;   // (per lane)
+    const int t = nx ? t1 : t0;
+    const uint16_t* base = (nx ? gptr(g1) : gptr(g0)) + (nx ? toff1 + (8 * ls - rem0) : toff0 + (cl0 + 8 * ls));
+    const bool tin = t < 32;
 #pragma unroll
     for (int j = 0; j < C::B_INS; ++j) {
-      const void* src = zero;
-      if (b_pn[j] >= 0 && b_tr[j] < kh) {
-        const int ih = b_ph[j] + b_tr[j] * tg.ys, iw = b_pw[j] + b_tc[j] * tg.xs;
-        if ((unsigned)ih < (unsigned)g.IH && (unsigned)iw < (unsigned)g.IW) {
-          const uint16_t* xb = x0p;
-          if (Gi > 1) {   // group pointer from the kernel arguments (scalars), no memory read
-#pragma unroll
-            for (int q = 1; q < kMaxGroups; ++q) xb = b_gi[j] == q ? a.x[q] : xb;
-          }
-          src = xb + ((long)(b_pn[j] + ih * g.IW + iw) * Cgi + b_cl[j]);
-        }
-      }
-      glds16(src, sb + C::A_BYTES + (8 * (j * C::NW + wave)) * kRowB);
-      // advance k by 64 (Cgi >= 64: at most one group / tap wrap)
-      b_cl[j] += kBK;
-      if (b_cl[j] >= Cgi) {
-        b_cl[j] -= Cgi;
-        if (++b_gi[j] == Gi) {
-          b_gi[j] = 0;
-          if (++b_tc[j] == tg.kw) { b_tc[j] = 0; ++b_tr[j]; }
-        }
-      }
+      const bool ok = tin && ((b_vm[j] >> t) & 1u);
+      glds16(ok ? (const void*)(base + b_pix[j]) : (const void*)zero,
+             sb + C::A_BYTES + (RPI * (j * C::NW + wave)) * kRowB);
     }
+    // advance the walk by BK (at most one boundary: Cgi >= 64)
+    cl0 += BK;
+    if (cl0 >= Cgi) { cl0 -= Cgi; g0 = g1; t0 = t1; tr0 = tr1; tc0 = tc1; toff0 = toff1; }
   };
 
   // ---- fragment reads: lane (r = lane & 31, h = lane >> 5) takes 8 k at logical slot 2s + h of row r
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int lr = lane & 31, lh = lane >> 5;
-  const int key = (lane >> 1) & 7;   // == (row >> 1) & 7 for every fragment row (bases are multiples of 32)
-  int soff[4];
+  const int key = C::swz(lr);   // == swz(row) for every fragment row (bases are multiples of 32)
+  constexpr int KS = BK / 16;    // MFMA k-steps per stage
+  int soff[KS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) soff[s] = (((2 * s + lh) ^ key) << 4);
+  for (int s = 0; s < KS; ++s) soff[s] = (((2 * s + lh) ^ key) << 4);
   const int a_row0 = (wm * FM * 32 + lr) * kRowB;
   const int b_row0 = C::A_BYTES + (wn * FN * 32 + lr) * kRowB;
 
@@ -230,15 +247,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
     if (p < nk) stage(p, sbase + p * C::STAGE);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(nk - 1 - kt, NS - 2);   // stages issued after kt and still allowed in flight
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * INS) : "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
+    if (NS >= 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * INS) : "memory");
+    else if (NS >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * INS) : "memory");
+    else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (kt + NS - 1 < nk) stage(kt + NS - 1, sbase + ((kt + NS - 1) % NS) * C::STAGE);
     const uint8_t* cur = smem + (kt % NS) * C::STAGE;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < KS; ++s) {
       uint4 af[FM], bfr[FN];
 #pragma unroll
 #ifdef GK_KO_LDS
@@ -371,18 +389,25 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
 
 // ---- configurations ------------------------------------------------------------------------------
 // (WM, WN, FM, FN): TCO = 32*WM*FM co rows x TPX = 32*WN*FN pixels per block
-struct CfgId { int wm, wn, fm, fn, ns; };
+struct CfgId { int wm, wn, fm, fn, ns, bk; };
 // Two LDS stages everywhere: two blocks per CU (8 waves) measured 1.5-2x faster than one block with
 // a third stage (profiles/r03/gemm_cfg_sweep_bs128.log); the tile height is the main lever (B-operand
 // reuse), so the planner picks the tallest tile whose row padding stays small.
 constexpr CfgId kCfgs[] = {
-    {2, 2, 3, 2, 2},   // 192 x 128 (80 KB)
-    {2, 2, 2, 2, 2},   // 128 x 128 (64 KB)
-    {1, 4, 3, 1, 2},   //  96 x 128 (56 KB)
-    {1, 4, 5, 1, 2},   // 160 x 128 (72 KB)
-    {2, 2, 1, 2, 2},   //  64 x 128 (48 KB)
+    {2, 2, 3, 2, 2, 64},   // 192 x 128 (80 KB)
+    {2, 2, 2, 2, 2, 64},   // 128 x 128 (64 KB)
+    {1, 4, 3, 1, 2, 64},   //  96 x 128 (56 KB)
+    {1, 4, 5, 1, 2, 64},   // 160 x 128 (72 KB)
+    {2, 2, 1, 2, 2, 64},   //  64 x 128 (48 KB)
+    // round 5: 32-wide stages, 3-4 of them in flight at two blocks per CU (8-wave 256 x 256 tiles at one
+    // block per CU measured slower: profiles/r05/gemm_cfg_sweep_bs320.txt)
+    {2, 2, 2, 2, 4, 32},   // 128 x 128, 4 stages (64 KB)
+    {2, 2, 3, 2, 4, 32},   // 192 x 128, 4 stages (80 KB)
+    {2, 2, 4, 2, 3, 32},   // 256 x 128, 3 stages (72 KB)
+    {2, 2, 2, 2, 5, 32},   // 128 x 128, 5 stages (80 KB)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+constexpr int kPlannerCfgs = 5;   // the planner's candidates (the rest: MSP_CONV_GEMM_CFG A/B only)
 constexpr int kGemmTPX = 128;   // stat partial rows = pixel tiles of 128 (a 256-pixel tile writes two rows)
 
 int g_gemm_mode = -1;     // env MSP_CONV_GEMM: 0 off, else on (default on)
@@ -409,7 +434,7 @@ int gemm_pick_cfg(int rows) {
   if (g_gemm_cfg >= 0) return g_gemm_cfg;
   int best = 0;
   double best_cost = 1e30;
-  for (int c = 0; c < kNumCfgs; ++c) {
+  for (int c = 0; c < kPlannerCfgs; ++c) {
     const int tco = 32 * kCfgs[c].wm * kCfgs[c].fm;
     const int tiles = cdiv(rows, tco);
     const double cost = (double)tiles * (tco + 48.0);   // + the B-operand staging each co tile repeats
@@ -434,36 +459,40 @@ bool tap_grid(const ConvGeom& g, TapGrid& tg) {
   return false;
 }
 
-template <int WM, int WN, int FM, int FN, int NS, bool BNE>
+template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE>
 void launch_gemm(const ConvArgs& a, hipStream_t s) {
-  using C = GemmCfg<WM, WN, FM, FN, NS>;
+  using C = GemmCfg<WM, WN, FM, FN, NS, BK>;
   const ConvGeom& g = a.g;
   GemmGeom gg;
   gg.OHW = (long)g.OH * g.OW;
   gg.M = (long)g.N * gg.OHW;
   gg.n_co = cdiv(g.Go * g.Cgo, C::TCO);
-  gg.nk = cdiv(g.Kp, kBK);
+  gg.nk = cdiv(g.Kp, BK);
   const long blocks = (long)cdiv(gg.M, C::TPX) * gg.n_co;
   static bool attr = false;
   if (!attr) {   // > 64 KB dynamic LDS: opted into once per instantiation, before any graph capture
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<WM, WN, FM, FN, NS, BNE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   TapGrid tg;
   (void)tap_grid(g, tg);   // conv_gemm_ok checked it
-  hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BNE>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
+  hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
                      tg);
 }
 
 template <bool BNE>
 int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_gemm<2, 2, 3, 2, 2, BNE>(a, s); return 0;
-    case 1: launch_gemm<2, 2, 2, 2, 2, BNE>(a, s); return 0;
-    case 2: launch_gemm<1, 4, 3, 1, 2, BNE>(a, s); return 0;
-    case 3: launch_gemm<1, 4, 5, 1, 2, BNE>(a, s); return 0;
-    case 4: launch_gemm<2, 2, 1, 2, 2, BNE>(a, s); return 0;
+    case 0: launch_gemm<2, 2, 3, 2, 2, 64, BNE>(a, s); return 0;
+    case 1: launch_gemm<2, 2, 2, 2, 2, 64, BNE>(a, s); return 0;
+    case 2: launch_gemm<1, 4, 3, 1, 2, 64, BNE>(a, s); return 0;
+    case 3: launch_gemm<1, 4, 5, 1, 2, 64, BNE>(a, s); return 0;
+    case 4: launch_gemm<2, 2, 1, 2, 2, 64, BNE>(a, s); return 0;
+    case 5: launch_gemm<2, 2, 2, 2, 4, 32, BNE>(a, s); return 0;
+    case 6: launch_gemm<2, 2, 3, 2, 4, 32, BNE>(a, s); return 0;
+    case 7: launch_gemm<2, 2, 4, 2, 3, 32, BNE>(a, s); return 0;
+    case 8: launch_gemm<2, 2, 2, 2, 5, 32, BNE>(a, s); return 0;
   }
   return 1;
 }
@@ -476,7 +505,7 @@ int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
 bool conv_gemm_ok(const ConvGeom& g, bool trans) {
   gemm_env();
   if (!g_gemm_mode || trans) return false;
-  if (g.Cgi < g_gemm_min_c || g.Cgi % 8 != 0 || g.T > kMaxTaps) return false;
+  if (g.Cgi < g_gemm_min_c || g.Cgi % 8 != 0 || g.T > 30) return false;   // tap bitmask per pixel (stage())
   TapGrid tg;
   if (!tap_grid(g, tg)) return false;
   const long M = (long)g.N * g.OH * g.OW;

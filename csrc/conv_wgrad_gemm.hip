@@ -299,6 +299,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_gemm_kernel(WgradP
   }
 }
 
+// the deferred-BN prologue needs one channel vector per lane: B rows of <= 256 B (TK <= 128)
+constexpr bool wg_pro_ok(int wn, int fn) { return 32 * wn * fn <= 128; }
+
 struct WgCfg { int wm, wn, fm, fn; };
 // TCO x TK tiles (LDS per stage = 64 * (TCO + TK) * 2 B, two stages).  Every TK <= 128 (B rows <= 256 B):
 // the deferred-BN prologue then works on every configuration, so it never changes the plan.
@@ -309,6 +312,10 @@ constexpr WgCfg kWgCfgs[] = {
     {2, 2, 2, 1},   // 128 x  64
     {1, 4, 2, 1},   //  64 x 128  (waves along k)
     {2, 2, 4, 1},   // 256 x  64
+    // 8-wave tiles, one block per CU (round 5, see conv_gemm.hip kCfgs); no deferred-BN prologue (TK > 128)
+    {2, 4, 4, 2},   // 256 x 256 (128 KB)
+    {2, 4, 2, 2},   // 128 x 256 ( 96 KB)
+    {4, 2, 2, 2},   // 256 x 128 ( 96 KB)
 };
 constexpr int kNumWgCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 
@@ -331,11 +338,12 @@ void wg_env() {
   }
 }
 
-int wg_pick(int rows, int KT) {
-  if (g_wg_cfg >= 0) return g_wg_cfg;
+int wg_pick(int rows, int KT, bool pro) {
+  if (g_wg_cfg >= 0 && (!pro || wg_pro_ok(kWgCfgs[g_wg_cfg].wn, kWgCfgs[g_wg_cfg].fn))) return g_wg_cfg;
   int best = 0;
   double best_cost = 1e30;
   for (int c = 0; c < kNumWgCfgs; ++c) {
+    if (pro && !wg_pro_ok(kWgCfgs[c].wn, kWgCfgs[c].fn)) continue;
     const int tco = 32 * kWgCfgs[c].wm * kWgCfgs[c].fm, tk = 32 * kWgCfgs[c].wn * kWgCfgs[c].fn;
     const double nt = (double)cdiv(rows, tco) * cdiv(KT, tk);
     // padded MFMA work + operand staging per tile (in MAC units of one 64-pixel stage)
@@ -361,9 +369,9 @@ bool wg_tap_grid(const ConvGeom& g, WgGeom& w) {
 
 struct WgPlan { int cfg; WgGeom w; long blocks; int nsplit; };
 
-WgPlan wg_plan(const ConvGeom& g) {
+WgPlan wg_plan(const ConvGeom& g, bool pro) {
   WgPlan p{};
-  p.cfg = wg_pick(g.Go * g.Cgo, g.T * g.Gi * g.Cgi);
+  p.cfg = wg_pick(g.Go * g.Cgo, g.T * g.Gi * g.Cgi, pro);
   const WgCfg& c = kWgCfgs[p.cfg];
   WgGeom& w = p.w;
   (void)wg_tap_grid(g, w);
@@ -384,10 +392,13 @@ WgPlan wg_plan(const ConvGeom& g) {
 }
 
 template <int WM, int WN, int FM, int FN>
-void launch_wg(const WgradPtrs& P, float* dw, const ConvGeom& g, const WgPlan& p, bool pro, hipStream_t s) {
+int launch_wg(const WgradPtrs& P, float* dw, const ConvGeom& g, const WgPlan& p, bool pro, hipStream_t s) {
   constexpr int LDS = 2 * kBP * (32 * WM * FM + 32 * WN * FN) * 2;
   static bool attr[2] = {false, false};
   if (pro) {
+    if constexpr (!wg_pro_ok(WN, FN)) {
+      return 1;
+    } else {
     if (!attr[1]) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_gemm_kernel<WM, WN, FM, FN, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -395,7 +406,8 @@ void launch_wg(const WgradPtrs& P, float* dw, const ConvGeom& g, const WgPlan& p
     }
     hipLaunchKernelGGL((conv_wgrad_gemm_kernel<WM, WN, FM, FN, true>), dim3((unsigned)p.blocks), dim3(64 * WM * WN),
                        LDS, s, P, dw, g, p.w);
-    return;
+    return 0;
+    }
   }
   if (!attr[0]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_gemm_kernel<WM, WN, FM, FN, false>),
@@ -404,6 +416,7 @@ void launch_wg(const WgradPtrs& P, float* dw, const ConvGeom& g, const WgPlan& p
   }
   hipLaunchKernelGGL((conv_wgrad_gemm_kernel<WM, WN, FM, FN, false>), dim3((unsigned)p.blocks), dim3(64 * WM * WN), LDS,
                      s, P, dw, g, p.w);
+  return 0;
 }
 
 
@@ -420,9 +433,9 @@ bool conv_wgrad_gemm_ok(const ConvGeom& g, bool trans) {
   return M < (1L << 31) - 2 * kBP;
 }
 
-int conv_wgrad_gemm_replicas(const ConvGeom& g) {
+int conv_wgrad_gemm_replicas(const ConvGeom& g, bool pro) {
   wg_env();
-  return wg_plan(g).nsplit;
+  return wg_plan(g, pro).nsplit;
 }
 
 void conv_wgrad_gemm_set(int mode) { wg_env(); g_wg_mode = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
@@ -431,14 +444,17 @@ void conv_wgrad_gemm_force_cfg(int cfg) { wg_env(); g_wg_cfg = (cfg >= 0 && cfg 
 int conv_wgrad_gemm_num_cfgs() { return kNumWgCfgs; }
 
 int conv_wgrad_gemm(const WgradPtrs& P, float* dw, const ConvGeom& g, bool prologue, hipStream_t s) {
-  const WgPlan p = wg_plan(g);
+  const WgPlan p = wg_plan(g, prologue);
   switch (p.cfg) {
-    case 0: launch_wg<2, 2, 2, 2>(P, dw, g, p, prologue, s); return 0;
-    case 1: launch_wg<1, 4, 1, 1>(P, dw, g, p, prologue, s); return 0;
-    case 2: launch_wg<2, 2, 1, 2>(P, dw, g, p, prologue, s); return 0;
-    case 3: launch_wg<2, 2, 2, 1>(P, dw, g, p, prologue, s); return 0;
-    case 4: launch_wg<1, 4, 2, 1>(P, dw, g, p, prologue, s); return 0;
-    case 5: launch_wg<2, 2, 4, 1>(P, dw, g, p, prologue, s); return 0;
+    case 0: return launch_wg<2, 2, 2, 2>(P, dw, g, p, prologue, s);
+    case 1: return launch_wg<1, 4, 1, 1>(P, dw, g, p, prologue, s);
+    case 2: return launch_wg<2, 2, 1, 2>(P, dw, g, p, prologue, s);
+    case 3: return launch_wg<2, 2, 2, 1>(P, dw, g, p, prologue, s);
+    case 4: return launch_wg<1, 4, 2, 1>(P, dw, g, p, prologue, s);
+    case 5: return launch_wg<2, 2, 4, 1>(P, dw, g, p, prologue, s);
+    case 6: return launch_wg<2, 4, 4, 2>(P, dw, g, p, prologue, s);
+    case 7: return launch_wg<2, 4, 2, 2>(P, dw, g, p, prologue, s);
+    case 8: return launch_wg<4, 2, 2, 2>(P, dw, g, p, prologue, s);
   }
   return 1;
 }

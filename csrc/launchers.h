@@ -73,7 +73,7 @@ struct WgradPtrs {
 
 // conv_wgrad_gemm.hip: LDS-tiled weight-gradient GEMM (LDS-DMA staging, transposed fragment reads)
 bool conv_wgrad_gemm_ok(const ConvGeom& g, bool trans);
-int conv_wgrad_gemm_replicas(const ConvGeom& g);
+int conv_wgrad_gemm_replicas(const ConvGeom& g, bool pro = false);
 int conv_wgrad_gemm(const WgradPtrs& P, float* dw, const ConvGeom& g, bool prologue, hipStream_t s);
 void conv_wgrad_gemm_set(int mode);   // 0 off, 1 auto (planner), 2 every eligible conv
 int conv_wgrad_gemm_mode();
@@ -105,7 +105,7 @@ int conv_gemm_num_cfgs();
 int conv_gemm_cfg_tco(int rows);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
 int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
-int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd = false);   // bwd: see conv_wgrad
+int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd = false, bool pro = false);   // bwd: see conv_wgrad
 // xc / xrelu: the deferred-BN prologue of the x groups (see ConvArgs; xc may be nullptr)
 // gy/gs/gk/grelu: the deferred BN-backward prologue of the dY groups (nullable; halo kernel only)
 int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, const ConvGeom& g, bool trans,

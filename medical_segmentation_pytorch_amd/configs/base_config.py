@@ -126,6 +126,9 @@ class BaseConfig:
         self.lr_scale = 'reference'    # lr vs batch: 'reference' (x gpu_num) | 'sqrt' | 'linear' in
                                        # global_batch / lr_ref_batch (utils/optimizer.lr_batch_factor)
         self.lr_ref_batch = 16         # the batch base_lr is tuned for (MyConfig train_bs)
+        self.accum_steps = 1           # gradient accumulation: micro-batches per optimizer step (DDP averaging
+                                       # semantics: global batch = train_bs x gpu_num x accum_steps; BN
+                                       # statistics per micro-batch, as torch DDP + no_sync)
         self.syncbn_comm = 'rccl'      # SyncBN statistic exchange: 'rccl' | 'auto' (IPC peer-memory kernel on one
                                        # node after a self-test, RCCL otherwise) | 'ipc'  (env MSP_SYNCBN_COMM
                                        # overrides; IPC is opt-in until a cross-GPU run of it is recorded)

@@ -117,6 +117,7 @@ def get_parser():
     _flag(p, 'syncbn_comm', type=str, choices=['auto', 'ipc', 'rccl'])
     _flag(p, 'lr_scale', type=str, choices=['reference', 'sqrt', 'linear'])
     _flag(p, 'lr_ref_batch', type=int)
+    _flag(p, 'accum_steps', type=int)
     _flag(p, 'val_fp32', action='store_true')
     _flag(p, 'gpu_augment', action='store_false')
     _flag(p, 'trace', action='store_true')

@@ -14,6 +14,7 @@ MI355X changes:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 
@@ -62,14 +63,26 @@ class SegTrainer(BaseTrainer):
         self.val_history = []
 
     # ------------------------------------------------------------------------------------------------
+    def _accum(self):
+        return max(1, int(getattr(self.config_ref, 'accum_steps', 1) or 1))
+
     def eager_step(self, images, masks):
+        """One eager micro-step.  Gradient accumulation (``config.accum_steps`` K): zero_grad on a group's
+        first micro-batch, ``loss / K`` back-propagated on each (torch DDP: ``no_sync`` on all but the last),
+        ``scaler.step`` / ``update`` on its last; ``self._stepped`` tells the caller."""
         config = self.config_ref
+        accum = self._accum()
+        micro = getattr(self, '_micro', 0)
+        first, last = micro == 0, micro == accum - 1
+        self._micro = 0 if last else micro + 1
+        self._stepped = last
         if getattr(self, 'channels_last', False) and images.dim() == 4:
             images = images.contiguous(memory_format=torch.channels_last)
-        self.optimizer.zero_grad()
-        ex = getattr(self.model, 'executor', None)
-        if ex is not None:   # prepacked conv weights must follow the last optimizer step
-            ex.repack()
+        if first:
+            self.optimizer.zero_grad()
+            ex = getattr(self.model, 'executor', None)
+            if ex is not None:   # prepacked conv weights must follow the last optimizer step
+                ex.repack()
         amp = config.amp_training and not self.fused and self.device.type == 'cuda'
         dtype = torch.float16 if config.amp_dtype == 'fp16' else torch.bfloat16
         with torch.autocast('cuda', dtype=dtype, enabled=amp):
@@ -82,10 +95,14 @@ class SegTrainer(BaseTrainer):
             loss_kd = kd_loss_fn(config, preds.float(), teacher_preds.detach().float())
             loss = loss + config.kd_loss_coefficient * loss_kd
             self._last_kd = loss_kd.detach()
-        self.scaler.scale(loss).backward()
+        obj = loss if accum == 1 else loss * (1.0 / accum)
+        no_sync = self.model.no_sync() if (not last and hasattr(self.model, 'no_sync')) else contextlib.nullcontext()
+        with no_sync:   # torch DDP: the gradient all-reduce only on the group's last micro-batch
+            self.scaler.scale(obj).backward()
         flush_pending()
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+        if last:
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
         return loss.detach()
 
     def _use_graph(self, config):
@@ -107,7 +124,7 @@ class SegTrainer(BaseTrainer):
             self.engine = StepEngine(self.model, self.optimizer, self.loss_fn, self.scaler,
                                      teacher=self.teacher_model if config.kd_training else None, kd_fn=kd_fn,
                                      kd_coef=config.kd_loss_coefficient, use_graph=self._use_graph(config),
-                                     warmup=config.graph_warmup)
+                                     warmup=config.graph_warmup, accum_steps=getattr(config, 'accum_steps', 1))
             if self.main_rank and self.logger:
                 self.logger.info(f'step engine: hipGraph capture {"on" if self.engine.use_graph else "off"} '
                                  f'(world {config.gpu_num if config.DDP else 1}, gradient bucketer '
@@ -127,8 +144,9 @@ class SegTrainer(BaseTrainer):
             self._last_kd = engine.last_kd.clone() if engine.last_kd is not None else None
             return loss
         loss = self.eager_step(images, masks)
-        self.scheduler.step()
-        self.ema_model.update(self.model, self.train_itrs)
+        if self._stepped:   # (gradient accumulation: only after an optimizer step)
+            self.scheduler.step()
+            self.ema_model.update(self.model, self.train_itrs // self._accum())
         return loss
 
     def _flush_logs(self, config, pbar=None):

@@ -26,6 +26,36 @@ except Exception as e:  # pragma: no cover - depends on build state
     _ERR = e
 
 
+def tree_sources_sha():
+    """sha256 of the csrc/ sources in this tree (``csrc/build.py sources_sha``), or None without them."""
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = os.path.join(root, 'csrc', 'build.py')
+    if not os.path.isfile(path):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('_msp_csrc_build', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.sources_sha()
+
+
+def _check_provenance():
+    """Refuse an extension built from other sources than the tree's (a stale prebuilt ``_C.so``): it would
+    bench / test kernels the sources do not describe.  env MSP_ALLOW_STALE_EXT=1 skips the check."""
+    global _C, _ERR
+    if _C is None or os.environ.get('MSP_ALLOW_STALE_EXT') == '1':
+        return
+    want = tree_sources_sha()
+    got = _C.sources_sha() if hasattr(_C, 'sources_sha') else None
+    if want is not None and got != want:
+        _ERR = RuntimeError(f'stale HIP extension {getattr(_C, "__file__", "?")}: built from sources {got!s:.16}, '
+                            f'the tree has {want:.16} -- rebuild with `python csrc/build.py`')
+        _C = None
+
+
+_check_provenance()
+
+
 def available() -> bool:
     return _C is not None
 

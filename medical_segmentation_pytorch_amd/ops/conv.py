@@ -480,7 +480,7 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None):
     dims = plan.fwd_dims(n, ih, iw, oh, ow)
     dy, dx = _taps(plan.taps_fwd)
     KT = plan.T * plan.Cip
-    nrep = C.conv_wgrad_replicas(dims, dy, dx, False, bool(bk))   # split-K dW slabs, summed in fixed order
+    nrep = C.conv_wgrad_replicas(dims, dy, dx, False, bool(bk), bool(coefs))   # split-K dW slabs, summed in fixed order
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
     C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask, **bk)
     return _unpack_slabs(plan, dwp, nrep, need)

@@ -158,6 +158,9 @@ class GradBucketer:
         # instrument=True records, per bucket, an event at issue time and the RCCL work (its on-stream
         # duration needs TORCH_NCCL_ENABLE_TIMING=1), read back by collect() after the step
         self.enabled = True
+        # gradient accumulation: False on every micro-step but an optimizer step's last (torch DDP no_sync):
+        # the gradients keep accumulating in the arena and only the last micro-step's backward buckets them
+        self.sync = True
         self.instrument = False
         self.records = []
         self.ready_order = []   # parameter indices in the order their gradients landed (first step)
@@ -217,6 +220,8 @@ class GradBucketer:
         self.launch_order = []
 
     def ready(self, params):
+        if not self.sync:
+            return
         for p in params:
             i = self.pidx.get(id(p))
             if i is None:

@@ -32,15 +32,29 @@ class StepEngine:
     ``loss_fn(preds, masks)``; ``scaler``: :class:`utils.optimizer.FusedGradScaler` or None; ``teacher``: a
     frozen eval-mode model (KD) with ``kd_fn(student, teacher)`` and ``kd_coef``.  ``static``: optional
     (images, masks) tensors that ARE the graph inputs (the caller writes every batch into them); otherwise
-    each call copies its batch into engine-owned static buffers."""
+    each call copies its batch into engine-owned static buffers.
+
+    ``accum_steps`` K > 1: gradient accumulation -- each call is one micro-batch; the first of a group zeroes
+    the gradient arena, every one back-propagates ``loss / K`` (the kernels accumulate weight / BN-parameter
+    gradients into the arena), and only the K-th runs the bucketed all-reduce (earlier micro-steps keep the
+    bucketer quiet: torch DDP ``no_sync``) and the optimizer; ``stepped`` tells the caller whether this call
+    stepped (scheduler / EMA follow optimizer steps).  Graph mode captures one graph per micro-step kind
+    (first / middle / last) in ONE shared memory pool (replayed strictly in capture order, never
+    concurrently).  BN statistics are per micro-batch, as with DDP + no_sync."""
 
     def __init__(self, model, optimizer, loss_fn, scaler=None, teacher=None, kd_fn=None, kd_coef=1.0,
-                 use_graph=True, warmup=1, static=None):
+                 use_graph=True, warmup=1, static=None, accum_steps=1):
         self.model, self.optimizer, self.loss_fn, self.scaler = model, optimizer, loss_fn, scaler
         self.teacher, self.kd_fn, self.kd_coef = teacher, kd_fn, kd_coef
-        self.use_graph, self.warmup = use_graph, max(1, int(warmup))
+        self.accum = max(1, int(accum_steps))
+        # every micro-step kind must have run eagerly once before its capture (lazy state, plan creation)
+        self.use_graph, self.warmup = use_graph, max(1, int(warmup), self.accum)
         self.images, self.masks = static if static is not None else (None, None)
-        self.graph = None
+        self.graph = None       # the most recently captured graph (accum 1: THE step graph)
+        self.graphs = {}        # (first, last) micro-step kind -> captured graph
+        self._pool = None
+        self.micro = 0          # micro-step index inside the current optimizer step
+        self.stepped = False    # whether the latest call ran the optimizer
         self.loss = self.kd = None
         self.last_kd = None    # KD term of the latest step (the graph's static output or a ragged eager step)
         self.calls = 0
@@ -66,11 +80,17 @@ class StepEngine:
             self._nbt_inc = inc
         arena.nbt.add_(self._nbt_inc)
 
-    def body(self, images, masks):
-        """zero_grad -> repack -> forward -> loss [+ KD] -> backward -> optimizer (+ scaler) -- capturable."""
+    def body(self, images, masks, first=True, last=True):
+        """zero_grad -> repack -> forward -> loss [+ KD] -> backward -> optimizer (+ scaler) -- capturable.
+        Gradient accumulation: zero_grad / repack only on a group's ``first`` micro-step, all-reduce + optimizer
+        only on its ``last``."""
         opt = self.optimizer
-        opt.zero_grad()
-        self.executor.repack()
+        if first:
+            opt.zero_grad()
+            self.executor.repack()
+        bk = getattr(opt, 'bucketer', None)
+        if bk is not None:
+            bk.sync = last
         preds = self.model(images)
         loss = self.loss_fn(preds, masks)
         kd = None
@@ -81,11 +101,13 @@ class StepEngine:
             loss = loss + self.kd_coef * kd
             kd = kd.detach()
         sc = self.scaler if self.scaler is not None and self.scaler.is_enabled() else None
-        (sc.scale(loss) if sc is not None else loss).backward()
+        obj = loss if self.accum == 1 else loss * (1.0 / self.accum)   # the mean over the group's micro-batches
+        (sc.scale(obj) if sc is not None else obj).backward()
         flush_pending()   # SyncBN exchanges parked by the last BN backwards (normally none)
-        opt.launch(sc)    # bucket all-reduce wait + one optimizer kernel (fp16: finite check / skip)
-        if sc is not None:
-            sc.update()
+        if last:
+            opt.launch(sc)    # bucket all-reduce wait + one optimizer kernel (fp16: finite check / skip)
+            if sc is not None:
+                sc.update()
         if self.model.training:
             self._count_bn()
         return loss.detach(), kd   # the autograd graph (and every ctx it holds) dies with this step
@@ -95,6 +117,9 @@ class StepEngine:
         stream, the last of them builds the weight pack program; the next call captures the body and
         replays it; every later call is one replay."""
         self.calls += 1
+        first, last = self.micro == 0, self.micro == self.accum - 1
+        self.micro = 0 if last else self.micro + 1
+        self.stepped = last
         if self.images is None:
             self.images, self.masks = torch.empty_like(images), torch.empty_like(masks)
         if images is not None and images is not self.images:
@@ -102,32 +127,39 @@ class StepEngine:
                 # ragged batch: not capturable, run eagerly.  Its loss / KD term are returned through
                 # last_kd, never stored over self.loss / self.kd: those are the captured graph's static
                 # outputs, which every later replay refreshes
-                self.optimizer.prepare()
-                loss, self.last_kd = self.body(images, masks)
+                if last:
+                    self.optimizer.prepare()
+                loss, self.last_kd = self.body(images, masks, first, last)
                 return loss
             self.images.copy_(images, non_blocking=True)
             self.masks.copy_(masks, non_blocking=True)
-        self.optimizer.prepare()
+        if last:   # this step's hyper-parameters (lr, bias corrections): host work, outside the graph
+            self.optimizer.prepare()
         ex = self.executor
         if not self.use_graph or self.calls <= self.warmup:
             if self.use_graph and self.images.is_cuda:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    self.loss, self.kd = self.body(self.images, self.masks)
+                    self.loss, self.kd = self.body(self.images, self.masks, first, last)
                 torch.cuda.current_stream().wait_stream(s)
             else:
-                self.loss, self.kd = self.body(self.images, self.masks)
+                self.loss, self.kd = self.body(self.images, self.masks, first, last)
             if ex.pack_program is None and (not self.use_graph or self.calls == self.warmup):
                 ex.build_pack_program(self.images.device)
             self.last_kd = self.kd
             return self.loss
-        if self.graph is None:
+        key = (first, last)
+        g = self.graphs.get(key)
+        if g is None:
             torch.cuda.synchronize()
-            self.graph = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(self.graph, capture_error_mode=capture_mode()):
-                self.loss, self.kd = self.body(self.images, self.masks)
-        self.graph.replay()
+            g = torch.cuda.CUDAGraph()
+            with no_gc(), torch.cuda.graph(g, pool=self._pool, capture_error_mode=capture_mode()):
+                self.loss, self.kd = self.body(self.images, self.masks, first, last)
+            self._pool = g.pool()
+            self.graphs[key] = g
+            self.graph = g
+        g.replay()
         self.last_kd = self.kd
         return self.loss
 
@@ -136,11 +168,13 @@ def iteration(engine, scheduler, ema, itrs, images=None, masks=None):
     """One training iteration exactly as ``SegTrainer.train_one_epoch`` runs it: device step, then the
     per-iteration scheduler step and EMA update (reference core/seg_trainer.py:82-87)."""
     loss = engine(images, masks)
+    if not engine.stepped:   # gradient accumulation: a micro-step without an optimizer step
+        return loss
     # the optimizer step ran inside the engine (launched, not via optimizer.step()): tell the LR
     # scheduler's call-order check so, which it otherwise warns about on the first step
     engine.optimizer._opt_called = True
     scheduler.step()
-    ema.update(engine.model, itrs)
+    ema.update(engine.model, itrs // engine.accum)   # the EMA ramp counts optimizer steps
     return loss
 
 
@@ -154,7 +188,7 @@ class FusedStep:
     def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
                  total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
                  syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
-                 kd_coef=1.0, feed=None):
+                 kd_coef=1.0, feed=None, accum_steps=1):
         from ..utils.model_ema import ModelEmaV2
         from ..utils.optimizer import FusedOptimizer
         from ..utils.parallel import FusedModel
@@ -184,7 +218,8 @@ class FusedStep:
             t_fm = FusedModel(teacher).eval()
         self.engine = StepEngine(self.fm, self.opt, lambda p, m: cross_entropy(p, m, None, ignore_index),
                                  teacher=t_fm, kd_fn=lambda s, t: kd_kl_div(s, t, kd_temperature),
-                                 kd_coef=kd_coef, use_graph=use_graph, warmup=1, static=(images, masks))
+                                 kd_coef=kd_coef, use_graph=use_graph, warmup=1, static=(images, masks),
+                                 accum_steps=accum_steps)
         self.feed = feed
         self.itrs = 0
 

@@ -183,14 +183,16 @@ def lr_batch_factor(config):
 
     ``config.lr_scale`` = ``'reference'`` (default; reference ``utils/optimizer.py:9,15``: x gpu_num, the
     per-GPU batch is fixed at MyConfig's 16), ``'sqrt'`` (x sqrt(global batch / lr_ref_batch)) or
-    ``'linear'`` (x global batch / lr_ref_batch).  The global batch is train_bs x gpu_num; lr_ref_batch
-    (16) is the batch the reference's base_lr was tuned for.  With Adam the square-root rule is the stable
-    one (the update is scale-free, so its noise falls as 1/sqrt(batch)); warm-up comes from the OneCycle
-    schedule's warmup_epochs."""
+    ``'linear'`` (x global batch / lr_ref_batch).  The global batch is train_bs x gpu_num x accum_steps;
+    lr_ref_batch (16) is the batch the reference's base_lr was tuned for.  With Adam the square-root rule is
+    the stable one (the update is scale-free, so its noise falls as 1/sqrt(batch)); warm-up comes from the
+    OneCycle schedule's warmup_epochs.  Gradient accumulation counts as replicas for the reference rule
+    (x gpu_num x accum_steps): one GPU accumulating 8 micro-batches takes the lr of the 8-GPU run it emulates."""
     rule = getattr(config, 'lr_scale', 'reference') or 'reference'
+    accum = max(1, int(getattr(config, 'accum_steps', 1) or 1))
     if rule == 'reference':
-        return float(config.gpu_num)
-    ratio = config.train_bs * config.gpu_num / float(getattr(config, 'lr_ref_batch', 16) or 16)
+        return float(config.gpu_num * accum)
+    ratio = config.train_bs * config.gpu_num * accum / float(getattr(config, 'lr_ref_batch', 16) or 16)
     if rule == 'sqrt':
         return ratio ** 0.5
     if rule == 'linear':

@@ -14,7 +14,10 @@ def get_scheduler(config, optimizer):
     else:
         config.iters_per_epoch = ceil(config.train_num / config.train_bs)
     config.iters_per_epoch = max(config.iters_per_epoch, 1)
-    config.total_itrs = int(config.total_epoch * config.iters_per_epoch)
+    # the schedule (and the EMA decay ramp) counts OPTIMIZER steps: with gradient accumulation one step takes
+    # accum_steps loader iterations (an incomplete group at an epoch end carries into the next epoch)
+    accum = max(1, int(getattr(config, 'accum_steps', 1) or 1))
+    config.total_itrs = max(int(config.total_epoch * config.iters_per_epoch) // accum, 1)
 
     if config.lr_policy == 'cos_warmup':
         warmup_ratio = config.warmup_epochs / config.total_epoch

@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size=2) tests of the distributed layer, CPU only."""
+"""Multi-process (gloo, world_size 2 and 4) tests of the distributed layer, CPU only."""
 import os
 import socket
 
@@ -36,7 +36,8 @@ def _bucketer_worker(rank, world, port, q, compress=None):
     for p in reversed(arena.params):
         b.ready([p])
     b.finish()
-    ok = all(torch.allclose(p.grad, torch.full_like(p.grad, 3.0 * (i + 1))) for i, p in enumerate(arena.params))
+    tot = world * (world + 1) / 2
+    ok = all(torch.allclose(p.grad, torch.full_like(p.grad, tot * (i + 1))) for i, p in enumerate(arena.params))
     q.put((rank, ok, len(b.buckets)))
     dist.destroy_process_group()
 
@@ -87,14 +88,15 @@ def test_grad_bucketer_rebuilds_in_ready_order(compress):
         assert any(packed)                         # scrambled order: some buckets go through the staging buffer
 
 
+@pytest.mark.parametrize('world', [2, 4])
 @pytest.mark.parametrize('compress', [None, 'bf16'])
-def test_grad_bucketer_allreduce(compress):
-    """Bucketed all-reduce (SUM) of the grad arena; values 1*(i+1) + 2*(i+1) are exact in bf16 too."""
+def test_grad_bucketer_allreduce(compress, world):
+    """Bucketed all-reduce (SUM) of the grad arena; values sum_r (r+1)*(i+1) are exact in bf16 too."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    mp.spawn(_bucketer_worker, args=(2, port, q, compress), nprocs=2, join=True)
-    res = [q.get() for _ in range(2)]
+    mp.spawn(_bucketer_worker, args=(world, port, q, compress), nprocs=world, join=True)
+    res = [q.get() for _ in range(world)]
     assert all(ok for _, ok, _ in res) and all(nb > 1 for _, _, nb in res)
 
 
@@ -112,26 +114,84 @@ def _metric_sampler_worker(rank, world, port, q):
     dice = d.compute()
     # sampler sharding: disjoint, covering
     from torch.utils.data.distributed import DistributedSampler
-    s = DistributedSampler(list(range(10)), num_replicas=world, rank=rank, shuffle=True, seed=1)
+    s = DistributedSampler(list(range(12)), num_replicas=world, rank=rank, shuffle=True, seed=1)
     s.set_epoch(3)
     q.put((rank, iou.tolist(), dice.item(), list(s), logits.tolist(), tgt.tolist()))
     dist.destroy_process_group()
 
 
-def test_distributed_metrics_and_sampler():
+@pytest.mark.parametrize('world', [2, 4])
+def test_distributed_metrics_and_sampler(world):
+    """One confusion-matrix all-reduce gives every rank the pooled (exact) IoU / Dice; the sampler's shards
+    are disjoint and cover the set (reference utils/parallel.py + torchmetrics sync)."""
     from medical_segmentation_pytorch_amd.utils.metrics import Dice, JaccardIndex
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    mp.spawn(_metric_sampler_worker, args=(2, _port(), q), nprocs=2, join=True)
-    res = sorted([q.get() for _ in range(2)], key=lambda r: r[0])
+    mp.spawn(_metric_sampler_worker, args=(world, _port(), q), nprocs=world, join=True)
+    res = sorted([q.get() for _ in range(world)], key=lambda r: r[0])
     m, d = JaccardIndex(num_classes=2, sync=False), Dice(num_classes=2, sync=False)
     for r in res:
         m.update(torch.tensor(r[4]), torch.tensor(r[5]))
         d.update(torch.tensor(r[4]), torch.tensor(r[5]))
-    assert torch.allclose(torch.tensor(res[0][1]), m.compute()) and torch.allclose(torch.tensor(res[1][1]), m.compute())
-    assert abs(res[0][2] - d.compute().item()) < 1e-6
-    a, b = res[0][3], res[1][3]
-    assert not set(a) & set(b) and sorted(a + b) == list(range(10))
+    for r in res:
+        assert torch.equal(torch.tensor(r[1]), m.compute())    # exact: integer confusion-matrix counts
+        assert abs(r[2] - d.compute().item()) < 1e-6
+    shards = [set(r[3]) for r in res]
+    assert sum(len(s) for s in shards) == len(set().union(*shards))   # disjoint
+    assert set().union(*shards) == set(range(12))                      # covering
+
+
+def _full_batch_worker(rank, world, port, q):
+    """DDP semantics at world ``world``: every rank back-propagates the mean loss of ITS shard into the grad
+    arena, the bucketer sums the ranks' gradients and the optimizer's 1/world makes it the mean -- which must
+    equal one process's gradient of the mean loss over the whole batch.  Same for SyncBN statistics: every
+    rank parks its (sum, sum^2) row in the exchange queue (ops.bn._Pending), one all-reduce, and the
+    finalized mean / biased variance must equal the full batch's."""
+    _init(rank, world, port)
+    try:
+        from medical_segmentation_pytorch_amd.ops import bn
+        from medical_segmentation_pytorch_amd.runtime.engine import Arena, GradBucketer
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Linear(24, 48), nn.Tanh(), nn.Linear(48, 5))
+        arena = Arena(model, torch.device('cpu'))
+        b = GradBucketer(arena, None, bucket_cap_mb=0.002, first_bucket_mb=0.001)
+        g = torch.Generator().manual_seed(3)
+        x, y = torch.randn(8 * world, 24, generator=g), torch.randn(8 * world, 5, generator=g)
+        ref = nn.Sequential(nn.Linear(24, 48), nn.Tanh(), nn.Linear(48, 5))
+        ref.load_state_dict(model.state_dict())
+        ((ref(x) - y) ** 2).mean().backward()                       # the single-process full batch
+        xs, ys = x[rank::world], y[rank::world]
+        arena.grad.zero_()
+        ((model(xs) - ys) ** 2).mean().backward()
+        for p in reversed(list(model.parameters())):
+            b.ready([p])
+        b.finish()
+        ok_grad = all(torch.allclose(p.grad / world, r.grad, rtol=1e-5, atol=1e-7)
+                      for p, r in zip(model.parameters(), ref.parameters()))
+        feats = torch.randn(6 * world, 7, generator=g) * 3 + 1
+        mine = feats[rank::world]
+        row = torch.cat([mine.sum(0), (mine * mine).sum(0)]).double().view(1, -1)
+        out = {}
+        bn._FWD.add(row, dist.group.WORLD, lambda s: out.__setitem__('s', s.clone()), 12345)
+        bn.need_stats_all()
+        s = out['s'].view(2, 7)
+        n = feats.shape[0]
+        mean, var = s[0] / n, s[1] / n - (s[0] / n) ** 2
+        ok_bn = torch.allclose(mean.float(), feats.mean(0), atol=1e-5) and \
+            torch.allclose(var.float(), feats.var(0, unbiased=False), atol=1e-4)
+        q.put((rank, ok_grad, ok_bn, len(b.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_ddp_step_and_syncbn_equal_full_batch_world4():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    mp.spawn(_full_batch_worker, args=(4, _port(), q), nprocs=4, join=True)
+    res = [q.get() for _ in range(4)]
+    assert all(ok_g for _, ok_g, _, _ in res), res
+    assert all(ok_b for _, _, ok_b, _ in res), res
+    assert all(nb > 1 for *_, nb in res)
 
 
 def _trainer_worker(rank, world, port, root, q):

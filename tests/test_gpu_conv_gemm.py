@@ -47,7 +47,7 @@ GEMM_CASES = [
 ]
 
 
-@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4])
+@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize('case', GEMM_CASES)
 def test_gemm_conv_fwd_bwd(gpu, ext, case, cfg):
     n, h, w, ci, co, (kh, kw), s, pad, dil, groups, bias = case
@@ -150,7 +150,7 @@ WGRAD_CASES = [
 ]
 
 
-@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize('prologue', [False, True])
 @pytest.mark.parametrize('case', WGRAD_CASES)
 def test_wgrad_gemm(gpu, ext, case, prologue, cfg):
@@ -182,7 +182,7 @@ def test_wgrad_gemm(gpu, ext, case, prologue, cfg):
             xc, xr = [st], 1
             z = _bf(torch.relu(x * st[0, :ci].view(1, -1, 1, 1) + st[1, :ci].view(1, -1, 1, 1)))
         KT = plan.T * plan.Cip
-        nrep = C.conv_wgrad_replicas(dims, dy, dx, False)
+        nrep = C.conv_wgrad_replicas(dims, dy, dx, False, False, bool(xc))
         dwp = torch.empty(nrep * plan.rows * KT, device=gpu)
         C.conv_wgrad(gys, [xf], dwp, dims, dy, dx, False, xc, xr)
         tot = dwp.view(nrep, plan.rows, KT).sum(0)          # [rows][t*Cip + c]

@@ -1,0 +1,136 @@
+"""Direct fp32 oracle of the fused narrow-conv backward (csrc/conv_bwd.hip ``conv_bwd_fused``): the kernel's
+data-gradient, weight-gradient split-K slabs and upstream-BN backward partials against ``F.conv2d``'s
+input / weight gradients in fp32 on the same bf16 operands -- not against the materialised HIP path.
+
+Chain case of the DUCKNet L1 level (reference models/ducknet.py:95-96,144-179): BN1 -> conv -> BN2, with
+  * x  = relu(BN1(y1)) rebuilt from y1 by the staging prologue (xc), y1 also the BN epilogue's input (the
+    kernel rebuilds y1 from the staged x tile),
+  * dY = bwd(dz2, y2) rebuilt from the deferred BN2 backward (bwd1 in csrc/common.h),
+for Go = 1 (3x3 at dilation 1 / 2 / 3, 1x7, 7x1) and Go = 2 (the ResidualBlock's 3x3 + 1x1 pair), padded
+widths 8 / 16 / 24 (17 real) / 32 channels, on grids of several tiles and blocks (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CASES = [
+    # n, h, w, ci, co, (kh, kw), dil, go
+    (3, 40, 56, 17, 17, (3, 3), 1, 1),
+    (2, 33, 70, 17, 17, (3, 3), 2, 1),
+    (2, 45, 38, 16, 16, (3, 3), 3, 1),
+    (2, 30, 66, 17, 17, (1, 7), 1, 1),
+    (2, 66, 30, 17, 17, (7, 1), 1, 1),
+    (2, 36, 52, 8, 8, (3, 3), 1, 1),
+    (2, 28, 44, 32, 32, (3, 3), 1, 1),
+    (3, 40, 56, 17, 17, (3, 3), 1, 2),
+    (2, 31, 47, 16, 16, (3, 3), 1, 2),
+]
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_fused_bwd_vs_fp32_conv_grads(gpu, case):
+    from medical_segmentation_pytorch_amd.ops._ext import require
+    from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, _taps
+    from medical_segmentation_pytorch_amd.ops.fm import cpad
+    C = require()
+    n, h, w, ci, co, (kh, kw), dil, go = case
+    g = torch.Generator(device=gpu).manual_seed(11)
+    T = kh * kw
+    pad = (dil * (kh // 2), dil * (kw // 2))
+    W0 = torch.randn(co, ci, kh, kw, device=gpu, generator=g) * 0.2
+    branches = [Branch(W0, 0, 0, T)]
+    ws = [W0]
+    if go == 2:   # the 1x1 shortcut at the centre tap (runtime.fused_model.plan_fused3x3)
+        W1 = torch.randn(co, ci, 1, 1, device=gpu, generator=g) * 0.2
+        branches.append(Branch(W1, 1, T // 2, 1))
+        ws.append(W1)
+    plan = ConvPlan(kh, kw, ci, co, branches, padding=pad, dilation=(dil, dil), Go=go)
+    cp, cq = cpad(ci), cpad(co)
+    dims = plan.fwd_dims(n, h, w, h, w)
+    tdy, tdx = _taps(plan.taps_fwd)
+    nblk = C.conv_bwd_fused_blocks(dims, tdy, tdx)
+    assert nblk > 1, 'the case must span several blocks'
+
+    def fm(t, c):   # NCHW fp32 -> NHWC bf16 padded to c channels
+        o = torch.zeros(t.shape[0], t.shape[2], t.shape[3], c, device=gpu, dtype=torch.bfloat16)
+        o[..., :t.shape[1]] = t.permute(0, 2, 3, 1).to(torch.bfloat16)
+        return o
+
+    def nchw(t, c):
+        return t[..., :c].permute(0, 3, 1, 2).float()
+
+    # BN1 (the conv's input BN): y1 -> x = relu(sc1 * y1 + sh1), its backward coefficients' mean row
+    y1 = fm(torch.randn(n, ci, h, w, device=gpu, generator=g), cp)
+    st1 = torch.zeros(4, cp, device=gpu)
+    st1[0, :ci] = torch.rand(ci, device=gpu, generator=g) + 0.5
+    st1[1, :ci] = torch.randn(ci, device=gpu, generator=g) * 0.3
+    st1[2, :ci] = torch.randn(ci, device=gpu, generator=g) * 0.2   # mean (BN epilogue centring)
+    x = _bf(torch.relu(nchw(y1, ci) * st1[0, :ci].view(1, -1, 1, 1) + st1[1, :ci].view(1, -1, 1, 1)))
+    # BN2 of each output group: dY = k1 * [sc2 * y2 + sh2 > 0] * dz2 + k2 * y2 + k3
+    dzs, y2s, st2s, k2s, dYs = [], [], [], [], []
+    for _ in range(go):
+        dz = fm(torch.randn(n, co, h, w, device=gpu, generator=g), cq)
+        y2 = fm(torch.randn(n, co, h, w, device=gpu, generator=g), cq)
+        st2 = torch.zeros(4, cq, device=gpu)
+        st2[0, :co] = torch.rand(co, device=gpu, generator=g) + 0.5
+        st2[1, :co] = torch.randn(co, device=gpu, generator=g) * 0.3
+        k = torch.zeros(3, cq, device=gpu)
+        k[0, :co] = torch.rand(co, device=gpu, generator=g) + 0.5
+        k[1, :co] = torch.randn(co, device=gpu, generator=g) * 0.1
+        k[2, :co] = torch.randn(co, device=gpu, generator=g) * 0.1
+        y2f, dzf = nchw(y2, co), nchw(dz, co)
+        v = lambda r: r[:co].view(1, -1, 1, 1)  # noqa: E731
+        mask = (y2f * v(st2[0]) + v(st2[1])) > 0
+        dYs.append(_bf(v(k[0]) * torch.where(mask, dzf, torch.zeros_like(dzf)) + v(k[1]) * y2f + v(k[2])))
+        dzs.append(dz); y2s.append(y2); st2s.append(st2); k2s.append(k)
+    # fp32 oracle: conv input / weight gradients on the bf16 operands
+    wb = [_bf(t) for t in ws]
+    dx_ref = F.grad.conv2d_input(x.shape, wb[0], dYs[0], padding=pad, dilation=dil)
+    dw_ref = [F.grad.conv2d_weight(x, wb[0].shape, dYs[0], padding=pad, dilation=dil)]
+    if go == 2:
+        dx_ref = dx_ref + F.grad.conv2d_input(x.shape, wb[1], dYs[1])
+        dw_ref.append(F.grad.conv2d_weight(x, wb[1].shape, dYs[1]))
+    # the kernel
+    wd, kp = plan.pack_dgrad(gpu)
+    dxt = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=gpu)
+    part = torch.empty(nblk, 2, cp, device=gpu)
+    dwp = torch.empty(nblk * plan.rows * plan.T * plan.Cip, device=gpu)
+    kw2 = {}
+    if go == 2:
+        kw2 = dict(dz2=dzs[1], gy2=y2s[1], gs2=st2s[1], gk2=k2s[1], grelu2=True, t1=T // 2)
+    C.conv_bwd_fused(dzs[0], y2s[0], st2s[0], k2s[0], True, y1, st1, True, wd, kp, dxt, y1, st1[:3].contiguous(), True,
+                     part, dwp, dims, tdy, tdx, **kw2)
+    torch.cuda.synchronize()
+    dx = nchw(dxt, ci)
+    assert torch.isfinite(dx).all()
+    assert _rel(dx, dx_ref) < 1e-2, _rel(dx, dx_ref)
+    if cp > ci:
+        assert dxt[..., ci:].float().abs().max().item() == 0.0   # padding channels stay zero
+    slab = dwp.view(nblk, plan.rows, plan.T, plan.Cip).sum(0)   # fixed-order split-K sum (as unpack_wgrad)
+    for gi, ref in enumerate(dw_ref):
+        got = slab[gi * cq:gi * cq + co, :, :ci]                   # [co][t][ci]
+        if gi == 0:
+            got = got.permute(0, 2, 1).reshape(co, ci, kh, kw)
+        else:
+            got = got[:, T // 2, :].reshape(co, ci, 1, 1)
+        assert _rel(got, ref) < 1e-2, (gi, _rel(got, ref))
+    # BN1 backward partials of the kernel's own (bf16) data-gradient: sum g, sum g * (y1 - mean)
+    y1f = nchw(y1, ci)
+    m1 = (y1f * st1[0, :ci].view(1, -1, 1, 1) + st1[1, :ci].view(1, -1, 1, 1)) > 0
+    gm = torch.where(m1, dx, torch.zeros_like(dx))
+    s_ref = gm.sum((0, 2, 3))
+    q_ref = (gm * (y1f - st1[2, :ci].view(1, -1, 1, 1))).sum((0, 2, 3))
+    p = part.sum(0)
+    assert _rel(p[0, :ci], s_ref) < 2e-3, _rel(p[0, :ci], s_ref)
+    assert _rel(p[1, :ci], q_ref) < 2e-2, _rel(p[1, :ci], q_ref)

@@ -110,3 +110,38 @@ def test_fused_training_converges_like_eager(gpu):
     print(f'macro Dice after {steps} steps: fused {d_fused:.4f}  eager {d_eager:.4f}')
     assert d_fused >= 0.8
     assert d_fused >= d_eager - 0.01
+
+
+def test_gradient_accumulation_graph_matches_eager_and_single_step(gpu):
+    """config.accum_steps on the fused engine: per-micro-step-kind hipGraphs (first / middle / last, one
+    shared pool) replay bitwise like the eager accumulation, and accumulating the SAME micro-batch twice
+    (loss / 2 each: exact halving) steps the weights exactly like one step on it."""
+    from medical_segmentation_pytorch_amd.runtime.bench_step import synthetic_batch
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep, make_model
+    torch.manual_seed(1)
+    base = make_model('ducknet', 17).to(gpu).train()
+    x, t = synthetic_batch(4, 64, gpu)
+    mk = lambda g, k: FusedStep(copy.deepcopy(base), x.clone(), t.clone(), lr=1e-3, use_graph=g,  # noqa: E731
+                                total_steps=50, accum_steps=k)
+    one, eager2, graph2 = mk(False, 1), mk(False, 2), mk(True, 2)
+    for it in range(3):   # graph2: eager warm-up (calls 1-2), capture (3: first, 4: last), replays (5-6)
+        one()
+        for _ in range(2):
+            eager2()
+            graph2()
+        torch.cuda.synchronize()
+        assert graph2.engine.stepped and eager2.engine.stepped
+        ps = [dict(s.model.named_parameters()) for s in (one, eager2, graph2)]
+        for n, p in ps[0].items():
+            assert torch.equal(ps[1][n], ps[2][n]), (it, n, 'graph != eager accumulation')
+            assert torch.equal(p, ps[1][n]), (it, n, 'accumulated != single step')
+    assert set(graph2.engine.graphs) == {(True, False), (False, True)}
+    # three micro-steps: the middle kind gets its own graph; replay == eager
+    eager3, graph3 = mk(False, 3), mk(True, 3)
+    for _ in range(9):
+        eager3()
+        graph3()
+    torch.cuda.synchronize()
+    assert set(graph3.engine.graphs) == {(True, False), (False, False), (False, True)}
+    for (n, p), q in zip(eager3.model.named_parameters(), graph3.model.parameters()):
+        assert torch.equal(p, q), n

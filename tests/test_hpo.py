@@ -88,3 +88,21 @@ def test_concurrent_trial_groups_gloo(tmp_path):
     assert out.returncode == 0, out.stderr[-3000:]
     res = json.load(open(tmp_path / 'save' / 'optuna_results.json'))
     assert res['finished_trials'] >= 2
+
+
+@pytest.mark.slow
+def test_two_concurrent_two_rank_trial_groups_gloo(tmp_path):
+    """World 4 split into two 2-rank trial groups (``--ranks-per-trial 2``): each group trains its trial with
+    DDP over its own sub-group, both write to the shared study (reference optuna_search.py over 4 GPUs)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS='1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=4',
+           '--master-addr', '127.0.0.1', '--master-port', str(30500 + os.getpid() % 1000),
+           os.path.join(ROOT, 'optuna_search.py'), '--ranks-per-trial', '2', '--storage',
+           f'sqlite:///{tmp_path}/c4.db', '--num-trial', '2', '--save_dir', str(tmp_path / 'save'), '--dataset',
+           'synthetic', '--synthetic_num', '8', '4', '4', '--synthetic_size', '64', '--crop_size', '64',
+           '--total_epoch', '1', '--warmup_epochs', '0', '--train_bs', '2', '--base_workers', '0', '--base_channel',
+           '8', '--no_progress_bar', '--data_root', str(tmp_path / 'data')]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.load(open(tmp_path / 'save' / 'optuna_results.json'))
+    assert res['finished_trials'] >= 2

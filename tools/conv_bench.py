@@ -106,7 +106,7 @@ def main():
         dims_d = [n, oh, ow, plan.Go, plan.Cgo, hw, hw, 1, plan.Cgi, ci, plan.T, Kp_d, s]
         bdy, bdx = [t[0] for t in plan.taps_bwd], [t[1] for t in plan.taps_bwd]
         t_d = timeit(lambda: C.conv_fwd(gys, wd, dxs, None, None, dims_d, bdy, bdx, s > 1), a.iters)
-        dwp = torch.empty(C.conv_wgrad_replicas(dims, dy, dx, False) * plan.rows * plan.T * plan.Cip, device=dev)
+        dwp = torch.empty(C.conv_wgrad_replicas(dims, dy, dx, False, False, bool(xc)) * plan.rows * plan.T * plan.Cip, device=dev)
         t_w = timeit(lambda: C.conv_wgrad(gys, [x], dwp, dims, dy, dx, False, xc, xr), a.iters)
         flops = 2.0 * n * oh * ow * co * ci * k[0] * k[1] * groups
         row = {'layer': name, 'fwd_ms': round(t_f, 4), 'dgrad_ms': round(t_d, 4), 'wgrad_ms': round(t_w, 4),
