@@ -38,6 +38,16 @@ DEVI f32x16_t mfma32(const uint4& a, const uint4& b, f32x16_t c) {
 #endif
 }
 
+// Output store.  (Round 5 tried global_store ... sc1 here, to keep the output stream out of the XCD's L2: the
+// L4 fused-8 forward and data-gradient got 5-25 % SLOWER and their L2 read misses rose, so plain stores.)
+DEVI void st_stream8(uint16_t* p, uint32_t lo, uint32_t hi) {
+#ifdef GK_KO_STORE   // (profiling knock-out: no output stores; a never-true test keeps the math alive)
+  if (lo == 0x7fc17fc1u && hi == 0x12345678u) *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+#else
+  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+#endif
+}
+
 // 64 zero bytes in global memory: the DMA source of every padding / out-of-range vector
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
@@ -80,6 +90,9 @@ DEVI void kpos_advance(KPos& p, int by, int Cgi, int Gi) {
 struct GemmGeom {
   long M, OHW;
   int n_co, nk;
+  int pxg;       // pixel tiles per block group (1: co tiles innermost), see the remap in conv_gemm_kernel
+  long n_px;     // pixel tiles
+  int krot;      // rotate each co tile's K start (see conv_gemm_kernel)
 };
 
 // BK = k per stage (64 or 32): one staged row (co or pixel) is BK bf16 = ROWB bytes, one DMA instruction
@@ -127,8 +140,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
-  const int co_t = wgid % gg.n_co;
-  const long px_t = wgid / gg.n_co;
+  // pxg > 1: consecutive blocks walk pxg pixel tiles per co tile, then the next co tile over the same pixel
+  // tiles -- fewer weight rows live in the XCD's L2 at a time (the blocks of one co tile share them)
+  int co_t;
+  long px_t;
+  if (gg.pxg <= 1) {
+    co_t = wgid % gg.n_co;
+    px_t = wgid / gg.n_co;
+  } else {
+    const long span = (long)gg.n_co * gg.pxg;
+    const long grp = wgid / span;
+    const int r = (int)(wgid - grp * span);
+    const int P = (int)min((long)gg.pxg, gg.n_px - grp * gg.pxg);
+    co_t = r / P;
+    px_t = grp * gg.pxg + (r - co_t * P);
+  }
   const int co0 = co_t * C::TCO;
   const long px0 = px_t * C::TPX;
   const int rows = g.Go * g.Cgo;
@@ -149,6 +175,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   for (int j = 0; j < C::A_INS; ++j) {
     const int co = co0 + RPI * (j * C::NW + wave) + lane / C::SLOTS;
     a_src[j] = a.w + (long)(co < rows ? co : 0) * g.Kp + 8 * ls;
+#ifdef GK_KO_AMISS   // (profiling knock-out: every A row reads row 0 -- L2-resident)
+    a_src[j] = a.w + 8 * ls;
+#endif
   }
   // B (im2col of the input): per instruction the pixel's input origin (element offset, taps excluded) and
   // a bitmask of the taps that land inside the image -- both fixed for the whole K walk.
@@ -165,6 +194,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
       const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
       const int ih0 = oh * g.stride, iw0 = ow * g.stride;
       b_pix[j] = ((long)n * IHW + (long)ih0 * g.IW + iw0) * Cgi;
+#ifdef GK_KO_BMISS   // (profiling knock-out: every pixel reads the tile's first rows -- L2-resident)
+      b_pix[j] = ((long)(ih0 % 4) * g.IW + (iw0 % 8)) * Cgi;
+#endif
       uint32_t vm = 0u;
       int tr = 0, tc = 0;
       for (int t = 0; t < g.T; ++t) {
@@ -179,8 +211,24 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   // element offset of tap t0 from the pixel origin.  Cgi >= 64 >= the stage width, so the slots of a row
   // cross at most one (group | tap) boundary: a lane at slot ls >= (Cgi - cl0) / 8 is in the next one.
   const long dcol = (long)tg.xs * Cgi, drow = ((long)tg.ys * g.IW - (long)tg.kw * tg.xs) * Cgi;
-  int t0 = 0, tr0 = 0, tc0 = 0, g0 = 0, cl0 = 0;
-  long toff0 = ((long)tg.y0 * g.IW + tg.x0) * Cgi;
+  // K rotation (A/B knob, off): co tile c starts its K walk at stage c * nk / n_co and wraps.  Hypothesis: the
+  // co tiles of one pixel tile, side by side on one XCD, miss the same im2col lines together (the L4 fused-8
+  // forward misses 32 % of its L2 reads at 7 co tiles vs 5 % at one, profiles/r05/pmc/tcc_L4_*).  Measured:
+  // no change in misses nor time (neighbouring taps read the same lines), so it stays off.
+  const int kstart = gg.krot ? (int)(((long)co_t * gg.nk) / gg.n_co) : 0;
+  int t0, tr0, tc0, g0, cl0;
+  long toff0;
+  auto walk_to = [&](int k) {   // uniform walk state at k (a multiple of BK)
+    const int Cip = Gi * Cgi;
+    t0 = k / Cip;
+    const int rem = k - t0 * Cip;
+    g0 = rem / Cgi;
+    cl0 = rem - g0 * Cgi;
+    tr0 = t0 / tg.kw;
+    tc0 = t0 - tr0 * tg.kw;
+    toff0 = ((long)(tg.y0 + tr0 * tg.ys) * g.IW + (tg.x0 + tc0 * tg.xs)) * Cgi;
+  };
+  walk_to(kstart * BK);
   auto gptr = [&](int q) {   // group pointer from the kernel arguments (scalars), no memory read
     const uint16_t* xb = a.x[0];
 #pragma unroll
@@ -189,7 +237,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   };
 
   auto stage = [&](int kt, uint32_t sb) {
-    const int kb = kt * BK;
+    int ks = kt + kstart;
+    if (ks >= gg.nk) ks -= gg.nk;
+    if (ks == 0 && kstart != 0) walk_to(0);   // the rotated walk wraps to k = 0
+    const int kb = ks * BK;
 #pragma unroll
     for (int j = 0; j < C::A_INS; ++j) glds16(a_src[j] + kb, sb + (RPI * (j * C::NW + wave)) * kRowB);
     // the (group | tap) after the current one
@@ -318,7 +369,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
           v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
         }
         const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(yp) = make_uint2(lo, hi);
+        st_stream8(yp, lo, hi);
         // statistics of the STORED (bf16-rounded) values, as a BN reading this tensor sees them
         const float w4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                              __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -413,8 +464,18 @@ constexpr int kGemmTPX = 128;   // stat partial rows = pixel tiles of 128 (a 256
 int g_gemm_mode = -1;     // env MSP_CONV_GEMM: 0 off, else on (default on)
 int g_gemm_min_c = -1;    // env MSP_CONV_GEMM_MINC: minimum input channels per group (default 64)
 int g_gemm_cfg = -2;      // env MSP_CONV_GEMM_CFG: force one configuration index (A/B), -1 = planner
+int g_gemm_pxg = -1;      // env MSP_GEMM_PXG: pixel tiles per block group (GemmGeom::pxg; A/B)
+int g_gemm_krot = -1;     // env MSP_GEMM_KROT=1: K rotation (A/B, measured neutral)
 
 void gemm_env() {
+  if (g_gemm_krot < 0) {
+    const char* e = getenv("MSP_GEMM_KROT");
+    g_gemm_krot = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  if (g_gemm_pxg < 0) {
+    const char* e = getenv("MSP_GEMM_PXG");
+    g_gemm_pxg = (e != nullptr && atoi(e) > 0) ? atoi(e) : 1;
+  }
   if (g_gemm_mode < 0) {
     const char* e = getenv("MSP_CONV_GEMM");
     g_gemm_mode = (e == nullptr || e[0] != '0') ? 1 : 0;
@@ -467,6 +528,9 @@ void launch_gemm(const ConvArgs& a, hipStream_t s) {
   gg.OHW = (long)g.OH * g.OW;
   gg.M = (long)g.N * gg.OHW;
   gg.n_co = cdiv(g.Go * g.Cgo, C::TCO);
+  gg.n_px = cdiv(gg.M, C::TPX);
+  gg.pxg = g_gemm_pxg;
+  gg.krot = g_gemm_krot;
   gg.nk = cdiv(g.Kp, BK);
   const long blocks = (long)cdiv(gg.M, C::TPX) * gg.n_co;
   static bool attr = false;
@@ -519,6 +583,7 @@ int conv_gemm_num_cfgs() { return kNumCfgs; }
 long conv_gemm_stat_blocks(const ConvGeom& g) { return cdiv((long)g.N * g.OH * g.OW, kGemmTPX); }
 
 int conv_gemm(const ConvArgs& a, hipStream_t s) {
+  gemm_env();
   for (int i = 0; i < a.g.Gi; ++i)
     if (a.xc[i] != nullptr) return 2;   // no prologue on this path (see conv_gemm_ok)
   const int cfg = gemm_pick_cfg(a.g.Go * a.g.Cgo);
