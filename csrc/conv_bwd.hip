@@ -30,11 +30,12 @@ namespace {
 constexpr int kFbWaves = 4;       // compute waves: data- then weight-gradient of tile i
 constexpr int kFbProd = 4;        // staging waves: tile i + 1 into the other LDS buffer meanwhile
 constexpr int kFbThreads = 64 * (kFbWaves + kFbProd);
-#ifndef FB_LD_BNE
-#define FB_LD_BNE 8   // (12 / 16 spill: 4.37 / 4.70 ms vs 3.47 ms, tools/dev/fused_bwd_bench.py)
+#ifndef FB_LDY
+#define FB_LDY 4   // dY vectors (two loads each) per staging thread and batch; two batches in flight
 #endif
-constexpr int kFbLd = 16;         // staging vectors in flight per thread (the data-gradient accumulators are
-                                  // dead while staging: only the weight-gradient ones stay live)
+#ifndef FB_LDX
+#define FB_LDX 4   // x vectors per staging thread and batch
+#endif
 constexpr int kFbMaxKS = 24;      // data-gradient k-steps (T <= 9 taps x <= 4 slots / 4)
 constexpr int kFbMaxT = 9;
 constexpr int kFbMaxLds = 156 * 1024;  // two dY + x buffer pairs, the data-gradient weights, the BN partials
@@ -162,6 +163,137 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     for (int c = tid; c < kFbWaves * 2 * 32; c += kFbThreads) s_stat[c] = 0.f;
   __syncthreads();
 
+  const int per_img = fg.tiles_y * fg.tiles_x;
+  const long img_px = (long)a.H * a.W;
+  auto tile_origin = [&](int tt, int& ty0, int& tx0, long& imoff) {
+    const int n = tt / per_img, trem = tt - n * per_img;
+    const int tyi = trem / fg.tiles_x;
+    ty0 = tyi * fg.TH;
+    tx0 = (trem - tyi * fg.tiles_x) * fg.TW;
+    imoff = (long)n * img_px;
+  };
+  const bool producer = wave >= kFbWaves;   // wave-uniform role
+  if (producer) {
+    // ---- staging waves: a continuous software pipeline of load batches over this block's tiles ------------
+    // Tile k (= blockIdx.x + k * gridDim.x) goes to LDS buffer pair k & 1.  Each batch is LDY dY vectors
+    // (dz2 + y2: dY = bwd(dz2, y2), bwd8) and LDX x vectors (y1: x = relu(BN1(y1))) per thread, every load
+    // issued unconditionally (out-of-image / past-the-end entries load a valid pixel and store zero / nothing),
+    // so the compiler's counted vmcnt waits retire exactly the batch being written: batch q + 1 (possibly the
+    // next tile's first) is in flight while batch q is transformed into LDS, and across the tile barrier.
+    // (Round 4 staged one tile at a time with every batch's latency exposed: ~2.2 TB/s.)
+    const int st = tid - 64 * kFbWaves;
+    constexpr int NP = 64 * kFbProd;
+    constexpr int LDY = FB_LDY, LDX = FB_LDX;
+    const int totY = hpx * C8y, totX = hpx * C8x;
+    const int NB = max((totY + NP * LDY - 1) / (NP * LDY), (totX + NP * LDX - 1) / (NP * LDX));
+    const int ntb = (fg.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // grid <= ntiles
+    const int Q = ntb * NB;
+    struct Batch {
+      uint4 v[LDY], w[LDY], x[LDX];
+      int dy[LDY], dx[LDX];   // LDS element offset << 5 | 8-channel slot << 2 | in-image << 1 | rebuild;
+                              // -1: nothing to store
+      int buf;
+    };
+    auto issue = [&](int k, int b, Batch& B) {
+      int ty0, tx0;
+      long imoff;
+      tile_origin((int)blockIdx.x + min(k, ntb - 1) * (int)gridDim.x, ty0, tx0, imoff);
+      B.buf = k & 1;
+#pragma unroll
+      for (int u = 0; u < LDY; ++u) {
+        const int idx = b * NP * LDY + u * NP + st;
+        const bool valid = idx < totY;
+        const int e = valid ? idx : 0;
+        const int hp = fdiv(e, C8y, fg.inv_c8y), c8 = e - hp * C8y;
+        const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
+        const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
+        const bool in = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        const long pix = imoff + (in ? (long)iy * a.W + ix : 0);
+        const bool g2 = GO2 && c8 >= C8g;   // (a select of two kernarg pointers, not an indexed load)
+        const int cl = 8 * (c8 - (g2 ? C8g : 0));
+        const uint16_t* dzp = (g2 ? a.dz2 : a.dz) + pix * Co + cl;
+        const uint16_t* yp = g2 ? a.gy2 : a.gy;
+        const bool tr = BWD && (!GO2 || yp != nullptr);   // else a plain gradient group: stored as loaded
+#ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
+        B.v[u] = fb_ldg4(dzp);
+        if (BWD) B.w[u] = fb_ldg4(tr ? yp + pix * Co + cl : dzp);
+#else
+        B.v[u] = make_uint4(0, 0, 0, 0);
+        B.w[u] = make_uint4(0, 0, 0, 0);
+#endif
+        B.dy[u] = valid ? ((hp * fg.py + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0) | (tr ? 1 : 0)) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < LDX; ++u) {
+        const int idx = b * NP * LDX + u * NP + st;
+        const bool valid = idx < totX;
+        const int e = valid ? idx : 0;
+        const int hp = fdiv(e, C8x, fg.inv_c8x), c8 = e - hp * C8x;
+        const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
+        const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
+        const bool in = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        const long pix = imoff + (in ? (long)iy * a.W + ix : 0);
+#ifndef FB_KO_LOADS
+        B.x[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
+#else
+        B.x[u] = make_uint4(0, 0, 0, 0);
+#endif
+        B.dx[u] = valid ? ((hp * fg.px + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0)) : -1;
+      }
+    };
+    auto commit = [&](const Batch& B) {
+      uint16_t* const tY = lds0 + B.buf * pair;
+      uint16_t* const tX = tY + hpx * fg.py + kFbSlack;
+#pragma unroll
+      for (int u = 0; u < LDY; ++u) {
+        const int d = B.dy[u];
+        if (d < 0) continue;
+        uint4 val = B.v[u];
+        if (BWD && (d & 1)) val = bwd8(val, B.w[u], s_bt + 8 * ((d >> 2) & 7), 64);
+        if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(tY + (d >> 5)) = val;
+      }
+#pragma unroll
+      for (int u = 0; u < LDX; ++u) {
+        const int d = B.dx[u];
+        if (d < 0) continue;
+        uint4 val = B.x[u];
+        if (XPRO) {
+          const int cc = 8 * ((d >> 2) & 7);
+          float f[8];
+          unpack8(val, f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], s_xt[cc + k], s_xt[32 + cc + k]), s_xt[64 + cc + k]);
+          val = pack8(f);
+        }
+        if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(tX + (d >> 5)) = val;
+      }
+    };
+    Batch B0, B1;
+    int k0 = 0, b0 = 0;   // batch q's tile / batch within the tile
+    auto next = [&](int& k, int& b) { if (++b == NB) { b = 0; ++k; } };
+    // (issues are unconditional -- past the end a clamped batch that is never committed -- so that every
+    // commit's vmcnt wait is the exact count of the one batch issued after it)
+    issue(0, 0, B0);
+    for (int q = 0; q < Q; q += 2) {
+      int k1 = k0, b1 = b0;
+      next(k1, b1);
+      issue(k1, b1, B1);
+      commit(B0);
+      if (b0 == NB - 1) __syncthreads();   // tile k0 staged
+      if (q + 1 >= Q) break;
+      int k2 = k1, b2 = b1;
+      next(k2, b2);
+      issue(k2, b2, B0);
+      commit(B1);
+      if (b1 == NB - 1) __syncthreads();
+      k0 = k2; b0 = b2;
+    }
+    __syncthreads();   // the compute waves' last tile
+    if (BNE) __syncthreads();   // (the BN1 partials' exchange below)
+    return;
+  }
   // data-gradient: the wave's NJ 16-pixel columns -> dY tile pixel offsets
   int pb[NJ];
 #pragma unroll
@@ -188,99 +320,10 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
 #pragma unroll
     for (int r = 0; r < 4; ++r) { cs[i][r] = 0.f; cq[i][r] = 0.f; }
 
-  const int per_img = fg.tiles_y * fg.tiles_x;
-  const long img_px = (long)a.H * a.W;
-  auto tile_origin = [&](int tt, int& ty0, int& tx0, long& imoff) {
-    const int n = tt / per_img, trem = tt - n * per_img;
-    const int tyi = trem / fg.tiles_x;
-    ty0 = tyi * fg.TH;
-    tx0 = (trem - tyi * fg.tiles_x) * fg.TW;
-    imoff = (long)n * img_px;
-  };
-  // staging of one tile by the staging waves (thread st of 64 * kFbProd) into the buffer pair tY / tX
-  auto stage = [&](int tt, uint16_t* tY, uint16_t* tX, int st) {
-    int ty0, tx0;
-    long imoff;
-    tile_origin(tt, ty0, tx0, imoff);
-    // staging: dY = bwd(dz, y2) and x = prologue(y1), zero outside the image -------------------------
-    {
-      const int totY = hpx * C8y, totX = hpx * C8x, tot = totY + totX;
-      constexpr int LD = BWD ? (BNE ? FB_LD_BNE : 10) : kFbLd;   // two loads per dY vector when rebuilding it
-      for (int base = st; base < tot; base += 64 * kFbProd * LD) {
-        uint4 v[LD], w[LD];
-        int dst[LD], cc[LD];
-#pragma unroll
-        for (int u = 0; u < LD; ++u) {
-          const int idx = base + u * 64 * kFbProd;
-          v[u] = make_uint4(0, 0, 0, 0);
-          w[u] = make_uint4(0, 0, 0, 0);
-          dst[u] = -1;
-          cc[u] = -1;
-          if (idx < tot) {
-            const bool isy = idx < totY;
-            const int e = isy ? idx : idx - totY;
-            const int C8 = isy ? C8y : C8x;
-            const int hp = fdiv(e, C8, isy ? fg.inv_c8y : fg.inv_c8x), c8 = e - hp * C8;
-            const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
-            const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
-            dst[u] = isy ? hp * fg.py + 8 * c8 : -2 - (hp * fg.px + 8 * c8);   // <= -2: an x-tile slot
-            if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
-              const long pix = imoff + iy * a.W + ix;
-              cc[u] = 8 * c8;
-#ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
-              if (isy) {
-                const bool g2 = GO2 && c8 >= C8g;   // (a select of two kernarg pointers, not an indexed load)
-                const int cl = 8 * (c8 - (g2 ? C8g : 0));
-                v[u] = fb_ldg4((g2 ? a.dz2 : a.dz) + pix * Co + cl);
-                if (BWD) {
-                  const uint16_t* yp = g2 ? a.gy2 : a.gy;
-                  if (!GO2 || yp != nullptr) w[u] = fb_ldg4(yp + pix * Co + cl);
-                  else cc[u] = -1;   // a plain gradient group: stored as loaded
-                }
-              } else {
-                v[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
-              }
-#endif
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < LD; ++u) {
-          if (dst[u] == -1) continue;
-          uint4 val = v[u];
-          if (dst[u] >= 0) {
-            if (BWD && cc[u] >= 0) val = bwd8(val, w[u], s_bt + cc[u], 64);
-            *reinterpret_cast<uint4*>(tY + dst[u]) = val;
-          } else {
-            if (XPRO && cc[u] >= 0) {
-              float f[8];
-              unpack8(val, f);
-#pragma unroll
-              for (int k = 0; k < 8; ++k)
-                f[k] = fmaxf(fmaf(f[k], s_xt[cc[u] + k], s_xt[32 + cc[u] + k]), s_xt[64 + cc[u] + k]);
-              val = pack8(f);
-            }
-            *reinterpret_cast<uint4*>(tX + (-2 - dst[u])) = val;
-          }
-        }
-      }
-    }
-  };
-
-  const bool producer = wave >= kFbWaves;   // wave-uniform role
-  if (producer && (int)blockIdx.x < fg.ntiles) stage(blockIdx.x, lds0, lds0 + hpx * fg.py + kFbSlack, tid - 64 * kFbWaves);
-  __syncthreads();
+  __syncthreads();   // tile 0 staged
   int it = 0;
   for (int tt = blockIdx.x; tt < fg.ntiles; tt += gridDim.x, ++it) {
     uint16_t* const cur = lds0 + (it & 1) * pair;
-    if (producer) {
-      // tile i + 1 into the other pair (read by the compute waves during tile i - 1: released by the barrier)
-      const int nt = tt + gridDim.x;
-      uint16_t* const nxt = lds0 + ((it + 1) & 1) * pair;
-      if (nt < fg.ntiles) stage(nt, nxt, nxt + hpx * fg.py + kFbSlack, tid - 64 * kFbWaves);
-      __syncthreads();
-      continue;
-    }
     int ty0, tx0;
     long imoff;
     tile_origin(tt, ty0, tx0, imoff);
@@ -434,14 +477,14 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float s2 = row16_sum(cs[i][r]), q2 = row16_sum(cq[i][r]);
-        if (!producer && lr == 0 && cb + r < Ci) {
+        if (lr == 0 && cb + r < Ci) {
           s_stat[(wave * 2 + 0) * 32 + cb + r] = s2;
           s_stat[(wave * 2 + 1) * 32 + cb + r] = q2;
         }
       }
     }
     __syncthreads();
-    for (int c = tid; c < Ci; c += kFbThreads) {
+    for (int c = tid; c < Ci; c += 64 * kFbWaves) {   // (compute waves only: the staging waves have left)
       float s2 = 0.f, q2 = 0.f;
 #pragma unroll
       for (int wv = 0; wv < kFbWaves; ++wv) { s2 += s_stat[(wv * 2 + 0) * 32 + c]; q2 += s_stat[(wv * 2 + 1) * 32 + c]; }
@@ -450,7 +493,6 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     }
   }
   // ---- dW slab of this block: [Go*Co][T * Ci], element (g*Co + co, t*Ci + ci) ----------------------------
-  if (producer) return;
   float* slab = a.dw + (long)blockIdx.x * (Go * Co) * (T * Ci);
 #pragma unroll
   for (int m = 0; m < NT; ++m) {

@@ -456,6 +456,8 @@ constexpr CfgId kCfgs[] = {
     {2, 2, 3, 2, 4, 32},   // 192 x 128, 4 stages (80 KB)
     {2, 2, 4, 2, 3, 32},   // 256 x 128, 3 stages (72 KB)
     {2, 2, 2, 2, 5, 32},   // 128 x 128, 5 stages (80 KB)
+    {2, 4, 2, 2, 3, 64},   // 128 x 256, 8 waves, 3 stages (144 KB, one block per CU)
+    {1, 8, 4, 1, 3, 64},   // 128 x 256, 8 waves along pixels, 3 stages (144 KB)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 constexpr int kPlannerCfgs = 5;   // the planner's candidates (the rest: MSP_CONV_GEMM_CFG A/B only)
@@ -557,6 +559,8 @@ int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
     case 6: launch_gemm<2, 2, 3, 2, 4, 32, BNE>(a, s); return 0;
     case 7: launch_gemm<2, 2, 4, 2, 3, 32, BNE>(a, s); return 0;
     case 8: launch_gemm<2, 2, 2, 2, 5, 32, BNE>(a, s); return 0;
+    case 9: launch_gemm<2, 4, 2, 2, 3, 64, BNE>(a, s); return 0;
+    case 10: launch_gemm<1, 8, 4, 1, 3, 64, BNE>(a, s); return 0;
   }
   return 1;
 }

@@ -322,6 +322,7 @@ constexpr int kNumWgCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 int g_wg_mode = -1;   // env MSP_WGRAD_GEMM: 0 off (the conv.hip kernels), 1 auto (default), 2 every eligible conv
 int g_wg_cfg = -2;    // env MSP_WGRAD_GEMM_CFG: force a configuration (A/B); -1 planner
 long g_wg_blocks = -1;   // env MSP_WGRAD_GEMM_BLOCKS: grid size target (default 1024 = 2 blocks x 2 waves/CU x 256)
+double g_wg_stage_cost = -1;   // env MSP_WGRAD_STAGE_COST: planner's per-row staging cost (MAC units), see wg_pick
 
 void wg_env() {
   if (g_wg_mode < 0) {
@@ -336,6 +337,10 @@ void wg_env() {
     const char* e = getenv("MSP_WGRAD_GEMM_BLOCKS");
     g_wg_blocks = (e != nullptr && atol(e) > 0) ? atol(e) : 1024;
   }
+  if (g_wg_stage_cost < 0) {
+    const char* e = getenv("MSP_WGRAD_STAGE_COST");
+    g_wg_stage_cost = (e != nullptr && atof(e) >= 0) ? atof(e) : 24.0;
+  }
 }
 
 int wg_pick(int rows, int KT, bool pro) {
@@ -347,7 +352,7 @@ int wg_pick(int rows, int KT, bool pro) {
     const int tco = 32 * kWgCfgs[c].wm * kWgCfgs[c].fm, tk = 32 * kWgCfgs[c].wn * kWgCfgs[c].fn;
     const double nt = (double)cdiv(rows, tco) * cdiv(KT, tk);
     // padded MFMA work + operand staging per tile (in MAC units of one 64-pixel stage)
-    const double cost = nt * ((double)tco * tk + 24.0 * (tco + tk));
+    const double cost = nt * ((double)tco * tk + g_wg_stage_cost * (tco + tk));
     if (cost < best_cost) { best_cost = cost; best = c; }
   }
   return best;

@@ -55,6 +55,7 @@ def summarise(hist, target):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=320)
+    ap.add_argument('--accum', type=int, default=1, help='gradient accumulation micro-batches (config.accum_steps)')
     ap.add_argument('--epochs', type=int, default=300)
     ap.add_argument('--val-every', type=int, default=10)
     ap.add_argument('--size', type=int, default=352)
@@ -77,7 +78,7 @@ def main():
            '--base_channel', str(a.base_channel), '--crop_size', str(a.size), '--synthetic_size', str(a.size),
            '--synthetic_num', str(a.train_images), str(a.val_images), str(a.val_images), '--train_bs', str(a.batch),
            '--total_epoch', str(a.epochs), '--val_interval', str(a.val_every), '--begin_val_epoch', str(a.begin_val),
-           '--lr_scale', a.lr_scale,
+           '--lr_scale', a.lr_scale, '--accum_steps', str(a.accum),
            '--val_bs', '16', '--save_dir', save, '--base_lr', str(a.base_lr), '--use_tb', '--load_ckpt',
            '--no_progress_bar', '--log_interval', '1000'] + (['--val_fp32'] if a.val_fp32 else []) + a.extra
     print('[acc]', ' '.join(cmd), file=sys.stderr, flush=True)
@@ -86,7 +87,7 @@ def main():
     if r.returncode != 0:
         sys.exit(r.returncode)
     out = {'entry': 'python main.py (SegTrainer.run -> val_best on best.pth)', 'model': f'{a.model}-{a.base_channel}',
-           'batch': a.batch, 'epochs': a.epochs, 'size': a.size, 'train_images': a.train_images,
+           'batch': a.batch, 'accum_steps': a.accum, 'global_batch': a.batch * a.accum, 'epochs': a.epochs, 'size': a.size, 'train_images': a.train_images,
            'val_images': a.val_images, 'lr_scale': a.lr_scale,
            'adam_lr': json.load(open(os.path.join(save, 'config.json'))).get('lr', 0.1 * a.base_lr),
            'val_fp32': a.val_fp32,

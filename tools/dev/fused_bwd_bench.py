@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dev: time one conv_bwd_fused launch (csrc/conv_bwd.hip) at the DUCKNet-17 L1 chain-conv shape (17 -> 24
 padded channels, 3x3, deferred dY + x prologue + BN epilogue: the <8, true, true, true> instantiation).
-python tools/dev/fused_bwd_bench.py [batch] [size] [dilation]   (MSP_C_SO=<variant .so> for knock-out builds)"""
+python tools/dev/fused_bwd_bench.py [batch] [size] [dilation] [go]  (go = 2: the ResidualBlock's 3x3 + 1x1 pair)   (MSP_C_SO=<variant .so> for knock-out builds)"""
 import os
 import sys
 
@@ -17,11 +17,15 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 320
     s = int(sys.argv[2]) if len(sys.argv) > 2 else 352
     dil = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    go = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     C = require()
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     m = nn.Conv2d(17, 17, 3, 1, dil, dil, bias=False).to(dev)
-    plan = ConvPlan(3, 3, 17, 17, [Branch(m.weight, 0, 0, 9)], padding=(dil, dil), dilation=(dil, dil))
+    branches = [Branch(m.weight, 0, 0, 9)]
+    if go == 2:
+        branches.append(Branch(nn.Conv2d(17, 17, 1, bias=False).to(dev).weight, 1, 4, 1))
+    plan = ConvPlan(3, 3, 17, 17, branches, padding=(dil, dil), dilation=(dil, dil), Go=go)
     cp = plan.Cgi
     dims = plan.fwd_dims(n, s, s, s, s)
     tdy, tdx = _taps(plan.taps_fwd)
@@ -38,8 +42,11 @@ def main():
     part = torch.empty(nblk, 2, cp, device=dev)
     dwp = torch.empty(nblk * plan.rows * plan.T * plan.Cip, device=dev)
 
+    kw2 = dict(dz2=t(cp), gy2=t(cp), gs2=st, gk2=coef, grelu2=True, t1=4) if go == 2 else {}
+
     def run():
-        C.conv_bwd_fused(dz, y2, st, coef, True, x, st, True, wd, kp, dxt, y1, coef, True, part, dwp, dims, tdy, tdx)
+        C.conv_bwd_fused(dz, y2, st, coef, True, x, st, True, wd, kp, dxt, y1, coef, True, part, dwp, dims, tdy, tdx,
+                         **kw2)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -52,8 +59,8 @@ def main():
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
     px = n * s * s
-    hbm = px * cp * 2 * (4 + 1) * 1.2   # dz, y2, x, y1 (+ halo) read, dx written
-    print(f'conv_bwd_fused N={n} {s}x{s} d={dil} blocks={nblk}: {ms:.3f} ms  (~{hbm / ms / 1e9:.2f} TB/s of '
+    hbm = px * cp * 2 * (4 + 1 + 2 * (go - 1)) * 1.2   # dz, y2 (per group), x, y1 (+ halo) read, dx written
+    print(f'conv_bwd_fused N={n} {s}x{s} d={dil} go={go} blocks={nblk}: {ms:.3f} ms  (~{hbm / ms / 1e9:.2f} TB/s of '
           f'{hbm / 1e9:.2f} GB)  variant={os.environ.get("MSP_C_SO", "default")}')
 
 
