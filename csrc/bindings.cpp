@@ -135,7 +135,7 @@ void conv_fwd_bn(std::vector<at::Tensor> xs, const at::Tensor& wp, std::vector<a
   const bool bwd = fill_bwd(gy, gs, gk, g.Gi, (int64_t)g.N * g.IH * g.IW * g.Cgi, g.Cgi, a.gy, a.gs, a.gk);
   a.grelu = (unsigned)grelu;
   CHECK_F32(stat_part);
-  TORCH_CHECK(stat_part.numel() == conv_stat_blocks(g, false, bwd) * 2 * g.Cgo, "stat_part numel mismatch");
+  TORCH_CHECK(stat_part.numel() == conv_stat_blocks(g, false, bwd, true) * 2 * g.Cgo, "stat_part numel mismatch");
   CHECK_BF16(bn_y);
   TORCH_CHECK(bn_y.numel() == ys[0].numel(), "bn_y must have the data-gradient's shape");
   CHECK_F32(bn_coef);
@@ -190,8 +190,8 @@ bool conv_wgrad_uses_halo_t(std::vector<int64_t> dims, std::vector<int64_t> dy, 
 }
 
 int64_t conv_stat_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx, bool trans,
-                           bool bwd) {
-  return conv_stat_blocks(make_geom(dims, dy, dx), trans, bwd);
+                           bool bwd, bool bne) {
+  return conv_stat_blocks(make_geom(dims, dy, dx), trans, bwd, bne);
 }
 
 void pack_weight_t(const at::Tensor& src, const at::Tensor& dst, int64_t nrow, int64_t nch, int64_t T, int64_t Cpk,
@@ -991,7 +991,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_pick_mi", &conv_pick_mi);
   m.def("conv_rows_alloc", &conv_rows_alloc);
   m.def("conv_stat_blocks", &conv_stat_blocks_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans") = false,
-        py::arg("bwd") = false);
+        py::arg("bwd") = false, py::arg("bne") = false);
   m.def("conv_uses_halo", &conv_uses_halo_t, py::arg("dims"), py::arg("dy"), py::arg("dx"), py::arg("trans"),
         py::arg("bwd") = false);
   m.def("conv_set_halo", [](bool on) { conv_set_halo(on ? 1 : 0); });
@@ -1095,6 +1095,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_wgrad", &dwconv_wgrad_t);
   m.def("colsum", &colsum_t);
   m.def("conv_bwd_fused_blocks", &conv_bwd_fused_blocks_t);
+  m.def("conv_set_fwd_fused", [](bool on) { conv_set_fwd_fused(on ? 1 : 0); });
+  m.def("conv_fwd_fused_ok", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
+    return conv_fwd_fused_ok(make_geom(dims, dy, dx));
+  });
   m.def("conv_bwd_fused", &conv_bwd_fused_t, py::arg("dz"), py::arg("gy"), py::arg("gs"), py::arg("gk"),
         py::arg("grelu"), py::arg("x"), py::arg("xc"), py::arg("xrelu"), py::arg("wd"), py::arg("Kp_d"), py::arg("dxo"),
         py::arg("bn_y"), py::arg("bn_coef"), py::arg("bn_relu"), py::arg("stat_part"), py::arg("dw"), py::arg("dims"),

@@ -1705,9 +1705,10 @@ static long halo_blocks(const ConvGeom& g, const HaloGeom& hg) {
 // takes: ``trans`` (a strided transposed conv, conv_igemm's flag) never takes the GEMM or halo kernel --
 // sizing its rows by conv_gemm_ok(g, false) under-allocated the gather kernel's rows (out-of-bounds stat
 // writes: UNet / Linknet deconvs from 64 input channels up)
-long conv_stat_blocks(const ConvGeom& g, bool trans, bool bwd) {
+long conv_stat_blocks(const ConvGeom& g, bool trans, bool bwd, bool bne) {
   HaloGeom hg;
   if (!trans && conv_gemm_ok(g, false)) return conv_gemm_stat_blocks(g);
+  if (!trans && !bwd && !bne && conv_fwd_fused_ok(g)) return conv_fwd_fused_blocks(g);
   if (!trans && halo_enabled() && conv_halo_ok(g, false, hg, bwd)) return halo_blocks(g, hg);
   const int mi = conv_pick_mi(g.Go * g.Cgo);
   const int nj = conv_pick_nj(g, mi);
@@ -1765,6 +1766,9 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   for (int i = 0; i < a.g.Gi; ++i) bwd |= a.gy[i] != nullptr;
   if (bwd && (trans || conv_gemm_ok(a.g, trans))) return 7;
   if (conv_gemm_ok(a.g, trans)) return conv_gemm(a, s);
+  // the 17-channel level's forward convs: persistent staging / compute-wave kernel (conv_bwd.hip)
+  if (!trans && !bwd && a.bn_y == nullptr && !a.accum && a.g.Gi == 1 && a.g.Go == 1 && conv_fwd_fused_ok(a.g))
+    return conv_fwd_fused(a, s);
   HaloGeom hg;
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg, bwd)) {
     const unsigned blocks = (unsigned)halo_blocks(a.g, hg);
@@ -2092,7 +2096,10 @@ int conv_plan_selfcheck(int verbose) {
                 if (cdiv(rows, 16 * hg.mi) * 16 * hg.mi > conv_rows_alloc(rows)) fail("weight rows under-allocated", g);
                 const long blocks = halo_blocks(g, hg);
                 if (blocks < 1 || blocks > (1L << 31) - 1) fail("halo grid size", g);
-                if (!conv_gemm_ok(g, false) && blocks != conv_stat_blocks(g)) fail("stat partial rows != launch grid", g);
+                if (!conv_gemm_ok(g, false) && blocks != conv_stat_blocks(g, false, false, true))
+                  fail("stat partial rows != launch grid", g);
+                if (conv_fwd_fused_ok(g) && conv_stat_blocks(g) != conv_fwd_fused_blocks(g))
+                  fail("fused forward stat rows != its grid", g);
               }
               if (cdiv(rows, 16 * conv_pick_mi(rows)) * 16 * conv_pick_mi(rows) > conv_rows_alloc(rows))
                 fail("igemm weight rows under-allocated", g);

@@ -27,9 +27,14 @@
 
 namespace {
 
-constexpr int kFbWaves = 4;       // compute waves: data- then weight-gradient of tile i
 constexpr int kFbProd = 4;        // staging waves: tile i + 1 into the other LDS buffer meanwhile
-constexpr int kFbThreads = 64 * (kFbWaves + kFbProd);
+// Compute waves CW (template): data- then weight-gradient of tile i.  CW = 8 (round 5): two per SIMD beside
+// the staging wave -- the single compute wave per SIMD of the CW = 4 layout exposed its LDS / MFMA
+// latencies (with every global load knocked out the kernel still took 3.04 of 3.15 ms at the L1 3x3,
+// tools/dev/fused_bwd_bench.py).  At 768 threads the register cap is 168 per wave, so each wave keeps half
+// the data-gradient columns and at most 2 weight-gradient (group, tap) units (wave, wave + 8).  CW = 4 stays
+// for the 256-pixel tiles (dilation 3) and the Go = 2 pair, where it measured faster (conv_bwd_fused_plan).
+constexpr int fb_threads(int cw) { return 64 * (cw + kFbProd); }
 #ifndef FB_LDY
 #define FB_LDY 4   // dY vectors (two loads each) per staging thread and batch; two batches in flight
 #endif
@@ -54,11 +59,12 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false>
-__global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
+template <int CW, int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false, bool FWD = false>
+__global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
+  constexpr int kFbWaves = CW, kFbThreads = fb_threads(CW), kFbTapGroups = CW;
   extern __shared__ uint4 fb_smem[];
   constexpr int MI = 2;                       // 32 data-gradient rows (input channels <= 32)
-  constexpr int NT = 3;                       // weight-gradient taps per wave (T <= 9 = 3 x 4 waves)
+  constexpr int NT = (kFbMaxT + 1 + kFbTapGroups - 1) / kFbTapGroups;   // weight-gradient units per wave
   constexpr int TP = kFbWaves * NJ * 16;      // pixels per tile
   constexpr int NCH = TP / 32;                // weight-gradient k chunks per tile
   const int hpx = fg.HH * fg.HWD;
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
+  const int wt = wave;   // compute waves: weight-gradient units wt, wt + CW
   const int Ci = a.Ci, Co = a.Co, T = a.T;
   constexpr int Go = GO2 ? 2 : 1;
   const int C8g = Co >> 3, C8y = Go * C8g, C8x = Ci >> 3;   // dY: Go groups of Co channels, stacked
@@ -97,10 +104,11 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     }
   }
   if constexpr (XPRO) {
+    const int Cx = FWD ? Co : Ci;   // FWD: the prologue applies to the staged input (Co slots)
     for (int c = tid; c < 32; c += kFbThreads) {
-      const bool on = c < Ci;
+      const bool on = c < Cx;
       s_xt[c] = on ? a.xc[c] : 0.f;
-      s_xt[32 + c] = on ? a.xc[Ci + c] : 0.f;
+      s_xt[32 + c] = on ? a.xc[Cx + c] : 0.f;
       s_xt[64 + c] = a.xrelu ? 0.f : -INFINITY;
     }
   }
@@ -184,7 +192,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     const int st = tid - 64 * kFbWaves;
     constexpr int NP = 64 * kFbProd;
     constexpr int LDY = FB_LDY, LDX = FB_LDX;
-    const int totY = hpx * C8y, totX = hpx * C8x;
+    const int totY = hpx * C8y, totX = FWD ? 0 : hpx * C8x;   // FWD: x is staged as the "dY" tile
     const int NB = max((totY + NP * LDY - 1) / (NP * LDY), (totX + NP * LDX - 1) / (NP * LDX));
     const int ntb = (fg.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // grid <= ntiles
     const int Q = ntb * NB;
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
         B.dy[u] = valid ? ((hp * fg.py + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0) | (tr ? 1 : 0)) : -1;
       }
 #pragma unroll
-      for (int u = 0; u < LDX; ++u) {
+      for (int u = 0; u < (FWD ? 0 : LDX); ++u) {
         const int idx = b * NP * LDX + u * NP + st;
         const bool valid = idx < totX;
         const int e = valid ? idx : 0;
@@ -250,11 +258,19 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
         if (d < 0) continue;
         uint4 val = B.v[u];
         if (BWD && (d & 1)) val = bwd8(val, B.w[u], s_bt + 8 * ((d >> 2) & 7), 64);
+        if (FWD && XPRO) {   // forward: the deferred BN(+ReLU) of the staged input
+          const int cc = 8 * ((d >> 2) & 7);
+          float f[8];
+          unpack8(val, f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], s_xt[cc + k], s_xt[32 + cc + k]), s_xt[64 + cc + k]);
+          val = pack8(f);
+        }
         if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(tY + (d >> 5)) = val;
       }
 #pragma unroll
-      for (int u = 0; u < LDX; ++u) {
+      for (int u = 0; u < (FWD ? 0 : LDX); ++u) {
         const int d = B.dx[u];
         if (d < 0) continue;
         uint4 val = B.x[u];
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       k0 = k2; b0 = b2;
     }
     __syncthreads();   // the compute waves' last tile
-    if (BNE) __syncthreads();   // (the BN1 partials' exchange below)
+    if (BNE || (FWD && a.stat_part != nullptr)) __syncthreads();   // (the BN partials' exchange below)
     return;
   }
   // data-gradient: the wave's NJ 16-pixel columns -> dY tile pixel offsets
@@ -381,7 +397,11 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
         if (BNE && !lds_y && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
-        float sc[4], sh[4], mu[4];
+        float sc[4], sh[4], mu[4], bb[4];
+        if (FWD) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bb[r] = (a.bias != nullptr && cb + r < a.Co_l) ? a.bias[cb + r] : 0.f;
+        }
         if (BNE) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -394,8 +414,24 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
         for (int j = 0; j < NJ; ++j) {
           const long pm = pix(j);
           if (pm < 0) continue;
-          const uint32_t lo = pack2(acc[i][j][0], acc[i][j][1]), hi = pack2(acc[i][j][2], acc[i][j][3]);
+          f32x4_t v = acc[i][j];
+          if (FWD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+          }
+          const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+#ifndef FB_KO_STORE   // (profiling knock-out builds only)
           *reinterpret_cast<uint2*>(a.dxo + pm + cb) = make_uint2(lo, hi);
+#endif
+          if (FWD) {   // the output's BN statistics, of the stored (bf16) values
+            const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              cs[i][r] += g4[r];
+              cq[i][r] = fmaf(g4[r], g4[r], cq[i][r]);
+            }
+          }
           if (BNE) {
             const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                  __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -431,7 +467,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     for (int s = 0; s < 0; ++s) {
 #else
 #pragma unroll 2
-    for (int s = 0; s < NCH; ++s) {
+    for (int s = 0; s < (FWD ? 0 : NCH); ++s) {
 #endif
       const int hlo = halo_pix(32 * s + plo), hhi = halo_pix(32 * s + phi);
       uint4 fa[2];
@@ -443,7 +479,7 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       }
 #pragma unroll
       for (int m = 0; m < NT; ++m) {
-        const int u = wave + kFbWaves * m;   // (group, tap) unit: group 0's taps, then group 1's tap t1
+        const int u = wt + kFbTapGroups * m;   // (group, tap) unit: group 0's taps, then group 1's tap t1
         if (u >= nWU) break;   // wave-uniform
         const bool g2 = GO2 && u >= T;
         const int t = g2 ? a.t1 : u;
@@ -469,8 +505,8 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
     __syncthreads();   // tile i consumed, tile i + 1 staged
   }   // tile loop
 
-  // ---- BN1 partials: this block's row -------------------------------------------------------------------
-  if (BNE) {
+  // ---- BN partials (BN1's backward, or FWD: the output's statistics): this block's row ------------------------
+  if (BNE || (FWD && a.stat_part != nullptr)) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int cb = 16 * i + 4 * lg;
@@ -492,11 +528,12 @@ __global__ __launch_bounds__(kFbThreads, 1) void conv_bwd_fused_kernel(FusedBwdA
       a.stat_part[((long)blockIdx.x * 2 + 1) * Ci + c] = q2;
     }
   }
+  if constexpr (FWD) return;
   // ---- dW slab of this block: [Go*Co][T * Ci], element (g*Co + co, t*Ci + ci) ----------------------------
   float* slab = a.dw + (long)blockIdx.x * (Go * Co) * (T * Ci);
 #pragma unroll
   for (int m = 0; m < NT; ++m) {
-    const int u = wave + kFbWaves * m;
+    const int u = wt + kFbTapGroups * m;
     if (u >= nWU) break;
     const int g = (GO2 && u >= T) ? 1 : 0, t = g ? a.t1 : u;
 #pragma unroll
@@ -559,39 +596,47 @@ size_t fb_pair_lds(const FusedBwdGeom& fg) {
 }
 
 size_t fb_lds(const FusedBwdGeom& fg) {
-  return 2 * fb_pair_lds(fg) + (size_t)32 * (32 * fg.KS + 8) * 2 + (size_t)kFbWaves * 2 * 32 * 4;
+  return 2 * fb_pair_lds(fg) + (size_t)32 * (32 * fg.KS + 8) * 2 + (size_t)fg.cw * 2 * 32 * 4;
 }
 
 }  // namespace
 
 // Plan: eligible shapes and the tile geometry (0 = not eligible).  Symmetric tap sets only (3x3 with any
 // dilation, 1x7 / 7x1): the dY halo of the data-gradient and the x halo of the weight-gradient coincide.
-bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
+// fwd: the forward mode (conv_fwd_fused): x staged in the dY slots, no x tile, any tap set (the halo is the
+// forward taps' extent; the kernel gets the negated taps so that its data-gradient offsets walk them)
+static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
   // Go == 2: the ResidualBlock's 3x3 + 1x1 pair (the 1x1 at one tap of the 3x3's grid, FusedBwdArgs::t1)
-  if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > 2 || g.OH != g.IH || g.OW != g.IW) return false;
+  if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > (fwd ? 1 : 2) || g.OH != g.IH || g.OW != g.IW) return false;
   if (g.Cgi > 32 || g.Cgo > 32 || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2) return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
   for (int t = 0; t < g.T; ++t) {
     bool mirrored = false;
     for (int u = 0; u < g.T; ++u) mirrored |= g.dy[u] == -g.dy[t] && g.dx[u] == -g.dx[t];
-    if (!mirrored) return false;
+    if (!mirrored && !fwd) return false;
     ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
-  const int C8g = g.Cgo / 8, C8y = g.Go * C8g, C8x = g.Cgi / 8;
-  const int py = 8 * ((C8y & 1) ? C8y : C8y + 1), px = 8 * ((C8x & 1) ? C8x : C8x + 1);
+  const int C8g = (fwd ? g.Cgi : g.Cgo) / 8, C8y = g.Go * C8g, C8x = fwd ? 0 : g.Cgi / 8;
+  const int py = 8 * ((C8y & 1) ? C8y : C8y + 1), px = fwd ? 0 : 8 * ((C8x & 1) ? C8x : C8x + 1);
   const int KS = (g.T * C8g + (g.Go == 2 ? C8g : 0) + 3) / 4;
   if (KS > kFbMaxKS) return false;
   double best = 1e30;
   bool found = false;
-  for (int nj = 8; nj >= 4; nj -= 4) {
-    const int tp = kFbWaves * nj * 16;
+  static int force_cw = -1;   // env MSP_FB_CW: 4 / 8 forces the compute-wave layout of 512-pixel tiles (A/B)
+  if (force_cw < 0) {
+    const char* e = getenv("MSP_FB_CW");
+    force_cw = e == nullptr ? 0 : atoi(e);
+  }
+  for (int tp = 512; tp >= 256; tp /= 2) {
+    const int cw = tp == 256 ? 4 : (force_cw == 4 || force_cw == 8 ? force_cw : (g.Go == 1 ? 8 : 4));
+    const int nj = tp / (16 * cw);
     for (int tw = 16; tw <= 64; tw *= 2) {
       const int th = tp / tw;
       FusedBwdGeom c{};
       c.TH = th; c.TW = tw; c.tw_shift = tw == 16 ? 4 : (tw == 32 ? 5 : 6);
       c.HH = th + ey1 - ey0; c.HWD = tw + ex1 - ex0; c.ey0 = ey0; c.ex0 = ex0;
-      c.py = py; c.px = px; c.KS = KS; c.nj = nj;
+      c.py = py; c.px = px; c.KS = KS; c.nj = nj; c.cw = cw;
       if (fb_lds(c) > (size_t)kFbMaxLds) continue;
       const double tiles = (double)((g.OH + th - 1) / th) * ((g.OW + tw - 1) / tw);
       const double cost = tiles * ((double)c.HH * c.HWD * (C8y + C8x) + 0.25 * tp * (C8x + C8y));
@@ -604,13 +649,15 @@ bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) {
   }
   if (!found) return false;
   fg.inv_c8y = 1.0f / (float)C8y;
-  fg.inv_c8x = 1.0f / (float)C8x;
+  fg.inv_c8x = fwd ? 0.f : 1.0f / (float)C8x;
   fg.inv_hwd = 1.0f / (float)fg.HWD;
   fg.tiles_y = (g.OH + fg.TH - 1) / fg.TH;
   fg.tiles_x = (g.OW + fg.TW - 1) / fg.TW;
   fg.ntiles = (long)g.N * fg.tiles_y * fg.tiles_x <= (1L << 30) ? g.N * fg.tiles_y * fg.tiles_x : 0;
   return fg.ntiles > 0;
 }
+
+bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg) { return fb_plan(g, fg, false); }
 
 int conv_bwd_fused_blocks(const ConvGeom& g) {
   FusedBwdGeom fg;
@@ -631,22 +678,88 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
   const size_t lds = fb_lds(fg);
   const bool bwd = a.gy != nullptr || a.gy2 != nullptr, xpro = a.xc != nullptr, bne = a.bn_y != nullptr;
-#define FB_(NJ_, B_, X_, E_, G_)                                                                            \
-  if (fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_ && (g.Go == 2) == G_) {                           \
+#define FB_(CW_, NJ_, B_, X_, E_, G_)                                                                       \
+  if (fg.cw == CW_ && fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_ && (g.Go == 2) == G_) {           \
     static bool lds_attr = false;                                                                            \
     if (!lds_attr) {                                                                                         \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<NJ_, B_, X_, E_, G_>),  \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                      \
       lds_attr = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((conv_bwd_fused_kernel<NJ_, B_, X_, E_, G_>), dim3(grid), dim3(kFbThreads), lds, s, a, fg); \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_>), dim3(grid), dim3(fb_threads(CW_)), lds, s, \
+                       a, fg);                                                                               \
     return 0;                                                                                                \
   }
-#define FB4_(NJ_, B_, G_) FB_(NJ_, B_, false, false, G_) FB_(NJ_, B_, true, false, G_) FB_(NJ_, B_, false, true, G_) \
-                          FB_(NJ_, B_, true, true, G_)
-  FB4_(8, false, false) FB4_(8, true, false) FB4_(4, false, false) FB4_(4, true, false)
-  FB4_(8, false, true) FB4_(8, true, true) FB4_(4, false, true) FB4_(4, true, true)
+#define FB4_(CW_, NJ_, B_, G_) FB_(CW_, NJ_, B_, false, false, G_) FB_(CW_, NJ_, B_, true, false, G_)             \
+                               FB_(CW_, NJ_, B_, false, true, G_) FB_(CW_, NJ_, B_, true, true, G_)
+  FB4_(8, 4, false, false) FB4_(8, 4, true, false) FB4_(8, 4, false, true) FB4_(8, 4, true, true)
+  FB4_(4, 8, false, false) FB4_(4, 8, true, false) FB4_(4, 4, false, false) FB4_(4, 4, true, false)
+  FB4_(4, 8, false, true) FB4_(4, 8, true, true) FB4_(4, 4, false, true) FB4_(4, 4, true, true)
 #undef FB4_
 #undef FB_
+  return 8;
+}
+
+// ---- forward mode ----------------------------------------------------------------------------------------
+static int g_fwd_fused = -1;   // env MSP_CONV_FWD_FUSED: 0 off (the halo kernel), default on
+static bool fwd_fused_enabled() {
+  if (g_fwd_fused < 0) {
+    const char* e = getenv("MSP_CONV_FWD_FUSED");
+    g_fwd_fused = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_fwd_fused == 1;
+}
+
+void conv_set_fwd_fused(int on) { g_fwd_fused = on ? 1 : 0; }
+
+bool conv_fwd_fused_ok(const ConvGeom& g) {
+  FusedBwdGeom fg;
+  return fwd_fused_enabled() && fb_plan(g, fg, true);
+}
+
+long conv_fwd_fused_blocks(const ConvGeom& g) {
+  FusedBwdGeom fg;
+  if (!fb_plan(g, fg, true)) return 0;
+  return std::min(fg.ntiles, kFusedBwdGrid);
+}
+
+int conv_fwd_fused(const ConvArgs& ca, hipStream_t s) {
+  const ConvGeom& g = ca.g;
+  FusedBwdGeom fg;
+  if (!fb_plan(g, fg, true) || g.Gi != 1 || g.Go != 1 || ca.bn_y != nullptr || ca.accum) return 8;
+  FusedBwdArgs a{};
+  a.dz = ca.x[0];          // the staged operand (the data-gradient's dY slots)
+  a.x = ca.x[0];
+  a.xc = ca.xc[0];
+  a.xrelu = (ca.xrelu & 1u) ? 1 : 0;
+  a.wd = ca.w;             // forward packing [rows][Kp], k = t * Cgi + ci: the data-gradient's [Ci][T * Co]
+  a.Kp = g.Kp;
+  a.dxo = ca.y[0];
+  a.stat_part = ca.stat_part;
+  a.bias = ca.bias;
+  a.Co_l = g.Cgo_l;
+  a.N = g.N; a.H = g.IH; a.W = g.IW; a.T = g.T; a.Go = 1;
+  a.Ci = g.Cgo;            // kernel rows = output channels
+  a.Co = g.Cgi;            // staged channels = input channels
+  for (int t = 0; t < g.T; ++t) { a.dy[t] = -g.dy[t]; a.dx[t] = -g.dx[t]; }
+  fb_unit_order(a, fg);
+  const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
+  const size_t lds = fb_lds(fg);
+  const bool xpro = a.xc != nullptr;
+#define FF_(CW_, NJ_, X_)                                                                                    \
+  if (fg.cw == CW_ && fg.nj == NJ_ && xpro == X_) {                                                          \
+    static bool lds_attr = false;                                                                            \
+    if (!lds_attr) {                                                                                         \
+      (void)hipFuncSetAttribute(                                                                             \
+          reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true>),    \
+          hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                                            \
+      lds_attr = true;                                                                                       \
+    }                                                                                                        \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true>), dim3(grid),         \
+                       dim3(fb_threads(CW_)), lds, s, a, fg);                                                \
+    return 0;                                                                                                \
+  }
+  FF_(8, 4, false) FF_(8, 4, true) FF_(4, 8, false) FF_(4, 8, true) FF_(4, 4, false) FF_(4, 4, true)
+#undef FF_
   return 8;
 }

@@ -456,8 +456,8 @@ constexpr CfgId kCfgs[] = {
     {2, 2, 3, 2, 4, 32},   // 192 x 128, 4 stages (80 KB)
     {2, 2, 4, 2, 3, 32},   // 256 x 128, 3 stages (72 KB)
     {2, 2, 2, 2, 5, 32},   // 128 x 128, 5 stages (80 KB)
-    {2, 4, 2, 2, 3, 64},   // 128 x 256, 8 waves, 3 stages (144 KB, one block per CU)
-    {1, 8, 4, 1, 3, 64},   // 128 x 256, 8 waves along pixels, 3 stages (144 KB)
+    // (8-wave 128 x 256 tiles at 3 x 64-wide stages, one block per CU, measured 15-35 % slower than the
+    // planner's tiles at every level 3-6 shape: profiles/r05/gemm_cfg_8wave_3stage_bs320.txt)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 constexpr int kPlannerCfgs = 5;   // the planner's candidates (the rest: MSP_CONV_GEMM_CFG A/B only)

@@ -322,7 +322,10 @@ constexpr int kNumWgCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 int g_wg_mode = -1;   // env MSP_WGRAD_GEMM: 0 off (the conv.hip kernels), 1 auto (default), 2 every eligible conv
 int g_wg_cfg = -2;    // env MSP_WGRAD_GEMM_CFG: force a configuration (A/B); -1 planner
 long g_wg_blocks = -1;   // env MSP_WGRAD_GEMM_BLOCKS: grid size target (default 1024 = 2 blocks x 2 waves/CU x 256)
-double g_wg_stage_cost = -1;   // env MSP_WGRAD_STAGE_COST: planner's per-row staging cost (MAC units), see wg_pick
+// env MSP_WGRAD_STAGE_COST: the planner's per-row staging cost (MAC units, wg_pick).  96 (round 5) picks the
+// 8-wave 256-wide tiles for the >= 136-channel 3x3 / 1x7 layers: conv_bench levels 3-6 wgrad 25.3 -> 22.4 ms
+// at bs320 against 24 (profiles/r05/wgrad_stage_cost_bs320.txt)
+double g_wg_stage_cost = -1;
 
 void wg_env() {
   if (g_wg_mode < 0) {
@@ -339,7 +342,7 @@ void wg_env() {
   }
   if (g_wg_stage_cost < 0) {
     const char* e = getenv("MSP_WGRAD_STAGE_COST");
-    g_wg_stage_cost = (e != nullptr && atof(e) >= 0) ? atof(e) : 24.0;
+    g_wg_stage_cost = (e != nullptr && atof(e) >= 0) ? atof(e) : 96.0;
   }
 }
 

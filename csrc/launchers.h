@@ -88,7 +88,8 @@ void conv_set_halo_split(int mode);   // 0 never, 1 occupancy-preserving (defaul
 void conv_set_phase(int on);   // phase-decomposed strided TRANS convs (default on; env MSP_CONV_PHASE=0 off)
 // bwd: the launch carries a deferred BN-backward prologue (ConvArgs::gy): no PIPE variant, larger table
 bool conv_uses_halo(const ConvGeom& g, bool trans, bool bwd = false);
-long conv_stat_blocks(const ConvGeom& g, bool trans = false, bool bwd = false);   // trans: conv_igemm's flag
+// trans: conv_igemm's flag; bne: a data-gradient launch with the BN-backward epilogue (conv_fwd_bn)
+long conv_stat_blocks(const ConvGeom& g, bool trans = false, bool bwd = false, bool bne = false);
 // whether conv_wgrad runs the halo weight-gradient kernel (the only one with the BN-backward prologue)
 bool conv_wgrad_uses_halo(const ConvGeom& g, bool trans);
 // returns 0, or an error code (conv_error_string) -- the bindings raise it as a Python error
@@ -316,18 +317,28 @@ struct FusedBwdArgs {
   float* dw;
   int N, H, W, Ci, Co, T;
   int dy[9], dx[9];
+  // forward mode (conv_fwd_fused): per-output-channel bias (nullable) over the Co_l logical channels
+  const float* bias;
+  int Co_l;
   // data-gradient K-unit order (set by conv_bwd_fused): unit index, or -1 for a zero-weight padding unit.  Paired k-groups (0/1, 2/3) share a ds_read_b128 lane group: units paired with
   // equal slot offsets mod 16 read conflict-free.
   short uperm[96];
 };
 struct FusedBwdGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, ntiles;
-  int py, px, KS, nj;
+  int py, px, KS, nj, cw;   // cw: compute waves (4 or 8, conv_bwd.hip)
   float inv_c8y, inv_c8x, inv_hwd;   // fp32 reciprocals (fdiv) of the staging index math
 };
 bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg);
 int conv_bwd_fused_blocks(const ConvGeom& g);   // 0: not eligible
 int conv_bwd_fused(const FusedBwdArgs& a, const ConvGeom& g, hipStream_t s);
+// The same persistent staging / compute-wave kernel as a FORWARD conv (stride 1, one input and one output
+// group of <= 32 channels each, T >= 2: the 17-channel level's 3x3 / dilated / 1x7 convs): x staged through
+// the deferred-BN prologue, y + its BN statistics (per-block partial rows, conv_stat_blocks) in the epilogue.
+bool conv_fwd_fused_ok(const ConvGeom& g);
+long conv_fwd_fused_blocks(const ConvGeom& g);   // its stat partial rows (persistent grid)
+void conv_set_fwd_fused(int on);                   // A/B and tests (default: env MSP_CONV_FWD_FUSED, on)
+int conv_fwd_fused(const ConvArgs& a, hipStream_t s);
 
 // gconv.hip: grouped convolution (ResNeXt grouped 3x3), NHWC bf16, fp32 weights repacked [T][C][CG]
 int gconv_fwd(const uint16_t* x, const float* w, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C, int CG,

@@ -422,7 +422,7 @@ class _ConvFn(torch.autograd.Function):
                 dxs, parked = [parked], None
             elif h is not None and h.y is not None and not trans:
                 # dL/dx is the BN output's gradient: emit the BN backward partials in the epilogue
-                nblk = C.conv_stat_blocks(dims_d, dy, dx, False, bwd is not None)
+                nblk = C.conv_stat_blocks(dims_d, dy, dx, False, bwd is not None, True)
                 part = torch.empty(nblk, 2, plan.Gi * plan.Cgi, dtype=torch.float32, device=dev)
                 C.conv_fwd_bn(gys, wd, dxs, part, dims_d, dy, dx, h.y, h.stats, h.relu, **bk)
                 h.part = part

@@ -7,7 +7,11 @@ Chain case of the DUCKNet L1 level (reference models/ducknet.py:95-96,144-179): 
     kernel rebuilds y1 from the staged x tile),
   * dY = bwd(dz2, y2) rebuilt from the deferred BN2 backward (bwd1 in csrc/common.h),
 for Go = 1 (3x3 at dilation 1 / 2 / 3, 1x7, 7x1) and Go = 2 (the ResidualBlock's 3x3 + 1x1 pair), padded
-widths 8 / 16 / 24 (17 real) / 32 channels, on grids of several tiles and blocks (MI355X only)."""
+widths 8 / 16 / 24 (17 real) / 32 channels, on grids of several tiles and blocks (MI355X only).
+
+The same kernel's FORWARD mode (``conv_fwd_fused``: the 17-channel level's forward convs) is scored the same way:
+y = conv(relu(BN(x))) (+ bias) against ``F.conv2d`` in fp32 and its BN-statistics partials against the sums of
+the stored output, for symmetric and one-sided tap sets, and against the halo kernel it replaces."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -134,3 +138,78 @@ def test_fused_bwd_vs_fp32_conv_grads(gpu, case):
     p = part.sum(0)
     assert _rel(p[0, :ci], s_ref) < 2e-3, _rel(p[0, :ci], s_ref)
     assert _rel(p[1, :ci], q_ref) < 2e-2, _rel(p[1, :ci], q_ref)
+
+
+FWD_CASES = [
+    # n, h, w, ci, co, (kh, kw), pad, dil, prologue, bias
+    (3, 40, 56, 17, 17, (3, 3), (1, 1), 1, True, False),
+    (2, 33, 70, 17, 17, (3, 3), (2, 2), 2, True, False),
+    (2, 45, 38, 16, 16, (3, 3), (3, 3), 3, False, False),
+    (2, 30, 66, 17, 17, (1, 7), (0, 3), 1, True, False),
+    (2, 66, 30, 17, 17, (7, 1), (3, 0), 1, True, True),
+    (2, 36, 52, 8, 24, (3, 3), (1, 1), 1, False, True),
+    (2, 28, 44, 32, 17, (3, 3), (1, 1), 1, True, False),
+    (1, 37, 41, 24, 32, (3, 3), (0, 0), 1, False, False),   # one-sided taps (valid-padding geometry, same size)
+]
+
+
+@pytest.mark.parametrize('case', FWD_CASES)
+def test_fused_forward_vs_fp32_conv(gpu, case):
+    from medical_segmentation_pytorch_amd.ops._ext import require
+    from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, _taps
+    from medical_segmentation_pytorch_amd.ops.fm import cpad
+    C = require()
+    n, h, w, ci, co, (kh, kw), pad, dil, pro, with_bias = case
+    g = torch.Generator(device=gpu).manual_seed(21)
+    W = torch.randn(co, ci, kh, kw, device=gpu, generator=g) * 0.2
+    b = torch.randn(co, device=gpu, generator=g) if with_bias else None
+    plan = ConvPlan(kh, kw, ci, co, [Branch(W, 0, 0, kh * kw)], padding=pad, dilation=(dil, dil), bias=b)
+    cp, cq = cpad(ci), cpad(co)
+    dims = plan.fwd_dims(n, h, w, h, w)
+    dy, dx = _taps(plan.taps_fwd)
+    assert C.conv_fwd_fused_ok(dims, dy, dx), 'the case must take the fused forward'
+    x = torch.zeros(n, h, w, cp, device=gpu, dtype=torch.bfloat16)
+    x[..., :ci] = torch.randn(n, h, w, ci, device=gpu, generator=g).to(torch.bfloat16)
+    coefs, rmask = [None], 0
+    xin = x[..., :ci].permute(0, 3, 1, 2).float()
+    if pro:
+        st = torch.zeros(4, cp, device=gpu)
+        st[0, :ci] = torch.rand(ci, device=gpu, generator=g) + 0.5
+        st[1, :ci] = torch.randn(ci, device=gpu, generator=g) * 0.3
+        coefs, rmask = [st], 1
+        xin = _bf(torch.relu(xin * st[0, :ci].view(1, -1, 1, 1) + st[1, :ci].view(1, -1, 1, 1)))
+    wb = _bf(W)
+    if pad == (0, 0):
+        ref = F.conv2d(F.pad(xin, (0, 2 * dil, 0, 2 * dil)), wb, None, 1, 0, dil)
+    else:
+        ref = F.conv2d(xin, wb, None, 1, pad, dil)
+    if b is not None:
+        ref = ref + b.view(1, -1, 1, 1)
+    nblk = C.conv_stat_blocks(dims, dy, dx)
+    outs = {}
+    for fused in (True, False):
+        C.conv_set_fwd_fused(fused)
+        try:
+            y = torch.empty(n, h, w, cq, device=gpu, dtype=torch.bfloat16)
+            part = torch.empty(C.conv_stat_blocks(dims, dy, dx), 2, plan.rows, device=gpu)
+            bias = b.float().contiguous() if b is not None else None
+            C.conv_fwd([x], plan.pack_fwd(gpu), [y], bias, part, dims, dy, dx, False, coefs, rmask)
+            torch.cuda.synchronize()
+            outs[fused] = (y, part)
+        finally:
+            C.conv_set_fwd_fused(True)
+    y, part = outs[True]
+    assert part.shape[0] == nblk
+    got = y[..., :co].permute(0, 3, 1, 2).float()
+    assert torch.isfinite(got).all()
+    assert _rel(got, ref) < 1e-2, _rel(got, ref)
+    if cq > co:
+        assert y[..., co:].float().abs().max().item() == 0.0   # padding channels stay zero
+    yh, ph = outs[False]
+    assert _rel(got, yh[..., :co].permute(0, 3, 1, 2).float()) < 5e-3
+    # BN statistics partials: of the stored bf16 output
+    s_ref = got.sum((0, 2, 3))
+    q_ref = (got * got).sum((0, 2, 3))
+    p = part.sum(0)
+    assert _rel(p[0, :co], s_ref) < 1e-3, _rel(p[0, :co], s_ref)
+    assert _rel(p[1, :co], q_ref) < 1e-3, _rel(p[1, :co], q_ref)

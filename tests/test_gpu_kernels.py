@@ -434,10 +434,12 @@ def test_conv_halo_matches_gather(gpu, case):
     from medical_segmentation_pytorch_amd.ops import _ext
     C = _ext.require()
     C.conv_set_gemm(False)
+    C.conv_set_fwd_fused(False)   # (the fused forward has its own oracle: test_gpu_fused_bwd_oracle.py)
     try:
         _halo_vs_gather(gpu, case, C)
     finally:
         C.conv_set_gemm(True)
+        C.conv_set_fwd_fused(True)
 
 
 @pytest.mark.parametrize('case', HALO_CASES)
@@ -456,6 +458,7 @@ def test_conv_halo_split_bank_image_is_bitwise(gpu, case):
           for i in range(go)]
     outs = []
     C.conv_set_gemm(False)
+    C.conv_set_fwd_fused(False)
     try:
         for mode in (0, 2):
             C.conv_set_halo_split(mode)
@@ -467,6 +470,7 @@ def test_conv_halo_split_bank_image_is_bitwise(gpu, case):
     finally:
         C.conv_set_halo_split(1)
         C.conv_set_gemm(True)
+        C.conv_set_fwd_fused(True)
     (y0, p0, d0), (y2, p2, d2) = outs
     assert all(torch.equal(a, b) for a, b in zip(y0, y2))
     assert torch.equal(p0, p2)

@@ -18,6 +18,7 @@ def main():
     s = int(sys.argv[2]) if len(sys.argv) > 2 else 352
     dil = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     go = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    fwd = len(sys.argv) > 5 and sys.argv[5] == 'fwd'
     C = require()
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
@@ -44,7 +45,18 @@ def main():
 
     kw2 = dict(dz2=t(cp), gy2=t(cp), gs2=st, gk2=coef, grelu2=True, t1=4) if go == 2 else {}
 
+    if fwd:   # the forward mode (conv_fwd_fused): y = conv(relu(BN(x))) + BN statistics
+        wp = plan.pack_fwd(dev)
+        fd = plan.fwd_dims(n, s, s, s, s)
+        fdy, fdx = _taps(plan.taps_fwd)
+        assert C.conv_fwd_fused_ok(fd, fdy, fdx)
+        fpart = torch.empty(C.conv_stat_blocks(fd, fdy, fdx), 2, plan.rows, device=dev)
+        xin, yout = t(cp), torch.empty(n, s, s, plan.Cgo, device=dev, dtype=torch.bfloat16)
+
     def run():
+        if fwd:
+            C.conv_fwd([xin], wp, [yout], None, fpart, fd, fdy, fdx, False, [st], 1)
+            return
         C.conv_bwd_fused(dz, y2, st, coef, True, x, st, True, wd, kp, dxt, y1, coef, True, part, dwp, dims, tdy, tdx,
                          **kw2)
     for _ in range(3):
@@ -60,7 +72,9 @@ def main():
     ms = a.elapsed_time(b) / reps
     px = n * s * s
     hbm = px * cp * 2 * (4 + 1 + 2 * (go - 1)) * 1.2   # dz, y2 (per group), x, y1 (+ halo) read, dx written
-    print(f'conv_bwd_fused N={n} {s}x{s} d={dil} go={go} blocks={nblk}: {ms:.3f} ms  (~{hbm / ms / 1e9:.2f} TB/s of '
+    if fwd:
+        hbm = px * cp * 2 * (1.2 + 1)   # x (+ halo) read, y written
+    print(f'{"conv_fwd_fused" if fwd else "conv_bwd_fused"} N={n} {s}x{s} d={dil} go={go} blocks={nblk}: {ms:.3f} ms  (~{hbm / ms / 1e9:.2f} TB/s of '
           f'{hbm / 1e9:.2f} GB)  variant={os.environ.get("MSP_C_SO", "default")}')
 
 
