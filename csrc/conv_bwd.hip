@@ -36,10 +36,13 @@ constexpr int kFbProd = 4;        // staging waves: tile i + 1 into the other LD
 // for the 256-pixel tiles (dilation 3) and the Go = 2 pair, where it measured faster (conv_bwd_fused_plan).
 constexpr int fb_threads(int cw) { return 64 * (cw + kFbProd); }
 #ifndef FB_LDY
-#define FB_LDY 4   // dY vectors (two loads each) per staging thread and batch; two batches in flight
+#define FB_LDY 3   // dY vectors (two loads each) per staging thread and batch; two batches in flight
 #endif
 #ifndef FB_LDX
-#define FB_LDX 4   // x vectors per staging thread and batch
+#define FB_LDX 3   // x vectors per staging thread and batch (4 / 4 spill at the 168-register cap of CW = 8)
+#endif
+#ifndef FB_LDF
+#define FB_LDF 8   // forward mode: x vectors per staging thread and batch (one load each, no x tile)
 #endif
 constexpr int kFbMaxKS = 24;      // data-gradient k-steps (T <= 9 taps x <= 4 slots / 4)
 constexpr int kFbMaxT = 9;
@@ -50,6 +53,15 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 DEVI uint2 fb_tr_read(const uint16_t* p) {
   s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t __attribute__((address_space(3)))*)(p));
   union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
+}
+
+// deferred BN(+ReLU) prologue of 8 staged channels: max(x * scale + shift, floor); t = [scale x 32][shift x 32]
+DEVI uint4 xpro8(const uint4& v, const float* t, float floor) {
+  float f[8];
+  unpack8(v, f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], t[k], t[32 + k]), floor);
+  return pack8(f);
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     // (Round 4 staged one tile at a time with every batch's latency exposed: ~2.2 TB/s.)
     const int st = tid - 64 * kFbWaves;
     constexpr int NP = 64 * kFbProd;
-    constexpr int LDY = FB_LDY, LDX = FB_LDX;
+    constexpr int LDY = FWD ? FB_LDF : FB_LDY, LDX = FB_LDX;
     const int totY = hpx * C8y, totX = FWD ? 0 : hpx * C8x;   // FWD: x is staged as the "dY" tile
     const int NB = max((totY + NP * LDY - 1) / (NP * LDY), (totX + NP * LDX - 1) / (NP * LDX));
     const int ntb = (fg.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // grid <= ntiles
@@ -202,53 +214,86 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
                               // -1: nothing to store
       int buf;
     };
+    // Element cursors: thread st stages elements st, st + NP, ... of each tile's [halo pixel][8-channel slot]
+    // list.  (halo row, column, slot) advance by NP with carries (one division per role at the start, not two
+    // per element), and the image offsets are 32-bit per image: round 5's first pipeline spent ~130
+    // instructions per 16-B vector in the staging waves.
+    struct Cursor { int hy, hx, c8; };   // (an element past the list has hy >= HH)
+    struct Step { int r, a, b; };
+    auto cursor0 = [&](int C8) {
+      Cursor c;
+      const int hp = st / C8;
+      c.c8 = st - hp * C8;
+      c.hy = hp / fg.HWD;
+      c.hx = hp - c.hy * fg.HWD;
+      return c;
+    };
+    auto step_of = [&](int C8) {
+      Step t;
+      const int q = NP / C8;
+      t.r = NP - q * C8;
+      t.a = q / fg.HWD;
+      t.b = q - t.a * fg.HWD;
+      return t;
+    };
+    auto advance = [&](Cursor& c, const Step& t, int C8) {
+      c.c8 += t.r;
+      const int carry = c.c8 >= C8 ? 1 : 0;
+      c.c8 -= carry * C8;
+      c.hx += t.b + carry;
+      c.hy += t.a;
+      if (c.hx >= fg.HWD) { c.hx -= fg.HWD; ++c.hy; }
+    };
+    const Step sy = step_of(C8y), sx = FWD ? Step{} : step_of(C8x);
+    Cursor cy{}, cx{};
     auto issue = [&](int k, int b, Batch& B) {
       int ty0, tx0;
       long imoff;
       tile_origin((int)blockIdx.x + min(k, ntb - 1) * (int)gridDim.x, ty0, tx0, imoff);
       B.buf = k & 1;
+      if (b == 0) {   // (re-derived per tile rather than kept: registers)
+        cy = cursor0(C8y);
+        if (!FWD) cx = cursor0(C8x);
+      }
+      const int gy0 = ty0 + fg.ey0, gx0 = tx0 + fg.ex0;   // image row / column of halo pixel (0, 0)
 #pragma unroll
       for (int u = 0; u < LDY; ++u) {
-        const int idx = b * NP * LDY + u * NP + st;
-        const bool valid = idx < totY;
-        const int e = valid ? idx : 0;
-        const int hp = fdiv(e, C8y, fg.inv_c8y), c8 = e - hp * C8y;
-        const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
-        const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
-        const bool in = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-        const long pix = imoff + (in ? (long)iy * a.W + ix : 0);
+        const bool valid = cy.hy < fg.HH;
+        const int c8 = cy.c8, iy = gy0 + cy.hy, ix = gx0 + cy.hx;
+        const bool in = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         const bool g2 = GO2 && c8 >= C8g;   // (a select of two kernarg pointers, not an indexed load)
         const int cl = 8 * (c8 - (g2 ? C8g : 0));
-        const uint16_t* dzp = (g2 ? a.dz2 : a.dz) + pix * Co + cl;
+        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Co + cl) : 0u;   // within the image
+        const uint16_t* dzb = (g2 ? a.dz2 : a.dz) + imoff * Co;
         const uint16_t* yp = g2 ? a.gy2 : a.gy;
         const bool tr = BWD && (!GO2 || yp != nullptr);   // else a plain gradient group: stored as loaded
 #ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
-        B.v[u] = fb_ldg4(dzp);
-        if (BWD) B.w[u] = fb_ldg4(tr ? yp + pix * Co + cl : dzp);
+        B.v[u] = fb_ldg4(dzb + off);
+        if (BWD) B.w[u] = fb_ldg4(tr ? yp + imoff * Co + off : dzb + off);
 #else
         B.v[u] = make_uint4(0, 0, 0, 0);
         B.w[u] = make_uint4(0, 0, 0, 0);
 #endif
-        B.dy[u] = valid ? ((hp * fg.py + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0) | (tr ? 1 : 0)) : -1;
+        B.dy[u] = valid ? (((cy.hy * fg.HWD + cy.hx) * fg.py + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0) | (tr ? 1 : 0))
+                        : -1;
+        advance(cy, sy, C8y);
       }
 #pragma unroll
       for (int u = 0; u < (FWD ? 0 : LDX); ++u) {
-        const int idx = b * NP * LDX + u * NP + st;
-        const bool valid = idx < totX;
-        const int e = valid ? idx : 0;
-        const int hp = fdiv(e, C8x, fg.inv_c8x), c8 = e - hp * C8x;
-        const int hy = fdiv(hp, fg.HWD, fg.inv_hwd), hx = hp - hy * fg.HWD;
-        const int iy = ty0 + fg.ey0 + hy, ix = tx0 + fg.ex0 + hx;
-        const bool in = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-        const long pix = imoff + (in ? (long)iy * a.W + ix : 0);
+        const bool valid = cx.hy < fg.HH;
+        const int c8 = cx.c8, iy = gy0 + cx.hy, ix = gx0 + cx.hx;
+        const bool in = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Ci + 8 * c8) : 0u;
 #ifndef FB_KO_LOADS
-        B.x[u] = fb_ldg4(a.x + pix * Ci + 8 * c8);
+        B.x[u] = fb_ldg4(a.x + imoff * Ci + off);
 #else
         B.x[u] = make_uint4(0, 0, 0, 0);
 #endif
-        B.dx[u] = valid ? ((hp * fg.px + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0)) : -1;
+        B.dx[u] = valid ? (((cx.hy * fg.HWD + cx.hx) * fg.px + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0)) : -1;
+        advance(cx, sx, C8x);
       }
     };
+    const float xfloor = a.xrelu ? 0.f : -INFINITY;   // the prologue's ReLU (uniform: no per-channel table)
     auto commit = [&](const Batch& B) {
       uint16_t* const tY = lds0 + B.buf * pair;
       uint16_t* const tX = tY + hpx * fg.py + kFbSlack;
@@ -258,14 +303,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (d < 0) continue;
         uint4 val = B.v[u];
         if (BWD && (d & 1)) val = bwd8(val, B.w[u], s_bt + 8 * ((d >> 2) & 7), 64);
-        if (FWD && XPRO) {   // forward: the deferred BN(+ReLU) of the staged input
-          const int cc = 8 * ((d >> 2) & 7);
-          float f[8];
-          unpack8(val, f);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], s_xt[cc + k], s_xt[32 + cc + k]), s_xt[64 + cc + k]);
-          val = pack8(f);
-        }
+        if (FWD && XPRO) val = xpro8(val, s_xt + 8 * ((d >> 2) & 7), xfloor);   // forward: BN(+ReLU) of x
         if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(tY + (d >> 5)) = val;
       }
@@ -274,14 +312,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         const int d = B.dx[u];
         if (d < 0) continue;
         uint4 val = B.x[u];
-        if (XPRO) {
-          const int cc = 8 * ((d >> 2) & 7);
-          float f[8];
-          unpack8(val, f);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], s_xt[cc + k], s_xt[32 + cc + k]), s_xt[64 + cc + k]);
-          val = pack8(f);
-        }
+        if (XPRO) val = xpro8(val, s_xt + 8 * ((d >> 2) & 7), xfloor);
         if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(tX + (d >> 5)) = val;
       }
@@ -310,6 +341,16 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     if (BNE || (FWD && a.stat_part != nullptr)) __syncthreads();   // (the BN partials' exchange below)
     return;
   }
+  // FWD: the bias of this lane's output channels, read once (a global load in the epilogue put a vmcnt(0)
+  // there, which also waited for every store of the tile before it)
+  float bias4[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * i + 4 * lg + r;
+      bias4[i][r] = (FWD && a.bias != nullptr && c < a.Co_l) ? a.bias[c] : 0.f;
+    }
   // data-gradient: the wave's NJ 16-pixel columns -> dY tile pixel offsets
   int pb[NJ];
 #pragma unroll
@@ -354,16 +395,19 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       // BN1: this tile's y1 at the output pixels; the first row block's loads go out ahead of the k loop
       // (their latency under the MFMAs), the second's ahead of the first block's epilogue
       uint2 yy[MI][NJ];
-      auto pix = [&](int j) -> long {   // element offset of column j's output pixel (-1: outside the image)
+      // per-image element offset of column j's output pixel (-1: outside the image; one image < 2^31 elements)
+      auto pix = [&](int j) -> int {
         const int p = (wave * NJ + j) * 16 + lr;
         const int ty = ty0 + (p >> fg.tw_shift), tx = tx0 + (p & (fg.TW - 1));
-        return (ty < a.H && tx < a.W) ? (imoff + (long)ty * a.W + tx) * Ci : -1;
+        return (ty < a.H && tx < a.W) ? (ty * a.W + tx) * Ci : -1;
       };
+      uint16_t* const dxo_im = a.dxo + imoff * Ci;   // this tile's image
+      const uint16_t* const bny_im = BNE ? a.bn_y + imoff * Ci : nullptr;
       auto load_y = [&](int i) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const long pm = pix(j);
-          yy[i][j] = (pm >= 0 && 16 * i + 4 * lg < Ci) ? *reinterpret_cast<const uint2*>(a.bn_y + pm + 16 * i + 4 * lg)
+          const int pm = pix(j);
+          yy[i][j] = (pm >= 0 && 16 * i + 4 * lg < Ci) ? *reinterpret_cast<const uint2*>(bny_im + pm + 16 * i + 4 * lg)
                                                        : make_uint2(0, 0);
         }
       };
@@ -397,11 +441,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (BNE && !lds_y && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
-        float sc[4], sh[4], mu[4], bb[4];
-        if (FWD) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) bb[r] = (a.bias != nullptr && cb + r < a.Co_l) ? a.bias[cb + r] : 0.f;
-        }
+        float sc[4], sh[4], mu[4];
         if (BNE) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -412,16 +452,16 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const long pm = pix(j);
+          const int pm = pix(j);
           if (pm < 0) continue;
           f32x4_t v = acc[i][j];
           if (FWD) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+            for (int r = 0; r < 4; ++r) v[r] += bias4[i][r];
           }
           const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
 #ifndef FB_KO_STORE   // (profiling knock-out builds only)
-          *reinterpret_cast<uint2*>(a.dxo + pm + cb) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(dxo_im + pm + cb) = make_uint2(lo, hi);
 #endif
           if (FWD) {   // the output's BN statistics, of the stored (bf16) values
             const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
