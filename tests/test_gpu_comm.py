@@ -26,6 +26,17 @@ comm.POLICY['mode'] = 'ipc'
 c = comm.attach(dist.group.WORLD, dev)
 assert c is not None
 res = {'self_test': True, 'mismatch': 0, 'checked': 0, 'rank_disagree': 0}
+
+
+def close(got, ref, x):
+    if world == 2:   # one fp64 addition: bitwise the collective
+        return torch.equal(got, ref)
+    # the kernel sums in rank order, gloo in its own: equal up to the rounding of world - 1 additions,
+    # bounded by the magnitude sum (cancellation makes any bound relative to the result meaningless)
+    mag = x.abs()
+    dist.all_reduce(mag)
+    return bool(((got - ref).abs() <= world * 2.0 ** -52 * mag).all())
+
 g = torch.Generator().manual_seed(100 + rank)
 for it in range(300):
     n = [1, 7, 1088, 4099, c.cap][it % 5]
@@ -35,10 +46,7 @@ for it in range(300):
     buf = x.to(dev)
     c.all_reduce(buf)
     got = buf.cpu()
-    if world == 2:   # one fp64 addition: bitwise the collective
-        res['mismatch'] += int(not torch.equal(got, ref))
-    else:            # the kernel sums in rank order, gloo in its own: equal up to fp64 rounding
-        res['mismatch'] += int(not torch.allclose(got, ref, rtol=1e-12, atol=1e-300))
+    res['mismatch'] += int(not close(got, ref, x))
     # every rank must hold the SAME bits (rank-order reduction on every rank)
     mine = got.clone()
     dist.broadcast(mine, 0)
@@ -69,7 +77,7 @@ for it in range(20):
     dist.barrier()
     graph.replay()
     torch.cuda.synchronize()
-    gmis += int(not torch.equal(buf.cpu(), ref))
+    gmis += int(not close(buf.cpu(), ref, v))
 res['graph_mismatch'] = gmis
 # latency: back-to-back exchanges of one DUCK level's rows (2 x 544 fp64 per BN, 6 BNs)
 row = torch.randn(6 * 2 * 544, dtype=torch.float64, device=dev)
