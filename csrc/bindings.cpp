@@ -904,6 +904,40 @@ void comm_allreduce_t(const at::Tensor& in, const at::Tensor& out, const std::ve
 }
 
 // ---- conv_bwd.hip: fused data- + weight-gradient of a narrow stride-1 conv ---------------------------
+// ---- MAnet position attention (csrc/attention.hip) -----------------------------------------------------------
+void batched_gemm_t(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t batch, int64_t M, int64_t N,
+                    int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sa, int64_t sb, int64_t sc, bool ta, bool tb) {
+  CHECK_BF16(A);
+  CHECK_BF16(B);
+  CHECK_DEV(C);
+  const bool out_bf16 = C.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(out_bf16 || C.scalar_type() == at::kFloat, "C must be bf16 or fp32");
+  // extent checks: the last element each operand's indexing can reach
+  const int64_t a_last = (batch - 1) * sa + (ta ? (K - 1) * lda + M - 1 : (M - 1) * lda + K - 1);
+  const int64_t b_last = (batch - 1) * sb + (tb ? (N - 1) * ldb + K - 1 : (K - 1) * ldb + N - 1);
+  const int64_t c_last = (batch - 1) * sc + (M - 1) * ldc + N - 1;
+  TORCH_CHECK(A.is_contiguous() && B.is_contiguous() && C.is_contiguous(), "contiguous operands");
+  TORCH_CHECK(a_last < A.numel() && b_last < B.numel() && c_last < C.numel(), "batched_gemm: operand extents");
+  const int rc = batched_gemm(bf(A), bf(B), C.data_ptr(), out_bf16, (int)batch, (int)M, (int)N, (int)K, (int)lda,
+                              (int)ldb, (int)ldc, sa, sb, sc, ta, tb, cur_stream());
+  TORCH_CHECK(rc == 0, "batched_gemm: bad shape");
+}
+
+void softmax_all_t(const at::Tensor& S, const at::Tensor& P, int64_t batch, int64_t n) {
+  CHECK_F32(S);
+  CHECK_BF16(P);
+  TORCH_CHECK(S.numel() == batch * n && P.numel() == batch * n, "softmax_all: [batch][n]");
+  softmax_all(S.data_ptr<float>(), bf(P), (int)batch, n, cur_stream());
+}
+
+void softmax_all_bwd_t(const at::Tensor& P, const at::Tensor& dP, const at::Tensor& dS, int64_t batch, int64_t n) {
+  CHECK_BF16(P);
+  CHECK_F32(dP);
+  CHECK_BF16(dS);
+  TORCH_CHECK(P.numel() == batch * n && dP.numel() == batch * n && dS.numel() == batch * n, "softmax_all_bwd: [batch][n]");
+  softmax_all_bwd(bf(P), dP.data_ptr<float>(), bf(dS), (int)batch, n, cur_stream());
+}
+
 int64_t conv_bwd_fused_blocks_t(std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
   return conv_bwd_fused_blocks(make_geom(dims, dy, dx));
 }
@@ -1095,6 +1129,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_wgrad", &dwconv_wgrad_t);
   m.def("colsum", &colsum_t);
   m.def("conv_bwd_fused_blocks", &conv_bwd_fused_blocks_t);
+  m.def("batched_gemm", &batched_gemm_t);
+  m.def("softmax_all", &softmax_all_t);
+  m.def("softmax_all_bwd", &softmax_all_bwd_t);
   m.def("conv_set_fwd_fused", [](bool on) { conv_set_fwd_fused(on ? 1 : 0); });
   m.def("conv_fwd_fused_ok", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
     return conv_fwd_fused_ok(make_geom(dims, dy, dx));

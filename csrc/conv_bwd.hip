@@ -361,8 +361,18 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   // weight-gradient transposed-read pixel rows: chunk pixel 8*lg + q (lo) and + 4 (hi), q = lr >> 2
   const int q = lr >> 2, p4 = lr & 3;
   const int plo = 8 * lg + q, phi = plo + 4;
-  // tile pixel P -> halo pixel index (per chunk s: P = 32 s + plo / phi)
-  auto halo_pix = [&](int P) { return ((P >> fg.tw_shift) - fg.ey0) * fg.HWD + ((P & (fg.TW - 1)) - fg.ex0); };
+  // lane part of a chunk's transposed-read halo pixels (tile pixel plo; phi = plo + 4 is in the same tile row):
+  // element offsets in the dY / x tiles, and each weight-gradient unit's tap offset in the x tile
+  const int Ly = (plo >> fg.tw_shift) * fg.HWD + (plo & (fg.TW - 1));
+  const int offYlo = Ly * fg.py + 4 * p4, offYhi = offYlo + 4 * fg.py;
+  const int offXlo = Ly * fg.px + 4 * p4, offXhi = offXlo + 4 * fg.px;
+  int swx[NT];
+#pragma unroll
+  for (int m = 0; m < NT; ++m) {
+    const int u = wt + kFbTapGroups * m;
+    swx[m] = u < nWU ? s_wb[(GO2 && u >= T) ? a.t1 : u] * fg.px : 0;
+  }
+  (void)phi;
 
   f32x4_t accw[NT][2][2];
 #pragma unroll
@@ -509,33 +519,35 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
 #pragma unroll 2
     for (int s = 0; s < (FWD ? 0 : NCH); ++s) {
 #endif
-      const int hlo = halo_pix(32 * s + plo), hhi = halo_pix(32 * s + phi);
+      // chunk s's halo pixel = a uniform part (the chunk's first tile pixel) + this lane's constant part: one
+      // scalar product per chunk instead of per-lane shifts and multiplies for every operand address
+      const int S = (((32 * s) >> fg.tw_shift) - fg.ey0) * fg.HWD + ((32 * s) & (fg.TW - 1)) - fg.ex0;
+      const uint16_t* const y0 = tY + S * fg.py;
+      const uint16_t* const x0 = tX + S * fg.px;
       uint4 fa[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const uint2 lo = fb_tr_read(tY + hlo * fg.py + 16 * i + 4 * p4);
-        const uint2 hi = fb_tr_read(tY + hhi * fg.py + 16 * i + 4 * p4);
+        const uint2 lo = fb_tr_read(y0 + offYlo + 16 * i);
+        const uint2 hi = fb_tr_read(y0 + offYhi + 16 * i);
         fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
 #pragma unroll
       for (int m = 0; m < NT; ++m) {
         const int u = wt + kFbTapGroups * m;   // (group, tap) unit: group 0's taps, then group 1's tap t1
         if (u >= nWU) break;   // wave-uniform
-        const bool g2 = GO2 && u >= T;
-        const int t = g2 ? a.t1 : u;
-        if (g2) {   // the second group's dY columns; its unit is the wave's last, so fa is overwritten
+        if (GO2 && u >= T) {   // the second group's dY columns; its unit is the wave's last, so fa is overwritten
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            const uint2 lo = fb_tr_read(tY + hlo * fg.py + Co + 16 * i + 4 * p4);
-            const uint2 hi = fb_tr_read(tY + hhi * fg.py + Co + 16 * i + 4 * p4);
+            const uint2 lo = fb_tr_read(y0 + offYlo + Co + 16 * i);
+            const uint2 hi = fb_tr_read(y0 + offYhi + Co + 16 * i);
             fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
           }
         }
-        const int sw = s_wb[t];
+        const uint16_t* const xb = x0 + swx[m];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const uint2 lo = fb_tr_read(tX + (hlo + sw) * fg.px + 16 * j + 4 * p4);
-          const uint2 hi = fb_tr_read(tX + (hhi + sw) * fg.px + 16 * j + 4 * p4);
+          const uint2 lo = fb_tr_read(xb + offXlo + 16 * j);
+          const uint2 hi = fb_tr_read(xb + offXhi + 16 * j);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
           for (int i = 0; i < 2; ++i) accw[m][i][j] = mfma16x16x32(fa[i], fb, accw[m][i][j]);

@@ -340,6 +340,13 @@ long conv_fwd_fused_blocks(const ConvGeom& g);   // its stat partial rows (persi
 void conv_set_fwd_fused(int on);                   // A/B and tests (default: env MSP_CONV_FWD_FUSED, on)
 int conv_fwd_fused(const ConvArgs& a, hipStream_t s);
 
+// attention.hip: batched bf16 GEMM C[b] = op(A[b]) . op(B[b]) (fp32 accumulation, bf16 / fp32 out) and the
+// whole-map softmax (+ backward) of MAnet's position-attention block
+int batched_gemm(const uint16_t* A, const uint16_t* B, void* C, bool out_bf16, int batch, int M, int N, int K, int lda,
+                 int ldb, int ldc, long sa, long sb, long sc, bool transA, bool transB, hipStream_t s);
+void softmax_all(const float* S, uint16_t* P, int batch, long n, hipStream_t s);
+void softmax_all_bwd(const uint16_t* P, const float* dP, uint16_t* dS, int batch, long n, hipStream_t s);
+
 // gconv.hip: grouped convolution (ResNeXt grouped 3x3), NHWC bf16, fp32 weights repacked [T][C][CG]
 int gconv_fwd(const uint16_t* x, const float* w, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C, int CG,
               int stride, int T, const int* dyv, const int* dxv, hipStream_t s);

@@ -7,9 +7,9 @@ are the decoder kernels of ``csrc/decoder.hip`` (bilinear resize, GroupNorm, ada
 depthwise conv) and the existing elementwise ones (nearest up2 + add / concat, n-way add).  Concats
 that feed a conv are read as the conv's input channel groups where the widths allow it (ASPP's five
 branches, PSP's pyramid + input, MAnet's gated high-level + skip), so they are never built.  PAN and
-MAnet: every conv / BN / pooling / resize on the HIP kernels; their attention glue (sigmoid gates,
-broadcast products, MAnet's position-attention matmuls + softmax) is torch tensor ops on the NHWC maps
-(the matmuls are plain library GEMMs on hipBLASLt).
+MAnet: every conv / BN / pooling / resize on the HIP kernels, and MAnet's position-attention products
++ whole-map softmax on ``csrc/attention.hip`` (``ops.attention``); the remaining attention glue (sigmoid
+gates, broadcast products) is torch elementwise ops on the NHWC maps.
 """
 from __future__ import annotations
 
@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import pab_attention
 from ..ops.bn import materialize
 from ..ops.conv import conv
 from ..ops.decoder import adaptive_avgpool, dwconv, group_norm_act, resize_bilinear
@@ -262,8 +263,7 @@ class SmpDecoders:
         top = self.conv_plain(pab.top_conv, x, training).reshape(b, hw, -1)[..., :P]
         center = self.conv_plain(pab.center_conv, x, training).reshape(b, hw, -1)[..., :P]
         bottom = self.conv_plain(pab.bottom_conv, x, training).reshape(b, hw, -1)[..., :C]
-        sp = torch.softmax(torch.matmul(center, top.transpose(1, 2)).reshape(b, -1).float(), dim=1)
-        sp = torch.matmul(sp.to(x.dtype).reshape(b, hw, hw), bottom)          # [b, hw, C]
+        sp = pab_attention(center, top, bottom)   # softmax over the whole map, . bottom: [b, hw, C] (HIP)
         # the reference reshapes the [b, hw, C] product straight to [b, C, h, w] (no transpose): same here
         sp = sp.reshape(b, C, h, w).permute(0, 2, 3, 1)
         if Cp != C:

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
                     reason='hipcc not available')
 def test_conv_planner_under_asan_ubsan():
-    srcs = [os.path.join(ROOT, 'csrc', f) for f in ('conv.hip', 'common.h', 'launchers.h')]
+    srcs = [os.path.join(ROOT, 'csrc', f) for f in ('conv.hip', 'conv_bwd.hip', 'common.h', 'launchers.h')]
     srcs += [os.path.join(ROOT, 'tools', 'sanitize', f) for f in ('plan_check.cpp', 'run.sh')]
     h = hashlib.sha1(b''.join(open(f, 'rb').read() for f in srcs)).hexdigest()[:12]
     exe = f'/tmp/msp_plan_check_{h}'
