@@ -55,12 +55,12 @@ DEVI uint2 fb_tr_read(const uint16_t* p) {
   union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
 }
 
-// deferred BN(+ReLU) prologue of 8 staged channels: max(x * scale + shift, floor); t = [scale x 32][shift x 32]
-DEVI uint4 xpro8(const uint4& v, const float* t, float floor) {
+// deferred BN(+ReLU) prologue of 8 staged channels: max(x * scale + shift, floor); c = [scale x 8][shift x 8]
+DEVI uint4 xpro8(const uint4& v, const float* c, float floor) {
   float f[8];
   unpack8(v, f);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], t[k], t[32 + k]), floor);
+  for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], c[k], c[8 + k]), floor);
   return pack8(f);
 }
 
@@ -204,47 +204,59 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     const int st = tid - 64 * kFbWaves;
     constexpr int NP = 64 * kFbProd;
     constexpr int LDY = FWD ? FB_LDF : FB_LDY, LDX = FB_LDX;
-    const int totY = hpx * C8y, totX = FWD ? 0 : hpx * C8x;   // FWD: x is staged as the "dY" tile
-    const int NB = max((totY + NP * LDY - 1) / (NP * LDY), (totX + NP * LDX - 1) / (NP * LDX));
+    // Fixed-slot staging: thread st serves ONE 8-channel slot c8 = st % C8 for the halo pixels st / C8 +
+    // k * (NP / C8), k = 0, 1, ... ((NP / C8) * C8 threads per role; the others issue clamped loads and store
+    // nothing).  The slot's BN coefficients then live in registers (round 5's element-order staging read 10
+    // LDS vectors of bwd8 coefficients per dY vector) and the pixel cursor advances by a constant with one
+    // carry; image offsets are 32-bit per image.
+    const int PY = NP / C8y, PX = FWD ? 1 : NP / C8x;             // pixels per step of a role
+    const int c8y = st % C8y, c8x = FWD ? 0 : st % C8x;
+    const bool acty = st < PY * C8y, actx = !FWD && st < PX * C8x;
+    const int jobsY = (hpx + PY - 1) / PY, jobsX = FWD ? 0 : (hpx + PX - 1) / PX;
+    const int NB = max((jobsY + LDY - 1) / LDY, (jobsX + LDX - 1) / LDX);
     const int ntb = (fg.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // grid <= ntiles
     const int Q = ntb * NB;
     struct Batch {
       uint4 v[LDY], w[LDY], x[LDX];
-      int dy[LDY], dx[LDX];   // LDS element offset << 5 | 8-channel slot << 2 | in-image << 1 | rebuild;
-                              // -1: nothing to store
+      int dy[LDY], dx[LDX];   // LDS element offset << 2 | in-image << 1; -1: nothing to store
       int buf;
     };
-    // Element cursors: thread st stages elements st, st + NP, ... of each tile's [halo pixel][8-channel slot]
-    // list.  (halo row, column, slot) advance by NP with carries (one division per role at the start, not two
-    // per element), and the image offsets are 32-bit per image: round 5's first pipeline spent ~130
-    // instructions per 16-B vector in the staging waves.
-    struct Cursor { int hy, hx, c8; };   // (an element past the list has hy >= HH)
-    struct Step { int r, a, b; };
+    struct Cursor { int hy, hx; };   // (a pixel past the halo has hy >= HH)
+    struct Step { int a, b; };       // pixel step = a rows + b columns
     auto cursor0 = [&](int C8) {
-      Cursor c;
-      const int hp = st / C8;
-      c.c8 = st - hp * C8;
-      c.hy = hp / fg.HWD;
-      c.hx = hp - c.hy * fg.HWD;
-      return c;
+      const int hp = st / C8, hy = hp / fg.HWD;
+      return Cursor{hy, hp - hy * fg.HWD};
     };
-    auto step_of = [&](int C8) {
-      Step t;
-      const int q = NP / C8;
-      t.r = NP - q * C8;
-      t.a = q / fg.HWD;
-      t.b = q - t.a * fg.HWD;
-      return t;
-    };
-    auto advance = [&](Cursor& c, const Step& t, int C8) {
-      c.c8 += t.r;
-      const int carry = c.c8 >= C8 ? 1 : 0;
-      c.c8 -= carry * C8;
-      c.hx += t.b + carry;
+    auto step_of = [&](int P) { const int a = P / fg.HWD; return Step{a, P - a * fg.HWD}; };
+    auto advance = [&](Cursor& c, const Step& t) {
+      c.hx += t.b;
       c.hy += t.a;
       if (c.hx >= fg.HWD) { c.hx -= fg.HWD; ++c.hy; }
     };
-    const Step sy = step_of(C8y), sx = FWD ? Step{} : step_of(C8x);
+    const Step sy = step_of(PY), sx = FWD ? Step{} : step_of(PX);
+    // this thread's slot: the dY group (GO2) and whether its dY is rebuilt (a plain gradient group is stored as
+    // loaded), its coefficient registers (BWD: bwd8's [scale, shift, k1, k2, k3] x 8; the prologues: scale,
+    // shift x 8) and LDS column offsets
+    const bool g2y = GO2 && c8y >= C8g;
+    const int cly = 8 * (c8y - (g2y ? C8g : 0));
+    const uint16_t* const dzbase = g2y ? a.dz2 : a.dz;
+    const uint16_t* const ybase = g2y ? a.gy2 : a.gy;
+    const bool try_ = BWD && (!GO2 || ybase != nullptr);
+    float cfy[BWD ? 40 : ((FWD && XPRO) ? 16 : 1)];
+    if constexpr (BWD) {
+#pragma unroll
+      for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cfy[8 * r + e] = s_bt[64 * r + 8 * c8y + e];
+    } else if constexpr (FWD && XPRO) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { cfy[e] = s_xt[8 * c8y + e]; cfy[8 + e] = s_xt[32 + 8 * c8y + e]; }
+    }
+    float cfx[(!FWD && XPRO) ? 16 : 1];
+    if constexpr (!FWD && XPRO) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { cfx[e] = s_xt[8 * c8x + e]; cfx[8 + e] = s_xt[32 + 8 * c8x + e]; }
+    }
     Cursor cy{}, cx{};
     auto issue = [&](int k, int b, Batch& B) {
       int ty0, tx0;
@@ -256,41 +268,36 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (!FWD) cx = cursor0(C8x);
       }
       const int gy0 = ty0 + fg.ey0, gx0 = tx0 + fg.ex0;   // image row / column of halo pixel (0, 0)
+      const uint16_t* const dzb = dzbase + imoff * Co;
 #pragma unroll
       for (int u = 0; u < LDY; ++u) {
-        const bool valid = cy.hy < fg.HH;
-        const int c8 = cy.c8, iy = gy0 + cy.hy, ix = gx0 + cy.hx;
+        const bool valid = acty && cy.hy < fg.HH;
+        const int iy = gy0 + cy.hy, ix = gx0 + cy.hx;
         const bool in = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-        const bool g2 = GO2 && c8 >= C8g;   // (a select of two kernarg pointers, not an indexed load)
-        const int cl = 8 * (c8 - (g2 ? C8g : 0));
-        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Co + cl) : 0u;   // within the image
-        const uint16_t* dzb = (g2 ? a.dz2 : a.dz) + imoff * Co;
-        const uint16_t* yp = g2 ? a.gy2 : a.gy;
-        const bool tr = BWD && (!GO2 || yp != nullptr);   // else a plain gradient group: stored as loaded
+        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Co + cly) : 0u;   // within the image
 #ifndef FB_KO_LOADS   // (profiling knock-out builds only: csrc/build.py MSP_BUILD_DEFINES)
         B.v[u] = fb_ldg4(dzb + off);
-        if (BWD) B.w[u] = fb_ldg4(tr ? yp + imoff * Co + off : dzb + off);
+        if (BWD) B.w[u] = fb_ldg4(try_ ? ybase + imoff * Co + off : dzb + off);
 #else
         B.v[u] = make_uint4(0, 0, 0, 0);
         B.w[u] = make_uint4(0, 0, 0, 0);
 #endif
-        B.dy[u] = valid ? (((cy.hy * fg.HWD + cy.hx) * fg.py + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0) | (tr ? 1 : 0))
-                        : -1;
-        advance(cy, sy, C8y);
+        B.dy[u] = valid ? (((cy.hy * fg.HWD + cy.hx) * fg.py + 8 * c8y) << 2 | (in ? 2 : 0)) : -1;
+        advance(cy, sy);
       }
 #pragma unroll
       for (int u = 0; u < (FWD ? 0 : LDX); ++u) {
-        const bool valid = cx.hy < fg.HH;
-        const int c8 = cx.c8, iy = gy0 + cx.hy, ix = gx0 + cx.hx;
+        const bool valid = actx && cx.hy < fg.HH;
+        const int iy = gy0 + cx.hy, ix = gx0 + cx.hx;
         const bool in = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Ci + 8 * c8) : 0u;
+        const unsigned off = in ? (unsigned)((iy * a.W + ix) * Ci + 8 * c8x) : 0u;
 #ifndef FB_KO_LOADS
         B.x[u] = fb_ldg4(a.x + imoff * Ci + off);
 #else
         B.x[u] = make_uint4(0, 0, 0, 0);
 #endif
-        B.dx[u] = valid ? (((cx.hy * fg.HWD + cx.hx) * fg.px + 8 * c8) << 5 | c8 << 2 | (in ? 2 : 0)) : -1;
-        advance(cx, sx, C8x);
+        B.dx[u] = valid ? (((cx.hy * fg.HWD + cx.hx) * fg.px + 8 * c8x) << 2 | (in ? 2 : 0)) : -1;
+        advance(cx, sx);
       }
     };
     const float xfloor = a.xrelu ? 0.f : -INFINITY;   // the prologue's ReLU (uniform: no per-channel table)
@@ -302,19 +309,19 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         const int d = B.dy[u];
         if (d < 0) continue;
         uint4 val = B.v[u];
-        if (BWD && (d & 1)) val = bwd8(val, B.w[u], s_bt + 8 * ((d >> 2) & 7), 64);
-        if (FWD && XPRO) val = xpro8(val, s_xt + 8 * ((d >> 2) & 7), xfloor);   // forward: BN(+ReLU) of x
+        if (BWD && try_) val = bwd8(val, B.w[u], cfy, 8);
+        if (FWD && XPRO) val = xpro8(val, cfy, xfloor);   // forward: BN(+ReLU) of x
         if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(tY + (d >> 5)) = val;
+        *reinterpret_cast<uint4*>(tY + (d >> 2)) = val;
       }
 #pragma unroll
       for (int u = 0; u < (FWD ? 0 : LDX); ++u) {
         const int d = B.dx[u];
         if (d < 0) continue;
         uint4 val = B.x[u];
-        if (XPRO) val = xpro8(val, s_xt + 8 * ((d >> 2) & 7), xfloor);
+        if (XPRO) val = xpro8(val, cfx, xfloor);
         if (!(d & 2)) val = make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(tX + (d >> 5)) = val;
+        *reinterpret_cast<uint4*>(tX + (d >> 2)) = val;
       }
     };
     Batch B0, B1;
