@@ -365,21 +365,25 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     const int p = (wave * NJ + j) * 16 + lr;
     pb[j] = ((p >> fg.tw_shift) * fg.HWD + (p & (fg.TW - 1))) * fg.py;   // + s_ub: tap offset - halo origin
   }
-  // weight-gradient transposed-read pixel rows: chunk pixel 8*lg + q (lo) and + 4 (hi), q = lr >> 2
+  // weight-gradient transposed reads: lane (lr, lg) reads chunk pixels plo / phi, channels 4 p4 .. + 3 (+ 16 i)
   const int q = lr >> 2, p4 = lr & 3;
-  const int plo = 8 * lg + q, phi = plo + 4;
-  // lane part of a chunk's transposed-read halo pixels (tile pixel plo; phi = plo + 4 is in the same tile row):
-  // element offsets in the dY / x tiles, and each weight-gradient unit's tap offset in the x tile
+  // The chunk's 32 pixels are the MFMA's k; any bijection works when the dY and x reads share it.  One
+  // ds_read_b64_tr_b16 serves 32 lanes per cycle = 8 pixels x 32 B: at an odd-16-B-slot pixel pitch (48 / 80 /
+  // 112 B) 8 pixels of ONE parity cover the 256-B bank row exactly once, mixed parities collide (PMC: bank
+  // conflict rate 0.39 with the consecutive mapping 8 lg + q).  So lanes 0-31 (lg 0, 1) take the even and lanes
+  // 32-63 the odd pixels of each 16-pixel half, and the second 8 k of a lane come from the other half (+ 16).
+  const int plo = 2 * (4 * (lg & 1) + q) + (lg >> 1), phi = plo + 16;
+  // lane part of a chunk's halo pixels: element offsets in the dY / x tiles (phi may be in the next tile row)
   const int Ly = (plo >> fg.tw_shift) * fg.HWD + (plo & (fg.TW - 1));
-  const int offYlo = Ly * fg.py + 4 * p4, offYhi = offYlo + 4 * fg.py;
-  const int offXlo = Ly * fg.px + 4 * p4, offXhi = offXlo + 4 * fg.px;
+  const int Lh = (phi >> fg.tw_shift) * fg.HWD + (phi & (fg.TW - 1));
+  const int offYlo = Ly * fg.py + 4 * p4, offYhi = Lh * fg.py + 4 * p4;
+  const int offXlo = Ly * fg.px + 4 * p4, offXhi = Lh * fg.px + 4 * p4;
   int swx[NT];
 #pragma unroll
   for (int m = 0; m < NT; ++m) {
     const int u = wt + kFbTapGroups * m;
     swx[m] = u < nWU ? s_wb[(GO2 && u >= T) ? a.t1 : u] * fg.px : 0;
   }
-  (void)phi;
 
   f32x4_t accw[NT][2][2];
 #pragma unroll
