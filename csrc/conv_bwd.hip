@@ -71,11 +71,13 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <int CW, int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false, bool FWD = false>
+// CB: 16-channel blocks of the data-gradient rows and of both weight-gradient operands: 2 (<= 32 channels, the
+// 17-channel level) or 3 (<= 48: the 34-channel level, Go = 1, CW = 4, 256-pixel tiles)
+template <int CW, int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false, bool FWD = false, int CB = 2>
 __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
   constexpr int kFbWaves = CW, kFbThreads = fb_threads(CW), kFbTapGroups = CW;
   extern __shared__ uint4 fb_smem[];
-  constexpr int MI = 2;                       // 32 data-gradient rows (input channels <= 32)
+  constexpr int MI = CB, CH = 16 * CB;        // data-gradient rows: input channels <= CH
   constexpr int NT = (kFbMaxT + 1 + kFbTapGroups - 1) / kFbTapGroups;   // weight-gradient units per wave
   constexpr int TP = kFbWaves * NJ * 16;      // pixels per tile
   constexpr int NCH = TP / 32;                // weight-gradient k chunks per tile
@@ -83,12 +85,12 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   const int pair = hpx * (fg.py + fg.px) + 2 * kFbSlack;   // elements of one dY + x buffer pair
   uint16_t* const lds0 = reinterpret_cast<uint16_t*>(fb_smem);
   const int wp = 32 * fg.KS + 8;                           // weight row pitch (elements; +16 B: bank spread)
-  uint16_t* const s_w = lds0 + 2 * pair;                   // [32 rows][wp] data-gradient weights, per block
-  float* s_stat = reinterpret_cast<float*>(s_w + 32 * wp);   // [waves][2][32]
+  uint16_t* const s_w = lds0 + 2 * pair;                   // [CH rows][wp] data-gradient weights, per block
+  float* s_stat = reinterpret_cast<float*>(s_w + CH * wp);   // [waves][2][CH]
   __shared__ float s_bt[BWD ? 5 * 64 : 1];    // dY rebuild table (stacked groups): scale, shift (+inf: no
                                               // ReLU), k1, k2, k3
-  __shared__ float s_xt[XPRO ? 3 * 32 : 1];   // x prologue: scale, shift, ReLU floor (0 / -inf)
-  __shared__ float s_bn[BNE ? 5 * 32 : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean,
+  __shared__ float s_xt[XPRO ? 2 * CH : 1];   // x prologue: scale, shift
+  __shared__ float s_bn[BNE ? 5 * CH : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean,
                                               // and (lds_y) 1 / prologue scale, -shift / scale - mean
   __shared__ int s_ldsy;
   __shared__ int s_ub[kFbMaxKS * 4];          // data-gradient unit -> dY tile offset
@@ -117,11 +119,10 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   }
   if constexpr (XPRO) {
     const int Cx = FWD ? Co : Ci;   // FWD: the prologue applies to the staged input (Co slots)
-    for (int c = tid; c < 32; c += kFbThreads) {
+    for (int c = tid; c < CH; c += kFbThreads) {
       const bool on = c < Cx;
       s_xt[c] = on ? a.xc[c] : 0.f;
-      s_xt[32 + c] = on ? a.xc[Cx + c] : 0.f;
-      s_xt[64 + c] = a.xrelu ? 0.f : -INFINITY;
+      s_xt[CH + c] = on ? a.xc[Cx + c] : 0.f;
     }
   }
   // unit e -> (tap t, stacked 8-channel slot c8): group 0 over every tap, then group 1 at its one tap t1
@@ -151,23 +152,23 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   if (tid == 0) s_ldsy = (BNE && XPRO && (const void*)a.bn_y == (const void*)a.x) ? 1 : 0;
   __syncthreads();
   if constexpr (BNE) {
-    for (int c = tid; c < 32; c += kFbThreads) {
+    for (int c = tid; c < CH; c += kFbThreads) {
       const bool on = c < Ci;
       s_bn[c] = on ? a.bn_coef[c] : 0.f;
-      s_bn[32 + c] = (on && a.bn_relu) ? a.bn_coef[Ci + c] : INFINITY;
-      s_bn[64 + c] = on ? a.bn_coef[2 * Ci + c] : 0.f;
+      s_bn[CH + c] = (on && a.bn_relu) ? a.bn_coef[Ci + c] : INFINITY;
+      s_bn[2 * CH + c] = on ? a.bn_coef[2 * Ci + c] : 0.f;
       if constexpr (XPRO) {
         const float sc = on ? a.xc[c] : 1.f, sh = on ? a.xc[Ci + c] : 0.f;
         const float inv = 1.f / sc;
-        s_bn[96 + c] = inv;
-        s_bn[128 + c] = on ? fmaf(-sh, inv, -a.bn_coef[2 * Ci + c]) : 0.f;
+        s_bn[3 * CH + c] = inv;
+        s_bn[4 * CH + c] = on ? fmaf(-sh, inv, -a.bn_coef[2 * Ci + c]) : 0.f;
         if (!(sc != 0.f) || !isfinite(inv)) s_ldsy = 0;   // (benign race: every writer stores 0)
       }
     }
   }
   {   // the data-gradient weights stay resident, in unit order: no global latency inside the k loop
     const int rowv = 4 * fg.KS;   // uint4 per row
-    for (int e = tid; e < 32 * rowv; e += kFbThreads) {
+    for (int e = tid; e < CH * rowv; e += kFbThreads) {
       const int r = e / rowv, u = e - r * rowv;
       const int pu = a.uperm[u];
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     }
   }
   if (BNE)
-    for (int c = tid; c < kFbWaves * 2 * 32; c += kFbThreads) s_stat[c] = 0.f;
+    for (int c = tid; c < kFbWaves * 2 * CH; c += kFbThreads) s_stat[c] = 0.f;
   __syncthreads();
 
   const int per_img = fg.tiles_y * fg.tiles_x;
@@ -250,12 +251,12 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         for (int e = 0; e < 8; ++e) cfy[8 * r + e] = s_bt[64 * r + 8 * c8y + e];
     } else if constexpr (FWD && XPRO) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { cfy[e] = s_xt[8 * c8y + e]; cfy[8 + e] = s_xt[32 + 8 * c8y + e]; }
+      for (int e = 0; e < 8; ++e) { cfy[e] = s_xt[8 * c8y + e]; cfy[8 + e] = s_xt[CH + 8 * c8y + e]; }
     }
     float cfx[(!FWD && XPRO) ? 16 : 1];
     if constexpr (!FWD && XPRO) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { cfx[e] = s_xt[8 * c8x + e]; cfx[8 + e] = s_xt[32 + 8 * c8x + e]; }
+      for (int e = 0; e < 8; ++e) { cfx[e] = s_xt[8 * c8x + e]; cfx[8 + e] = s_xt[CH + 8 * c8x + e]; }
     }
     Cursor cy{}, cx{};
     auto issue = [&](int k, int b, Batch& B) {
@@ -385,13 +386,13 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     swx[m] = u < nWU ? s_wb[(GO2 && u >= T) ? a.t1 : u] * fg.px : 0;
   }
 
-  f32x4_t accw[NT][2][2];
+  f32x4_t accw[NT][CB][CB];
 #pragma unroll
   for (int m = 0; m < NT; ++m)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < CB; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) accw[m][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < CB; ++j) accw[m][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float cs[MI][4], cq[MI][4];   // BN1 partials (BNE), over the block's tiles
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       for (int i = 0; i < MI; ++i) wrow[i] = s_w + (16 * i + lr) * wp + 8 * lg;
       // BN1: this tile's y1 at the output pixels; the first row block's loads go out ahead of the k loop
       // (their latency under the MFMAs), the second's ahead of the first block's epilogue
-      uint2 yy[MI][NJ];
+      uint2 yy[2][NJ];   // row blocks i and i + 1 (a ring: at most two in flight)
       // per-image element offset of column j's output pixel (-1: outside the image; one image < 2^31 elements)
       auto pix = [&](int j) -> int {
         const int p = (wave * NJ + j) * 16 + lr;
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int pm = pix(j);
-          yy[i][j] = (pm >= 0 && 16 * i + 4 * lg < Ci) ? *reinterpret_cast<const uint2*>(bny_im + pm + 16 * i + 4 * lg)
+          yy[i & 1][j] = (pm >= 0 && 16 * i + 4 * lg < Ci) ? *reinterpret_cast<const uint2*>(bny_im + pm + 16 * i + 4 * lg)
                                                        : make_uint2(0, 0);
         }
       };
@@ -466,9 +467,9 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (BNE) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            sc[r] = lds_y ? s_bn[96 + cb + r] : s_bn[cb + r];
-            sh[r] = s_bn[32 + cb + r];
-            mu[r] = lds_y ? s_bn[128 + cb + r] : s_bn[64 + cb + r];
+            sc[r] = lds_y ? s_bn[3 * CH + cb + r] : s_bn[cb + r];
+            sh[r] = s_bn[CH + cb + r];
+            mu[r] = lds_y ? s_bn[4 * CH + cb + r] : s_bn[2 * CH + cb + r];
           }
         }
 #pragma unroll
@@ -509,8 +510,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
                 cq[i][r] += gr * fmaf(x4[r], sc[r], mu[r]);
               }
             } else {
-              const float y4[4] = {__uint_as_float(yy[i][j].x << 16), __uint_as_float(yy[i][j].x & 0xffff0000u),
-                                   __uint_as_float(yy[i][j].y << 16), __uint_as_float(yy[i][j].y & 0xffff0000u)};
+              const float y4[4] = {__uint_as_float(yy[i & 1][j].x << 16), __uint_as_float(yy[i & 1][j].x & 0xffff0000u),
+                                   __uint_as_float(yy[i & 1][j].y << 16), __uint_as_float(yy[i & 1][j].y & 0xffff0000u)};
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float gr = fmaf(y4[r], sc[r], sh[r]) > 0.f ? g4[r] : 0.f;
@@ -535,9 +536,9 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       const int S = (((32 * s) >> fg.tw_shift) - fg.ey0) * fg.HWD + ((32 * s) & (fg.TW - 1)) - fg.ex0;
       const uint16_t* const y0 = tY + S * fg.py;
       const uint16_t* const x0 = tX + S * fg.px;
-      uint4 fa[2];
+      uint4 fa[CB];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < CB; ++i) {
         const uint2 lo = fb_tr_read(y0 + offYlo + 16 * i);
         const uint2 hi = fb_tr_read(y0 + offYhi + 16 * i);
         fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (u >= nWU) break;   // wave-uniform
         if (GO2 && u >= T) {   // the second group's dY columns; its unit is the wave's last, so fa is overwritten
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
+          for (int i = 0; i < CB; ++i) {
             const uint2 lo = fb_tr_read(y0 + offYlo + Co + 16 * i);
             const uint2 hi = fb_tr_read(y0 + offYhi + Co + 16 * i);
             fa[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -556,12 +557,12 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         }
         const uint16_t* const xb = x0 + swx[m];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < CB; ++j) {
           const uint2 lo = fb_tr_read(xb + offXlo + 16 * j);
           const uint2 hi = fb_tr_read(xb + offXhi + 16 * j);
           const uint4 fb = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) accw[m][i][j] = mfma16x16x32(fa[i], fb, accw[m][i][j]);
+          for (int i = 0; i < CB; ++i) accw[m][i][j] = mfma16x16x32(fa[i], fb, accw[m][i][j]);
         }
       }
     }
@@ -577,8 +578,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       for (int r = 0; r < 4; ++r) {
         const float s2 = row16_sum(cs[i][r]), q2 = row16_sum(cq[i][r]);
         if (lr == 0 && cb + r < Ci) {
-          s_stat[(wave * 2 + 0) * 32 + cb + r] = s2;
-          s_stat[(wave * 2 + 1) * 32 + cb + r] = q2;
+          s_stat[(wave * 2 + 0) * CH + cb + r] = s2;
+          s_stat[(wave * 2 + 1) * CH + cb + r] = q2;
         }
       }
     }
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     for (int c = tid; c < Ci; c += 64 * kFbWaves) {   // (compute waves only: the staging waves have left)
       float s2 = 0.f, q2 = 0.f;
 #pragma unroll
-      for (int wv = 0; wv < kFbWaves; ++wv) { s2 += s_stat[(wv * 2 + 0) * 32 + c]; q2 += s_stat[(wv * 2 + 1) * 32 + c]; }
+      for (int wv = 0; wv < kFbWaves; ++wv) { s2 += s_stat[(wv * 2 + 0) * CH + c]; q2 += s_stat[(wv * 2 + 1) * CH + c]; }
       a.stat_part[((long)blockIdx.x * 2 + 0) * Ci + c] = s2;
       a.stat_part[((long)blockIdx.x * 2 + 1) * Ci + c] = q2;
     }
@@ -600,9 +601,9 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
     if (u >= nWU) break;
     const int g = (GO2 && u >= T) ? 1 : 0, t = g ? a.t1 : u;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < CB; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < CB; ++j) {
         const int ci = 16 * j + lr;
         if (ci >= Ci) continue;
 #pragma unroll
@@ -659,7 +660,7 @@ size_t fb_pair_lds(const FusedBwdGeom& fg) {
 }
 
 size_t fb_lds(const FusedBwdGeom& fg) {
-  return 2 * fb_pair_lds(fg) + (size_t)32 * (32 * fg.KS + 8) * 2 + (size_t)fg.cw * 2 * 32 * 4;
+  return 2 * fb_pair_lds(fg) + (size_t)16 * fg.cb * (32 * fg.KS + 8) * 2 + (size_t)fg.cw * 2 * 16 * fg.cb * 4;
 }
 
 }  // namespace
@@ -671,7 +672,10 @@ size_t fb_lds(const FusedBwdGeom& fg) {
 static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
   // Go == 2: the ResidualBlock's 3x3 + 1x1 pair (the 1x1 at one tap of the 3x3's grid, FusedBwdArgs::t1)
   if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > (fwd ? 1 : 2) || g.OH != g.IH || g.OW != g.IW) return false;
-  if (g.Cgi > 32 || g.Cgo > 32 || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2) return false;
+  // <= 32 channels: 2 sixteen-channel blocks; <= 48 (the 34-channel level): 3, one output group only
+  const int cb = std::max(g.Cgi, g.Cgo) > 32 ? 3 : 2;
+  if (g.Cgi > 48 || g.Cgo > 48 || (cb == 3 && g.Go != 1) || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2)
+    return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
   for (int t = 0; t < g.T; ++t) {
     bool mirrored = false;
@@ -692,14 +696,17 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
     force_cw = e == nullptr ? 0 : atoi(e);
   }
   for (int tp = 512; tp >= 256; tp /= 2) {
-    const int cw = tp == 256 ? 4 : (force_cw == 4 || force_cw == 8 ? force_cw : (g.Go == 1 ? 8 : 4));
+    // (cb 3 backward: the 9 x 4 weight-gradient accumulators of 3 units need the 256-register budget of CW 4)
+    const int cw = (tp == 256 || (cb == 3 && !fwd)) ? 4
+                   : (force_cw == 4 || force_cw == 8 ? force_cw : (g.Go == 1 ? 8 : 4));
     const int nj = tp / (16 * cw);
+    if (cb == 3 && !fwd && tp == 512) continue;   // (never fits the LDS; no instantiation)
     for (int tw = 16; tw <= 64; tw *= 2) {
       const int th = tp / tw;
       FusedBwdGeom c{};
       c.TH = th; c.TW = tw; c.tw_shift = tw == 16 ? 4 : (tw == 32 ? 5 : 6);
       c.HH = th + ey1 - ey0; c.HWD = tw + ex1 - ex0; c.ey0 = ey0; c.ex0 = ex0;
-      c.py = py; c.px = px; c.KS = KS; c.nj = nj; c.cw = cw;
+      c.py = py; c.px = px; c.KS = KS; c.nj = nj; c.cw = cw; c.cb = cb;
       if (fb_lds(c) > (size_t)kFbMaxLds) continue;
       const double tiles = (double)((g.OH + th - 1) / th) * ((g.OW + tw - 1) / tw);
       const double cost = tiles * ((double)c.HH * c.HWD * (C8y + C8x) + 0.25 * tp * (C8x + C8y));
@@ -741,23 +748,25 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
   const size_t lds = fb_lds(fg);
   const bool bwd = a.gy != nullptr || a.gy2 != nullptr, xpro = a.xc != nullptr, bne = a.bn_y != nullptr;
-#define FB_(CW_, NJ_, B_, X_, E_, G_)                                                                       \
-  if (fg.cw == CW_ && fg.nj == NJ_ && bwd == B_ && xpro == X_ && bne == E_ && (g.Go == 2) == G_) {           \
+#define FB_(CW_, NJ_, B_, X_, E_, G_, CB_)                                                                  \
+  if (fg.cw == CW_ && fg.nj == NJ_ && fg.cb == CB_ && bwd == B_ && xpro == X_ && bne == E_ && (g.Go == 2) == G_) { \
     static bool lds_attr = false;                                                                            \
     if (!lds_attr) {                                                                                         \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_>), \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                      \
+      (void)hipFuncSetAttribute(                                                                             \
+          reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_, false, CB_>),       \
+          hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                                            \
       lds_attr = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_>), dim3(grid), dim3(fb_threads(CW_)), lds, s, \
-                       a, fg);                                                                               \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, B_, X_, E_, G_, false, CB_>), dim3(grid),            \
+                       dim3(fb_threads(CW_)), lds, s, a, fg);                                                \
     return 0;                                                                                                \
   }
-#define FB4_(CW_, NJ_, B_, G_) FB_(CW_, NJ_, B_, false, false, G_) FB_(CW_, NJ_, B_, true, false, G_)             \
-                               FB_(CW_, NJ_, B_, false, true, G_) FB_(CW_, NJ_, B_, true, true, G_)
-  FB4_(8, 4, false, false) FB4_(8, 4, true, false) FB4_(8, 4, false, true) FB4_(8, 4, true, true)
-  FB4_(4, 8, false, false) FB4_(4, 8, true, false) FB4_(4, 4, false, false) FB4_(4, 4, true, false)
-  FB4_(4, 8, false, true) FB4_(4, 8, true, true) FB4_(4, 4, false, true) FB4_(4, 4, true, true)
+#define FB4_(CW_, NJ_, B_, G_, CB_) FB_(CW_, NJ_, B_, false, false, G_, CB_) FB_(CW_, NJ_, B_, true, false, G_, CB_) \
+                                    FB_(CW_, NJ_, B_, false, true, G_, CB_) FB_(CW_, NJ_, B_, true, true, G_, CB_)
+  FB4_(8, 4, false, false, 2) FB4_(8, 4, true, false, 2) FB4_(8, 4, false, true, 2) FB4_(8, 4, true, true, 2)
+  FB4_(4, 8, false, false, 2) FB4_(4, 8, true, false, 2) FB4_(4, 4, false, false, 2) FB4_(4, 4, true, false, 2)
+  FB4_(4, 8, false, true, 2) FB4_(4, 8, true, true, 2) FB4_(4, 4, false, true, 2) FB4_(4, 4, true, true, 2)
+  FB4_(4, 4, false, false, 3) FB4_(4, 4, true, false, 3)
 #undef FB4_
 #undef FB_
   return 8;
@@ -809,20 +818,21 @@ int conv_fwd_fused(const ConvArgs& ca, hipStream_t s) {
   const unsigned grid = (unsigned)std::min(fg.ntiles, kFusedBwdGrid);
   const size_t lds = fb_lds(fg);
   const bool xpro = a.xc != nullptr;
-#define FF_(CW_, NJ_, X_)                                                                                    \
-  if (fg.cw == CW_ && fg.nj == NJ_ && xpro == X_) {                                                          \
+#define FF_(CW_, NJ_, X_, CB_)                                                                               \
+  if (fg.cw == CW_ && fg.nj == NJ_ && fg.cb == CB_ && xpro == X_) {                                           \
     static bool lds_attr = false;                                                                            \
     if (!lds_attr) {                                                                                         \
       (void)hipFuncSetAttribute(                                                                             \
-          reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true>),    \
+          reinterpret_cast<const void*>(&conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true, CB_>), \
           hipFuncAttributeMaxDynamicSharedMemorySize, kFbMaxLds);                                            \
       lds_attr = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true>), dim3(grid),         \
+    hipLaunchKernelGGL((conv_bwd_fused_kernel<CW_, NJ_, false, X_, false, false, true, CB_>), dim3(grid),    \
                        dim3(fb_threads(CW_)), lds, s, a, fg);                                                \
     return 0;                                                                                                \
   }
-  FF_(8, 4, false) FF_(8, 4, true) FF_(4, 8, false) FF_(4, 8, true) FF_(4, 4, false) FF_(4, 4, true)
+  FF_(8, 4, false, 2) FF_(8, 4, true, 2) FF_(4, 8, false, 2) FF_(4, 8, true, 2) FF_(4, 4, false, 2) FF_(4, 4, true, 2)
+  FF_(8, 4, false, 3) FF_(8, 4, true, 3) FF_(4, 4, false, 3) FF_(4, 4, true, 3)
 #undef FF_
   return 8;
 }

@@ -326,7 +326,7 @@ struct FusedBwdArgs {
 };
 struct FusedBwdGeom {
   int TH, TW, tw_shift, HH, HWD, ey0, ex0, tiles_y, tiles_x, ntiles;
-  int py, px, KS, nj, cw;   // cw: compute waves (4 or 8, conv_bwd.hip)
+  int py, px, KS, nj, cw, cb;   // cw: compute waves (4 or 8), cb: 16-channel blocks (2 or 3) (conv_bwd.hip)
   float inv_c8y, inv_c8x, inv_hwd;   // fp32 reciprocals (fdiv) of the staging index math
 };
 bool conv_bwd_fused_plan(const ConvGeom& g, FusedBwdGeom& fg);

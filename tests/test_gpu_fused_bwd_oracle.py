@@ -7,7 +7,8 @@ Chain case of the DUCKNet L1 level (reference models/ducknet.py:95-96,144-179): 
     kernel rebuilds y1 from the staged x tile),
   * dY = bwd(dz2, y2) rebuilt from the deferred BN2 backward (bwd1 in csrc/common.h),
 for Go = 1 (3x3 at dilation 1 / 2 / 3, 1x7, 7x1) and Go = 2 (the ResidualBlock's 3x3 + 1x1 pair), padded
-widths 8 / 16 / 24 (17 real) / 32 channels, on grids of several tiles and blocks (MI355X only).
+widths 8 / 16 / 24 (17 real) / 32 channels and the 34-channel level's 40 / 48 (three 16-channel blocks), on grids
+of several tiles and blocks (MI355X only).
 
 The same kernel's FORWARD mode (``conv_fwd_fused``: the 17-channel level's forward convs) is scored the same way:
 y = conv(relu(BN(x))) (+ bias) against ``F.conv2d`` in fp32 and its BN-statistics partials against the sums of
@@ -39,6 +40,12 @@ CASES = [
     (2, 28, 44, 32, 32, (3, 3), 1, 1),
     (3, 40, 56, 17, 17, (3, 3), 1, 2),
     (2, 31, 47, 16, 16, (3, 3), 1, 2),
+    # 34-channel level (40 padded: three 16-channel blocks, 256-pixel tiles; the dilated halos do not fit the
+    # LDS at 40 channels and stay on the separate kernels)
+    (2, 36, 52, 34, 34, (3, 3), 1, 1),
+    (2, 44, 30, 34, 34, (7, 1), 1, 1),
+    (2, 28, 66, 34, 34, (1, 7), 1, 1),
+    (1, 30, 40, 40, 24, (3, 3), 1, 1),
 ]
 
 
@@ -150,6 +157,8 @@ FWD_CASES = [
     (2, 36, 52, 8, 24, (3, 3), (1, 1), 1, False, True),
     (2, 28, 44, 32, 17, (3, 3), (1, 1), 1, True, False),
     (1, 37, 41, 24, 32, (3, 3), (0, 0), 1, False, False),   # one-sided taps (valid-padding geometry, same size)
+    (2, 36, 52, 34, 34, (3, 3), (1, 1), 1, True, False),    # 34-channel level: three 16-channel blocks
+    (2, 30, 66, 34, 40, (1, 7), (0, 3), 1, True, True),
 ]
 
 
