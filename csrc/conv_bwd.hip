@@ -695,15 +695,18 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
     const char* e = getenv("MSP_FB_CW");
     force_cw = e == nullptr ? 0 : atoi(e);
   }
-  for (int tp = 512; tp >= 256; tp /= 2) {
+  // (128-pixel tiles: only the 34-channel level's dilated / wide halos, which fit no larger double buffer)
+  for (int tp = 512; tp >= (cb == 3 && !fwd ? 128 : 256); tp /= 2) {
+    if (tp == 128 && found) break;
     // (cb 3 backward: the 9 x 4 weight-gradient accumulators of 3 units need the 256-register budget of CW 4)
-    const int cw = (tp == 256 || (cb == 3 && !fwd)) ? 4
+    const int cw = (tp <= 256 || (cb == 3 && !fwd)) ? 4
                    : (force_cw == 4 || force_cw == 8 ? force_cw : (g.Go == 1 ? 8 : 4));
     const int nj = tp / (16 * cw);
     if (cb == 3 && !fwd && tp == 512) continue;   // (never fits the LDS; no instantiation)
     for (int tw = 16; tw <= 64; tw *= 2) {
       const int th = tp / tw;
       FusedBwdGeom c{};
+      if (th < 1) continue;
       c.TH = th; c.TW = tw; c.tw_shift = tw == 16 ? 4 : (tw == 32 ? 5 : 6);
       c.HH = th + ey1 - ey0; c.HWD = tw + ex1 - ex0; c.ey0 = ey0; c.ex0 = ex0;
       c.py = py; c.px = px; c.KS = KS; c.nj = nj; c.cw = cw; c.cb = cb;
@@ -766,7 +769,7 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   FB4_(8, 4, false, false, 2) FB4_(8, 4, true, false, 2) FB4_(8, 4, false, true, 2) FB4_(8, 4, true, true, 2)
   FB4_(4, 8, false, false, 2) FB4_(4, 8, true, false, 2) FB4_(4, 4, false, false, 2) FB4_(4, 4, true, false, 2)
   FB4_(4, 8, false, true, 2) FB4_(4, 8, true, true, 2) FB4_(4, 4, false, true, 2) FB4_(4, 4, true, true, 2)
-  FB4_(4, 4, false, false, 3) FB4_(4, 4, true, false, 3)
+  FB4_(4, 4, false, false, 3) FB4_(4, 4, true, false, 3) FB4_(4, 2, false, false, 3) FB4_(4, 2, true, false, 3)
 #undef FB4_
 #undef FB_
   return 8;

@@ -40,9 +40,10 @@ CASES = [
     (2, 28, 44, 32, 32, (3, 3), 1, 1),
     (3, 40, 56, 17, 17, (3, 3), 1, 2),
     (2, 31, 47, 16, 16, (3, 3), 1, 2),
-    # 34-channel level (40 padded: three 16-channel blocks, 256-pixel tiles; the dilated halos do not fit the
-    # LDS at 40 channels and stay on the separate kernels)
+    # 34-channel level (40 padded: three 16-channel blocks, 256-pixel tiles; the dilated halos in 128-pixel ones)
     (2, 36, 52, 34, 34, (3, 3), 1, 1),
+    (2, 30, 44, 34, 34, (3, 3), 2, 1),
+    (1, 45, 38, 34, 34, (3, 3), 3, 1),
     (2, 44, 30, 34, 34, (7, 1), 1, 1),
     (2, 28, 66, 34, 34, (1, 7), 1, 1),
     (1, 30, 40, 40, 24, (3, 3), 1, 1),
