@@ -389,7 +389,11 @@ WgPlan wg_plan(const ConvGeom& g, bool pro) {
   w.n_k = cdiv(w.KT, 32 * c.wn * c.fn);
   w.nstages = (int)((w.M + kBP - 1) / kBP);
   const long ntile = (long)w.n_co * w.n_k;
-  long ns = std::max(1L, std::min((long)w.nstages, g_wg_blocks / std::max(1L, ntile)));
+  // grid target: two rounds of resident blocks -- 8-wave tiles hold one block per CU (96-128 KB of LDS), so
+  // half the 4-wave configs' target: every extra split is one more fp32 dW slab for unpack_wgrad to sum
+  // (round 5: with the 1024 target the 8-wave tiles doubled smp-Unet R101's unpack time, 2.2 -> 5.1 ms/step)
+  const long target = c.wm * c.wn >= 8 ? g_wg_blocks / 2 : g_wg_blocks;
+  long ns = std::max(1L, std::min((long)w.nstages, target / std::max(1L, ntile)));
   w.stages_per_split = (int)((w.nstages + ns - 1) / ns);
   ns = (w.nstages + w.stages_per_split - 1) / w.stages_per_split;   // no empty splits
   p.nsplit = (int)ns;
