@@ -837,6 +837,31 @@ void gconv_dgrad_t(const at::Tensor& g, const at::Tensor& w, const at::Tensor& d
   TORCH_CHECK(rc == 0, "gconv_dgrad: no instantiation");
 }
 
+// x: the source map (fwd: x [N, IH, IW, C]; trans: dY [N, OH, OW, C]), y: the output map
+void gconv_mfma_t(const at::Tensor& x, const at::Tensor& wpk, const at::Tensor& y, int64_t KW, int64_t stride,
+                  bool trans, std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  CHECK_BF16(x); CHECK_BF16(y); CHECK_BF16(wpk);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3), "gconv_mfma: NHWC maps");
+  const int C = x.size(3), T = dy.size();
+  TORCH_CHECK(C % 16 == 0 && T == 9 && dx.size() == dy.size() && (KW == 16 || KW == 32 || KW == 64), "gconv_mfma: C % 16, 3x3, KW");
+  const int64_t nst = (9 * KW + 31) / 32;
+  TORCH_CHECK(wpk.numel() == (int64_t)(C / 16) * nst * 64 * 8, "gconv_mfma: wpk [C/16][nst][64][8]");
+  const at::Tensor& xi = trans ? y : x;   // input-space map
+  const at::Tensor& yo = trans ? x : y;   // output-space map
+  // shape contract the kernel indexes with: output-space size from the taps / stride (host-checked)
+  int lo_y = 0, hi_y = 0, lo_x = 0, hi_x = 0;
+  for (int t = 0; t < T; ++t) { lo_y = std::min(lo_y, (int)dy[t]); hi_y = std::max(hi_y, (int)dy[t]);
+                                lo_x = std::min(lo_x, (int)dx[t]); hi_x = std::max(hi_x, (int)dx[t]); }
+  TORCH_CHECK(yo.size(1) == (xi.size(1) - lo_y - hi_y - 1) / stride + 1 &&
+              yo.size(2) == (xi.size(2) - lo_x - hi_x - 1) / stride + 1,
+              "gconv_mfma: output size does not match the taps / stride");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = gconv_mfma(bf(x), bf(wpk), bf(y), xi.size(0), xi.size(1), xi.size(2), yo.size(1), yo.size(2), C,
+                            (int)KW, (int)stride, trans, T, ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "gconv_mfma: no instantiation");
+}
+
 int64_t gconv_wgrad_slices_t(int64_t P, int64_t C, int64_t CG, int64_t T) { return gconv_wgrad_slices(P, C, CG, T); }
 
 void gconv_wgrad_t(const at::Tensor& x, const at::Tensor& g, const at::Tensor& part, int64_t CG, int64_t stride,
@@ -1069,6 +1094,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gconv_dgrad", &gconv_dgrad_t);
   m.def("gconv_wgrad_slices", &gconv_wgrad_slices_t);
   m.def("gconv_wgrad", &gconv_wgrad_t);
+  m.def("gconv_mfma", &gconv_mfma_t);
   m.def("aug_gray_scratch_doubles", &aug_gray_scratch_doubles);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),

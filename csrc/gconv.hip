@@ -188,6 +188,85 @@ __global__ __launch_bounds__(kBlock) void gconv_wgrad_kernel(const uint16_t* __r
       *reinterpret_cast<float4*>(o + e * 8 + k) = make_float4(acc[e][k], acc[e][k + 1], acc[e][k + 2], acc[e][k + 3]);
 }
 
+// ---- MFMA path (round 5): forward and data-gradient on the matrix cores ----------------------------------
+// The grouped conv as a dense GEMM over a KW-channel window (KW = max(16, CG): the 16-output-channel block
+// of an MFMA tile reads exactly that window) with BLOCK-DIAGONAL weights -- the off-group entries are zero
+// and cost MFMA cycles only, which the short per-group reduction (CG x 9 = 36..576) leaves to spare: the
+// VALU kernels above were compute-bound at ~14 TFLOP/s (profiles/r04/kernels_smp_unet_resnext50_bs64.txt).
+// One wave = one 16-channel output block x NCH chunks of 16 pixels; v_mfma_f32_16x16x32_bf16 with
+//   A = weights [16 out][32 k] (k = tap * KW + window channel; pre-packed per lane by ops/gconv.py),
+//   B = activations [32 k][16 px]: lane l loads pixel l % 16, k-slot l / 16 = 8 window channels of one tap,
+//       ONE 16-B global vector (NHWC), zero outside the image / for the padding taps,
+//   D = [16 out][16 px]: lane l holds 4 consecutive channels of pixel l % 16 -> one 8-B store.
+// TRANS: the data-gradient (output pixels are input-space pixels; tap t reads dY at (p - d_t) / stride where
+// that divides exactly).  Weights stay in VGPRs (NST x 4) across the wave's chunks.
+constexpr int kGmT = 9;
+constexpr int kGmNch = 4;
+
+template <int KW, bool TRANS>
+__global__ __launch_bounds__(256) void gconv_mfma_kernel(const uint16_t* __restrict__ x, const uint4* __restrict__ wpk,
+                                                         uint16_t* __restrict__ y, int N, int IH, int IW, int OH,
+                                                         int OW, int C, int stride, GTaps tp) {
+  constexpr int NST = (kGmT * KW + 31) / 32;
+  const int lane = threadIdx.x & 63, q = lane >> 4, pl = lane & 15;
+  const int nob = C >> 4;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ob = (int)(gw % nob);
+  const long pc = gw / nob;
+  // output / source geometry: fwd reads x [N, IH, IW] for outputs [N, OH, OW]; TRANS reads dY [N, OH, OW]
+  // for outputs dX [N, IH, IW]
+  const int PH = TRANS ? IH : OH, PW = TRANS ? IW : OW, SH = TRANS ? OH : IH, SW = TRANS ? OW : IW;
+  const long P = (long)N * PH * PW;
+  if (pc * 16 * kGmNch >= P) return;
+  const int co0 = 16 * ob, g0w = (co0 / KW) * KW;
+  uint4 a[NST];
+#pragma unroll
+  for (int s = 0; s < NST; ++s) a[s] = wpk[((long)ob * NST + s) * 64 + lane];
+#pragma unroll 1
+  for (int ch = 0; ch < kGmNch; ++ch) {
+    const long p = (pc * kGmNch + ch) * 16 + pl;
+    const bool pin = p < P;
+    const long pp = pin ? p : 0;
+    const int ox = (int)(pp % PW);
+    const long r = pp / PW;
+    const int oy = (int)(r % PH);
+    const long n = r / PH;
+    const uint16_t* src = x + n * SH * SW * C + g0w;
+    uint4 b[NST];
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      const int k0 = 32 * s + 8 * q;
+      const int tap = k0 / KW, cl = k0 % KW;
+      const int tA = (32 * s) / KW;
+      const int tB = tA + 1 < kGmT ? tA + 1 : kGmT - 1;
+      const int ddy = tap == tA ? tp.dy[tA < kGmT ? tA : kGmT - 1] : tp.dy[tB];
+      const int ddx = tap == tA ? tp.dx[tA < kGmT ? tA : kGmT - 1] : tp.dx[tB];
+      bool ok = pin && tap < kGmT;
+      int sy, sx;
+      if (!TRANS) {
+        sy = oy * stride + ddy;
+        sx = ox * stride + ddx;
+      } else {
+        const int ry = oy - ddy, rx = ox - ddx;
+        sy = ry / stride;
+        sx = rx / stride;
+        ok = ok && ry >= 0 && rx >= 0 && sy * stride == ry && sx * stride == rx;
+      }
+      ok = ok && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+      b[s] = ok ? *reinterpret_cast<const uint4*>(src + ((long)sy * SW + sx) * C + cl) : make_uint4(0, 0, 0, 0);
+    }
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NST; ++s) acc = mfma16x16x32(a[s], b[s], acc);
+    if (pin) {
+      uint2 o;
+      o.x = pack2(acc[0], acc[1]);
+      o.y = pack2(acc[2], acc[3]);
+      *reinterpret_cast<uint2*>(y + p * C + co0 + 4 * q) = o;
+    }
+  }
+}
+
 GTaps make_taps(int T, const int* dyv, const int* dxv) {
   GTaps tp{};
   tp.T = T;
@@ -240,3 +319,23 @@ int gconv_wgrad(const uint16_t* x, const uint16_t* dy, float* part, int nslice, 
   GC_DISPATCH_(gconv_wgrad_kernel, grid, dim3(kBlock), 0, s, x, dy, part, N, IH, IW, OH, OW, C, stride, tp, nslice)
 }
 #undef GC_DISPATCH_
+
+// wpk: [C/16][NST][64 lanes] uint4 (ops/gconv.py _mfma_pack); KW = max(16, CG); TRANS: the data-gradient
+// (x = dY [N, OH, OW, C], y = dX [N, IH, IW, C]).  Returns 1 when no instantiation fits (caller falls back).
+int gconv_mfma(const uint16_t* x, const uint16_t* wpk, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C,
+               int KW, int stride, bool trans, int T, const int* dyv, const int* dxv, hipStream_t s) {
+  if (T != kGmT || C % 16 != 0) return 1;
+  const GTaps tp = make_taps(T, dyv, dxv);
+  const long P = trans ? (long)N * IH * IW : (long)N * OH * OW;
+  const long waves = (long)(C / 16) * ((P + 16 * kGmNch - 1) / (16 * kGmNch));
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  const uint4* w = reinterpret_cast<const uint4*>(wpk);
+#define GM_(KWV, TR) hipLaunchKernelGGL((gconv_mfma_kernel<KWV, TR>), grid, dim3(256), 0, s, x, w, y, N, IH, IW, OH, OW, C, stride, tp)
+  switch (KW) {
+    case 16: if (trans) GM_(16, true); else GM_(16, false); return 0;
+    case 32: if (trans) GM_(32, true); else GM_(32, false); return 0;
+    case 64: if (trans) GM_(64, true); else GM_(64, false); return 0;
+  }
+#undef GM_
+  return 1;
+}

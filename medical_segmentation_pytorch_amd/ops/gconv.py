@@ -2,14 +2,61 @@
 ``Bottleneck.conv2``, groups 32) inside the fused graph -- the last conv that used to run on MIOpen.
 
 NHWC bf16 maps with C % 8 == 0 (unpadded: ResNeXt widths are multiples of 8); fp32 weights repacked to
-[T][C][CG] per call.  The weight gradient is reduced over pixel slices in a fixed order (``colsum``):
+[T][C][CG] per call.  3x3 convs with C % 16 == 0 and 4 <= CG <= 64 run forward and data-gradient on the MFMA
+kernel (``gconv_mfma``: block-diagonal weights over a max(16, CG)-channel window, packed per MFMA lane by
+``_mfma_pack``); env MSP_GCONV_MFMA=0 keeps the VALU kernels (A/B).  The weight gradient is reduced over pixel slices in a fixed order (``colsum``):
 bitwise deterministic.  Reference: models/__init__.py:8-10 (smp encoders, resnext50_32x4d).
 """
 from __future__ import annotations
 
+import os
+
+import numpy as np
 import torch
 
 from ._ext import require
+
+_MFMA = os.environ.get('MSP_GCONV_MFMA', '1') != '0'
+_PACK_IDX = {}
+
+
+def _mfma_ok(C, CG, T):
+    # CG >= 4: ResNeXt's groups (depthwise / CG 2 stay on the VALU kernels: 1/16 - 1/8 of the MFMA work useful)
+    return _MFMA and T == 9 and C % 16 == 0 and 4 <= CG <= 64
+
+
+def _mfma_pack_index(C, CG, T, trans, device):
+    """Gather index into [T*C*CG + 1] (the last slot a zero) building the MFMA A operands: [C/16][NST][64][8]
+    with lane l = row l % 16 (output channel co = 16*ob + l % 16), k = 32*s + 8*(l // 16) + j -> tap k // KW,
+    window channel (co // KW) * KW + k % KW; block-diagonal (other groups and padding taps read the zero).
+    fwd: w[tap][co][cin - g(co)]; trans (data-gradient, output channel = an input channel ci): w[tap][cin][ci - g(ci)]."""
+    key = (C, CG, T, trans, str(device))
+    idx = _PACK_IDX.get(key)
+    if idx is None:
+        KW = max(16, CG)
+        nst = (T * KW + 31) // 32
+        ob = np.arange(C // 16).reshape(-1, 1, 1, 1)
+        st = np.arange(nst).reshape(1, -1, 1, 1)
+        ln = np.arange(64).reshape(1, 1, -1, 1)
+        j = np.arange(8).reshape(1, 1, 1, -1)
+        co = 16 * ob + ln % 16
+        k = 32 * st + 8 * (ln // 16) + j
+        tap = k // KW
+        cin = (co // KW) * KW + k % KW
+        ok = (tap < T) & (cin // CG == co // CG)
+        if trans:
+            flat = tap * C * CG + cin * CG + (co - (co // CG) * CG)
+        else:
+            flat = tap * C * CG + co * CG + (cin - (cin // CG) * CG)
+        flat = np.where(ok, flat, T * C * CG)
+        idx = torch.from_numpy(flat.reshape(-1).astype(np.int64)).to(device)
+        _PACK_IDX[key] = idx
+    return idx
+
+
+def _mfma_pack(wp, C, CG, T, trans):
+    flat = torch.cat([wp.reshape(-1), wp.new_zeros(1)])
+    return flat[_mfma_pack_index(C, CG, T, trans, wp.device)].to(torch.bfloat16)
 
 
 def _taps(conv):
@@ -37,7 +84,10 @@ class _GConv(torch.autograd.Function):
         wp = weight.detach().float().reshape(Cc, CG, T).permute(2, 0, 1).contiguous()
         oh, ow = _out_size(H, kh, sh, ph, dh), _out_size(W, kw, sw, pw, dw)
         y = torch.empty(N, oh, ow, Cc, dtype=torch.bfloat16, device=x.device)
-        C.gconv_fwd(x, wp, y, CG, sh, dy, dx)
+        if _mfma_ok(Cc, CG, T):
+            C.gconv_mfma(x, _mfma_pack(wp, Cc, CG, T, False), y, max(16, CG), sh, False, dy, dx)
+        else:
+            C.gconv_fwd(x, wp, y, CG, sh, dy, dx)
         ctx.save_for_backward(x, wp)
         ctx.cfg = (kh, kw, sh, CG, T, dy, dx)
         return y
@@ -52,7 +102,10 @@ class _GConv(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            C.gconv_dgrad(g, wp, gx, CG, stride, dy, dx)
+            if _mfma_ok(Cc, CG, T):
+                C.gconv_mfma(g, _mfma_pack(wp, Cc, CG, T, True), gx, max(16, CG), stride, True, dy, dx)
+            else:
+                C.gconv_dgrad(g, wp, gx, CG, stride, dy, dx)
         gw = None
         if ctx.needs_input_grad[1]:
             P = N * g.shape[1] * g.shape[2]

@@ -777,7 +777,8 @@ def test_parked_gradient_aliasing_its_own_dy_is_not_overwritten(gpu):
 
 
 @pytest.mark.parametrize('c,groups,stride', [(128, 32, 1), (64, 32, 2), (256, 32, 1), (512, 32, 2), (1024, 32, 1),
-                                             (64, 8, 1), (48, 48, 1), (192, 192, 2), (96, 96, 2), (96, 96, 1)])
+                                             (64, 8, 1), (48, 48, 1), (192, 192, 2), (96, 96, 2), (96, 96, 1),
+                                             (256, 4, 1), (128, 2, 2), (96, 6, 1), (96, 6, 2)])
 def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
     """HIP grouped 3x3 (csrc/gconv.hip; ResNeXt conv2, CG = 4..32 channels per group, stride 1 / 2) vs the
     fp32 PyTorch conv on the same bf16 inputs: output, input gradient and weight gradient."""
@@ -798,6 +799,28 @@ def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
     assert _rel(xf.grad.permute(0, 3, 1, 2), xr.grad) < 1e-2
     assert _rel(m.weight.grad, wr.grad) < 1e-3
+
+
+@pytest.mark.parametrize('c,groups,stride', [(128, 32, 1), (256, 32, 2), (1024, 32, 2), (256, 4, 1)])
+def test_grouped_conv_mfma_matches_valu(gpu, c, groups, stride, monkeypatch):
+    """The MFMA grouped 3x3 (gconv_mfma: block-diagonal weights over a max(16, CG) window) against the VALU
+    kernels on the same bf16 inputs: both accumulate in fp32, so outputs and input gradients agree to bf16
+    rounding; the MFMA path is the one the ResNeXt shapes take."""
+    from medical_segmentation_pytorch_amd.ops import gconv as G
+    torch.manual_seed(9)
+    m = nn.Conv2d(c, c, 3, stride, 1, groups=groups, bias=False).to(gpu)
+    x = torch.randn(3, 13, 21, c, device=gpu).to(torch.bfloat16)
+    assert G._mfma_ok(c, c // groups, 9)
+    out = []
+    for mfma in (True, False):
+        monkeypatch.setattr(G, '_MFMA', mfma)
+        xf = x.clone().requires_grad_(True)
+        y = G.gconv(xf, m)
+        g = torch.randn_like(y, dtype=torch.float32).mul(0.5).to(torch.bfloat16) if not out else out[0][2]
+        y.backward(g)
+        out.append((y.detach().float(), xf.grad.float(), g))
+    assert _rel(out[0][0], out[1][0]) < 5e-3
+    assert _rel(out[0][1], out[1][1]) < 5e-3
 
 
 def test_relu6_forward_backward(gpu):
