@@ -862,6 +862,28 @@ void gconv_mfma_t(const at::Tensor& x, const at::Tensor& wpk, const at::Tensor& 
   TORCH_CHECK(rc == 0, "gconv_mfma: no instantiation");
 }
 
+int64_t gconv_wgrad_mfma_slices_t(int64_t P, int64_t C) { return gconv_wgrad_mfma_slices(P, C); }
+
+void gconv_wgrad_mfma_t(const at::Tensor& x, const at::Tensor& g, const at::Tensor& part, int64_t KW, int64_t stride,
+                        std::vector<int64_t> dy, std::vector<int64_t> dx) {
+  CHECK_BF16(x); CHECK_BF16(g); CHECK_F32(part);
+  TORCH_CHECK(x.dim() == 4 && g.dim() == 4 && x.size(0) == g.size(0) && x.size(3) == g.size(3), "gconv_wgrad_mfma: NHWC maps");
+  const int C = x.size(3), T = dy.size();
+  TORCH_CHECK(C % 16 == 0 && T == 9 && dx.size() == dy.size() && (KW == 16 || KW == 32 || KW == 64), "gconv_wgrad_mfma: C % 16, 3x3, KW");
+  const int64_t row = (int64_t)(C / 16) * (9 * KW / 16) * 256;
+  TORCH_CHECK(part.numel() % row == 0 && part.numel() / row >= 1, "gconv_wgrad_mfma: part [S][C/16][9*KW/16][256]");
+  int lo_y = 0, hi_y = 0, lo_x = 0, hi_x = 0;
+  for (int t = 0; t < T; ++t) { lo_y = std::min(lo_y, (int)dy[t]); hi_y = std::max(hi_y, (int)dy[t]);
+                                lo_x = std::min(lo_x, (int)dx[t]); hi_x = std::max(hi_x, (int)dx[t]); }
+  TORCH_CHECK(g.size(1) == (x.size(1) - lo_y - hi_y - 1) / stride + 1 && g.size(2) == (x.size(2) - lo_x - hi_x - 1) / stride + 1,
+              "gconv_wgrad_mfma: dY size does not match the taps / stride");
+  int ty[kMaxTaps], tx[kMaxTaps];
+  for (int t = 0; t < T; ++t) { ty[t] = dy[t]; tx[t] = dx[t]; }
+  const int rc = gconv_wgrad_mfma(bf(x), bf(g), f32(part), (int)(part.numel() / row), x.size(0), x.size(1), x.size(2),
+                                  g.size(1), g.size(2), C, (int)KW, (int)stride, T, ty, tx, cur_stream());
+  TORCH_CHECK(rc == 0, "gconv_wgrad_mfma: no instantiation");
+}
+
 int64_t gconv_wgrad_slices_t(int64_t P, int64_t C, int64_t CG, int64_t T) { return gconv_wgrad_slices(P, C, CG, T); }
 
 void gconv_wgrad_t(const at::Tensor& x, const at::Tensor& g, const at::Tensor& part, int64_t CG, int64_t stride,
@@ -1095,6 +1117,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gconv_wgrad_slices", &gconv_wgrad_slices_t);
   m.def("gconv_wgrad", &gconv_wgrad_t);
   m.def("gconv_mfma", &gconv_mfma_t);
+  m.def("gconv_wgrad_mfma", &gconv_wgrad_mfma_t);
+  m.def("gconv_wgrad_mfma_slices", &gconv_wgrad_mfma_slices_t);
   m.def("aug_gray_scratch_doubles", &aug_gray_scratch_doubles);
   m.def("bn_act_bwd_partial", &bn_act_bwd_partial_t);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),

@@ -267,6 +267,129 @@ __global__ __launch_bounds__(256) void gconv_mfma_kernel(const uint16_t* __restr
   }
 }
 
+// Weight gradient on MFMA: dW_blk[16 co][tap][KW window ch] = sum_p dY[p][co] * X[src(p, tap)][window ch]
+// (K = pixels; the block-diagonal entries are extracted on the host side, ops/gconv.py).  Block = one
+// 16-co block x one pixel slice; 64-pixel stages of dY [64][16] and the 9 gathered tap rows X_t [64][KW]
+// go through LDS in their NHWC row layout and feed the MFMA with ds_read_b64_tr_b16 (the transposed read:
+// a lane addresses 4 channels of one pixel, the 16-lane group receives 4 pixels per channel).  The next
+// stage's global loads are in flight during the current stage's MFMAs.  The 9*KW/16 output tiles are dealt
+// to the 4 waves; each slice writes its partial tiles to part[slice] (summed in slice order by colsum).
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+DEVI uint2 gm_tr_read(const uint16_t* p) {
+  s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t __attribute__((address_space(3)))*)(p));
+  union { s16x4_t s; uint2 u; } c; c.s = v; return c.u;
+}
+
+constexpr int kGwPx = 64;   // pixels per stage (KW <= 32)
+
+template <int KW>
+__global__ __launch_bounds__(256) void gconv_wgrad_mfma_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                               float* __restrict__ part, int N, int IH, int IW, int OH,
+                                                               int OW, int C, int stride, GTaps tp, long per) {
+  constexpr int NPX = KW == 64 ? 32 : kGwPx;      // pixels per stage (KW 64: the 9 tap rows fit 40 KB)
+  constexpr int NTI = kGmT * KW / 16;            // output tiles (tap, 16-ch sub-block of the window)
+  constexpr int TPW = (NTI + 3) / 4;             // tiles per wave
+  constexpr int PY = 16 + 4, PX = KW + 4;        // LDS row pitches (elements; 8-B aligned rows)
+  constexpr int XV = KW / 8;                     // 16-B vectors per X row
+  constexpr int NXS = (kGmT * NPX * XV + 255) / 256;   // X staging vectors per thread
+  __shared__ __attribute__((aligned(16))) uint16_t sY[NPX * PY];
+  __shared__ __attribute__((aligned(16))) uint16_t sX[kGmT * NPX * PX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, p4 = lr & 3;
+  const int ob = blockIdx.y, co0 = 16 * ob, g0w = (co0 / KW) * KW;
+  const long P = (long)N * OH * OW;
+  const long p0 = (long)blockIdx.x * per, p1 = p0 + per < P ? p0 + per : P;
+  const int nstage = p1 > p0 ? (int)((p1 - p0 + NPX - 1) / NPX) : 0;
+
+  uint4 vy = make_uint4(0, 0, 0, 0);
+  uint4 vx[NXS];
+  auto load = [&](int st) {
+    const long pb = p0 + (long)st * NPX;
+    if (tid < 2 * NPX) {   // dY: NPX px x 2 vectors
+      const long p = pb + (tid >> 1);
+      vy = p < p1 ? *reinterpret_cast<const uint4*>(dy + p * C + co0 + 8 * (tid & 1)) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < NXS; ++u) {
+      const int e = tid + 256 * u;   // (tap, px, vec)
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < kGmT * NPX * XV) {
+        const int t = e / (NPX * XV), r = e - t * (NPX * XV), px = r / XV, vv = r - px * XV;
+        const long p = pb + px;
+        if (p < p1) {
+          const int ox = (int)(p % OW);
+          const long rr = p / OW;
+          const int oy = (int)(rr % OH);
+          const long n = rr / OH;
+          const int iy = oy * stride + tp.dy[t < kGmT ? t : 0], ix = ox * stride + tp.dx[t < kGmT ? t : 0];
+          if ((unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW)
+            v = *reinterpret_cast<const uint4*>(x + ((n * IH + iy) * IW + ix) * C + g0w + 8 * vv);
+        }
+      }
+      vx[u] = v;
+    }
+  };
+  auto store = [&]() {
+    if (tid < 2 * NPX) {   // 8-B aligned rows: two 8-B halves
+      uint2* d = reinterpret_cast<uint2*>(&sY[(tid >> 1) * PY + 8 * (tid & 1)]);
+      d[0] = make_uint2(vy.x, vy.y);
+      d[1] = make_uint2(vy.z, vy.w);
+    }
+#pragma unroll
+    for (int u = 0; u < NXS; ++u) {
+      const int e = tid + 256 * u;
+      if (e < kGmT * NPX * XV) {
+        const int t = e / (NPX * XV), r = e - t * (NPX * XV), px = r / XV, vv = r - px * XV;
+        // two 8-B halves: PX rows are 8-B (not 16-B) aligned
+        uint2* d = reinterpret_cast<uint2*>(&sX[(t * NPX + px) * PX + 8 * vv]);
+        d[0] = make_uint2(vx[u].x, vx[u].y);
+        d[1] = make_uint2(vx[u].z, vx[u].w);
+      }
+    }
+  };
+
+  f32x4_t acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // per-lane transposed-read offsets within a 32-pixel k-step: pixels 8*lg + q (lo) and + 4 (hi), channels 4*p4
+  const int offYlo = (8 * lg + q) * PY + 4 * p4, offYhi = offYlo + 4 * PY;
+  int offX[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int ti = wave + 4 * j < NTI ? wave + 4 * j : 0;
+    const int t = ti / (KW / 16), c16 = ti % (KW / 16);
+    offX[j] = (t * NPX + 8 * lg + q) * PX + 16 * c16 + 4 * p4;
+  }
+  if (nstage > 0) load(0);
+  for (int st = 0; st < nstage; ++st) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (st + 1 < nstage) load(st + 1);
+#pragma unroll
+    for (int ks = 0; ks < NPX / 32; ++ks) {
+      const uint2 alo = gm_tr_read(&sY[ks * 32 * PY + offYlo]);
+      const uint2 ahi = gm_tr_read(&sY[ks * 32 * PY + offYhi]);
+      const uint4 a = make_uint4(alo.x, alo.y, ahi.x, ahi.y);
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const uint2 blo = gm_tr_read(&sX[ks * 32 * PX + offX[j]]);
+        const uint2 bhi = gm_tr_read(&sX[ks * 32 * PX + offX[j] + 4 * PX]);
+        acc[j] = mfma16x16x32(a, make_uint4(blo.x, blo.y, bhi.x, bhi.y), acc[j]);
+      }
+    }
+  }
+  // part[slice][ob][tile][16 co][16 ch]; D row (co) = 4*lg + r, column (ch) = lr
+  float* o = part + ((long)blockIdx.x * gridDim.y + ob) * NTI * 256;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int ti = wave + 4 * j;
+    if (ti >= NTI) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[ti * 256 + (4 * lg + r) * 16 + lr] = acc[j][r];
+  }
+}
+
 GTaps make_taps(int T, const int* dyv, const int* dxv) {
   GTaps tp{};
   tp.T = T;
@@ -337,5 +460,28 @@ int gconv_mfma(const uint16_t* x, const uint16_t* wpk, uint16_t* y, int N, int I
     case 64: if (trans) GM_(64, true); else GM_(64, false); return 0;
   }
 #undef GM_
+  return 1;
+}
+
+// part [nslice][C/16][9*KW/16][16][16] fp32 (summed over slices by colsum; the block diagonal is extracted by
+// ops/gconv.py).  3x3, C % 16 == 0, KW = max(16, CG) in {16, 32, 64}.
+int gconv_wgrad_mfma_slices(long P, int C) {
+  long s = std::max(1L, 1024L / std::max(1, C / 16));
+  s = std::min(s, std::max(1L, P / 256));   // >= 4 stages per slice
+  return (int)std::max(1L, std::min(s, 1024L));
+}
+
+int gconv_wgrad_mfma(const uint16_t* x, const uint16_t* dy, float* part, int nslice, int N, int IH, int IW, int OH,
+                     int OW, int C, int KW, int stride, int T, const int* dyv, const int* dxv, hipStream_t s) {
+  if (T != kGmT || C % 16 != 0) return 1;
+  const GTaps tp = make_taps(T, dyv, dxv);
+  const long P = (long)N * OH * OW;
+  const long per = (P + nslice - 1) / nslice;
+  const dim3 grid((unsigned)nslice, (unsigned)(C / 16));
+  switch (KW) {
+    case 16: hipLaunchKernelGGL((gconv_wgrad_mfma_kernel<16>), grid, dim3(256), 0, s, x, dy, part, N, IH, IW, OH, OW, C, stride, tp, per); return 0;
+    case 32: hipLaunchKernelGGL((gconv_wgrad_mfma_kernel<32>), grid, dim3(256), 0, s, x, dy, part, N, IH, IW, OH, OW, C, stride, tp, per); return 0;
+    case 64: hipLaunchKernelGGL((gconv_wgrad_mfma_kernel<64>), grid, dim3(256), 0, s, x, dy, part, N, IH, IW, OH, OW, C, stride, tp, per); return 0;
+  }
   return 1;
 }

@@ -353,6 +353,10 @@ int gconv_fwd(const uint16_t* x, const float* w, uint16_t* y, int N, int IH, int
 int gconv_dgrad(const uint16_t* dy, const float* w, uint16_t* dx, int N, int IH, int IW, int OH, int OW, int C, int CG,
                 int stride, int T, const int* dyv, const int* dxv, hipStream_t s);
 int gconv_wgrad_slices(long P, int C, int CG, int T);
+// MFMA weight-gradient: part [nslice][C/16][9*KW/16][16][16] (colsum over slices; block diagonal on the host)
+int gconv_wgrad_mfma_slices(long P, int C);
+int gconv_wgrad_mfma(const uint16_t* x, const uint16_t* dy, float* part, int nslice, int N, int IH, int IW, int OH,
+                     int OW, int C, int KW, int stride, int T, const int* dyv, const int* dxv, hipStream_t s);
 // MFMA forward / data-gradient (trans): wpk bf16 [C/16][ceil(9*KW/32)][64][8], KW = max(16, CG); 3x3 only
 int gconv_mfma(const uint16_t* x, const uint16_t* wpk, uint16_t* y, int N, int IH, int IW, int OH, int OW, int C,
                int KW, int stride, bool trans, int T, const int* dyv, const int* dxv, hipStream_t s);

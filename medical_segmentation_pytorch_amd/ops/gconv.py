@@ -4,7 +4,9 @@
 NHWC bf16 maps with C % 8 == 0 (unpadded: ResNeXt widths are multiples of 8); fp32 weights repacked to
 [T][C][CG] per call.  3x3 convs with C % 16 == 0 and 4 <= CG <= 64 run forward and data-gradient on the MFMA
 kernel (``gconv_mfma``: block-diagonal weights over a max(16, CG)-channel window, packed per MFMA lane by
-``_mfma_pack``); env MSP_GCONV_MFMA=0 keeps the VALU kernels (A/B).  The weight gradient is reduced over pixel slices in a fixed order (``colsum``):
+``_mfma_pack``) and so does the weight-gradient (``gconv_wgrad_mfma``: the dense 16-co x 9-tap x window
+tiles, reduced over pixel slices by ``colsum``, block diagonal gathered by ``_wgrad_diag_index``); env
+MSP_GCONV_MFMA=0 keeps the VALU kernels (A/B).  The weight gradient is reduced over pixel slices in a fixed order (``colsum``):
 bitwise deterministic.  Reference: models/__init__.py:8-10 (smp encoders, resnext50_32x4d).
 """
 from __future__ import annotations
@@ -50,6 +52,24 @@ def _mfma_pack_index(C, CG, T, trans, device):
             flat = tap * C * CG + co * CG + (cin - (cin // CG) * CG)
         flat = np.where(ok, flat, T * C * CG)
         idx = torch.from_numpy(flat.reshape(-1).astype(np.int64)).to(device)
+        _PACK_IDX[key] = idx
+    return idx
+
+
+def _wgrad_diag_index(C, CG, T, device):
+    """Gather index from the MFMA weight-gradient tiles red [C/16][T*KW/16][16 co][16 ch] (tile = tap * KW/16 +
+    16-ch sub-block of the co block's KW window) to dW [C][CG][T] (the block diagonal)."""
+    key = ('wg', C, CG, T, str(device))
+    idx = _PACK_IDX.get(key)
+    if idx is None:
+        KW = max(16, CG)
+        co = np.arange(C).reshape(-1, 1, 1)
+        cil = np.arange(CG).reshape(1, -1, 1)
+        t = np.arange(T).reshape(1, 1, -1)
+        wch = (co // CG) * CG + cil - (co // KW) * KW
+        tile = t * (KW // 16) + wch // 16
+        flat = (((co // 16) * (T * KW // 16) + tile) * 16 + co % 16) * 16 + wch % 16
+        idx = torch.from_numpy(np.broadcast_to(flat, (C, CG, T)).reshape(-1).astype(np.int64)).to(device)
         _PACK_IDX[key] = idx
     return idx
 
@@ -107,7 +127,16 @@ class _GConv(torch.autograd.Function):
             else:
                 C.gconv_dgrad(g, wp, gx, CG, stride, dy, dx)
         gw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and _mfma_ok(Cc, CG, T):
+            P = N * g.shape[1] * g.shape[2]
+            KW = max(16, CG)
+            S = C.gconv_wgrad_mfma_slices(P, Cc)
+            part = torch.empty(S, (Cc // 16) * (T * KW // 16) * 256, dtype=torch.float32, device=x.device)
+            C.gconv_wgrad_mfma(x, g, part, KW, stride, dy, dx)
+            red = torch.empty(part.shape[1], dtype=torch.float32, device=x.device)
+            C.colsum(part, red, False)
+            gw = red[_wgrad_diag_index(Cc, CG, T, x.device)].view(Cc, CG, kh, kw)
+        elif ctx.needs_input_grad[1]:
             P = N * g.shape[1] * g.shape[2]
             nib = CG // 8 if CG >= 8 else 1
             S = C.gconv_wgrad_slices(P, Cc, CG, T)

@@ -805,7 +805,7 @@ def test_grouped_conv_matches_fp32(gpu, c, groups, stride):
 def test_grouped_conv_mfma_matches_valu(gpu, c, groups, stride, monkeypatch):
     """The MFMA grouped 3x3 (gconv_mfma: block-diagonal weights over a max(16, CG) window) against the VALU
     kernels on the same bf16 inputs: both accumulate in fp32, so outputs and input gradients agree to bf16
-    rounding; the MFMA path is the one the ResNeXt shapes take."""
+    rounding, weight gradients to fp32 summation order; the MFMA path is the one the ResNeXt shapes take."""
     from medical_segmentation_pytorch_amd.ops import gconv as G
     torch.manual_seed(9)
     m = nn.Conv2d(c, c, 3, stride, 1, groups=groups, bias=False).to(gpu)
@@ -817,10 +817,12 @@ def test_grouped_conv_mfma_matches_valu(gpu, c, groups, stride, monkeypatch):
         xf = x.clone().requires_grad_(True)
         y = G.gconv(xf, m)
         g = torch.randn_like(y, dtype=torch.float32).mul(0.5).to(torch.bfloat16) if not out else out[0][2]
+        m.weight.grad = None
         y.backward(g)
-        out.append((y.detach().float(), xf.grad.float(), g))
+        out.append((y.detach().float(), xf.grad.float(), g, m.weight.grad.clone()))
     assert _rel(out[0][0], out[1][0]) < 5e-3
     assert _rel(out[0][1], out[1][1]) < 5e-3
+    assert _rel(out[0][3], out[1][3]) < 1e-4   # both fp32 accumulations of the same bf16 products
 
 
 def test_relu6_forward_backward(gpu):
