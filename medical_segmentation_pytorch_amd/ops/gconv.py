@@ -2,7 +2,7 @@
 ``Bottleneck.conv2``, groups 32) inside the fused graph -- the last conv that used to run on MIOpen.
 
 NHWC bf16 maps with C % 8 == 0 (unpadded: ResNeXt widths are multiples of 8); fp32 weights repacked to
-[T][C][CG] per call.  3x3 convs with C % 16 == 0 and 4 <= CG <= 64 run forward and data-gradient on the MFMA
+[T][C][CG] per call.  3x3 convs with C % 16 == 0 and CG <= 64 (depthwise included) run forward and data-gradient on the MFMA
 kernel (``gconv_mfma``: block-diagonal weights over a max(16, CG)-channel window, packed per MFMA lane by
 ``_mfma_pack``) and so does the weight-gradient (``gconv_wgrad_mfma``: the dense 16-co x 9-tap x window
 tiles, reduced over pixel slices by ``colsum``, block diagonal gathered by ``_wgrad_diag_index``); env
@@ -19,12 +19,15 @@ import torch
 from ._ext import require
 
 _MFMA = os.environ.get('MSP_GCONV_MFMA', '1') != '0'
+# smallest group width on the MFMA path (env MSP_GCONV_MFMA_MINCG, A/B).  Depthwise (CG = 1) included: only
+# 1/16 of the MFMA work is useful, but the VALU kernels are slower still -- smp-Unet MobileNetV2 bs64
+# 2020 -> 2947 img/s (profiles/r05/gconv/bench_smp_unet_mobilenetv2_bs64_*.json)
+_MFMA_MINCG = int(os.environ.get('MSP_GCONV_MFMA_MINCG', '1'))
 _PACK_IDX = {}
 
 
 def _mfma_ok(C, CG, T):
-    # CG >= 4: ResNeXt's groups (depthwise / CG 2 stay on the VALU kernels: 1/16 - 1/8 of the MFMA work useful)
-    return _MFMA and T == 9 and C % 16 == 0 and 4 <= CG <= 64
+    return _MFMA and T == 9 and C % 16 == 0 and _MFMA_MINCG <= CG <= 64
 
 
 def _mfma_pack_index(C, CG, T, trans, device):
