@@ -4,10 +4,14 @@
 // Reference: models/__init__.py:8-10 (smp encoders incl. resnext50_32x4d; SURVEY §2 "encoders").  Until
 // round 4 this was the one conv of the fused graph that ran on MIOpen's channels-last grouped kernels.
 //
-// A group has CG = C / groups channels in and out (ResNeXt 32x4d: 4, 8, 16, 32 on layers 1-4), so per
-// output channel the reduction is only CG x taps (36..288) long: too short for an MFMA tile, and the
-// block-diagonal weight would waste groups-fold MFMA work as a dense GEMM.  These kernels are direct VALU
-// convolutions instead, memory-shaped like the depthwise kernels (decoder.hip):
+// A group has CG = C / groups channels in and out (ResNeXt 32x4d: 4, 8, 16, 32 on layers 1-4; depthwise 1),
+// so per output channel the reduction is only CG x taps (9..288) long.  Round 5: 3x3 convs with C % 16 == 0
+// run on the MFMA kernels at the end of this file (gconv_mfma / gconv_wgrad_mfma): a dense GEMM over a
+// max(16, CG)-channel window with block-diagonal weights -- only CG / 16 of the MFMA work is useful at
+// CG < 16, but the matrix cores have that to spare and the VALU kernels below were compute-bound (~14
+// TFLOP/s): ResNeXt50 bs64 1227 -> 1749 img/s, MobileNetV2 2020 -> 2947 (profiles/r05/gconv/).
+// The VALU kernels remain for the other shapes (non-3x3, C % 16 != 0, CG > 64) and as the A/B reference
+// (env MSP_GCONV_MFMA=0), memory-shaped like the depthwise kernels (decoder.hip):
 //   fwd / dgrad : a thread owns 8 consecutive channels of one pixel (one 16-B vector out); threads of a
 //                 wave share the channel block and walk 64 consecutive pixels, so the weight reads are
 //                 wave-uniform (broadcast) and the activation reads are one 16-B vector per lane per tap.
