@@ -113,7 +113,10 @@ def bench_config(model_name, base_channel, batch, size, lr, total_steps, train_i
         from .trainer_engine import smp_arch
         parts = model_name.split('-')
         cfg.model = 'smp'
-        cfg.decoder = smp_arch(parts[1]).lower() if len(parts) == 3 else 'unet'
+        # the reference hub's key of that smp class (models/__init__.py decoder_hub: 'DeepLabV3Plus' ->
+        # 'deeplabv3p', 'UnetPlusPlus' -> 'unetpp', else the lower-case name)
+        arch = smp_arch(parts[1].lower()).lower() if len(parts) == 3 else 'unet'
+        cfg.decoder = {'deeplabv3plus': 'deeplabv3p', 'unetplusplus': 'unetpp'}.get(arch, arch)
         cfg.encoder = parts[-1]
         cfg.encoder_weights = None
     cfg.train_bs = batch

@@ -1,3 +1,4 @@
+import pytest
 from medical_segmentation_pytorch_amd.configs import BaseConfig, MyConfig, OptunaConfig, load_parser
 
 
@@ -52,3 +53,16 @@ def test_optuna_trial_params():
     c.get_trial_params(_Trial())
     assert c.randscale[0] <= 0 <= c.randscale[1]
     assert c.optimizer_type in ('sgd', 'adam', 'adamw') and c.loss_type in ('ohem', 'ce')
+
+
+@pytest.mark.parametrize('name,key', [('smp-resnet101', 'unet'), ('smp-fpn-resnet101', 'fpn'),
+                                      ('smp-deeplabv3plus-resnet101', 'deeplabv3p'),
+                                      ('smp-UnetPlusPlus-resnet34', 'unetpp'), ('smp-pspnet-resnet18', 'pspnet')])
+def test_bench_config_smp_decoder_keys(tmp_path, name, key):
+    """bench.py's ``smp-<decoder>-<encoder>`` names map onto the reference hub's decoder keys
+    (models/__init__.py decoder_hub: DeepLabV3Plus is 'deeplabv3p', UnetPlusPlus 'unetpp')."""
+    from medical_segmentation_pytorch_amd.models import decoder_hub
+    from medical_segmentation_pytorch_amd.runtime.bench_step import bench_config
+    cfg = bench_config(name, 17, 2, 64, 1e-3, 10, 4, 1, str(tmp_path))
+    assert cfg.model == 'smp' and cfg.decoder == key and cfg.decoder in decoder_hub
+    assert cfg.encoder == name.split('-')[-1]
