@@ -213,6 +213,12 @@ def dwconv(x, conv: torch.nn.Conv2d):
     if 2 * ph != dh * (kh - 1) or 2 * pw != dw * (kw - 1):
         raise ValueError(f'dwconv: only same-size depthwise convs are fused (kernel {kh}x{kw}, padding '
                          f'{(ph, pw)}, dilation {(dh, dw)})')
+    C = conv.in_channels
+    if conv.bias is None and (kh, kw) == (3, 3) and x.shape[-1] == C and C % 16 == 0:
+        # unpadded 3x3 without bias (smp SeparableConv2d's depthwise): the MFMA grouped-conv kernels
+        # (ops/gconv.py, CG = 1; any dilation) -- forward, data- and weight-gradient
+        from .gconv import gconv
+        return gconv(x, conv)
     return _DwConv.apply(x, conv.weight, conv.bias, kh, kw, tuple(conv.padding), tuple(conv.dilation))
 
 
