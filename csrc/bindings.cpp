@@ -309,6 +309,14 @@ void bn_act_apply_t(const at::Tensor& y, const at::Tensor& stats, const at::Tens
   bn_act_apply(bf(y), st, st + Cp, bf(z), P, Cp, relu ? 1 : 0, cur_stream());
 }
 
+// the same pass with ReLU6 (MobileNetV2's BN -> ReLU6 in one pass)
+void bn_act_apply_relu6_t(const at::Tensor& y, const at::Tensor& stats, const at::Tensor& z, int64_t P, int64_t Cp) {
+  CHECK_BF16(y); CHECK_BF16(z); CHECK_F32(stats);
+  TORCH_CHECK(y.numel() == P * Cp && z.numel() == P * Cp && stats.numel() == 4 * Cp);
+  const float* st = f32(stats);
+  bn_act_apply(bf(y), st, st + Cp, bf(z), P, Cp, 2, cur_stream());
+}
+
 void bn_add_act_t(const at::Tensor& y, const at::Tensor& sa, bool relu_a, const at::Tensor& x,
                   const c10::optional<at::Tensor>& sb, bool relu_b, const at::Tensor& z, bool relu) {
   CHECK_BF16(y); CHECK_BF16(x); CHECK_BF16(z); CHECK_F32(sa);
@@ -1109,6 +1117,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_reduce_bwd_finalize", &bn_reduce_bwd_finalize_t);
   m.def("bn_rf_chunks", [](int64_t Cp) { return bn_rf_chunks((int)Cp); });
   m.def("bn_act_apply", &bn_act_apply_t);
+  m.def("bn_act_apply_relu6", &bn_act_apply_relu6_t);
   m.def("bn_add_act", &bn_add_act_t);
   m.def("gconv_fwd", &gconv_fwd_t);
   m.def("relu6", &relu6_t);

@@ -249,7 +249,9 @@ __global__ __launch_bounds__(kBlock) void bn_act_apply_kernel(const uint16_t* __
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float o = fmaf(v[e], a[e], b[e]);
-        v[e] = relu ? fmaxf(o, 0.f) : o;
+        // relu 2: ReLU6 (MobileNetV2), clamped before the one bf16 rounding -- bitwise the rounded BN
+        // output clamped by a separate relu6 pass (6 is exact in bf16; rounding is monotone)
+        v[e] = relu == 2 ? fminf(fmaxf(o, 0.f), 6.f) : (relu ? fmaxf(o, 0.f) : o);
       }
       *reinterpret_cast<uint4*>(z + q * Cp + 8 * cg) = pack8(v);
     }

@@ -1,6 +1,8 @@
 """Layout conversion and glue ops on the HIP kernels (``csrc/elementwise.hip``)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._ext import require
@@ -117,6 +119,9 @@ def add_n(*xs):
     return _AddN.apply((coefs, mask), *ts)
 
 
+_BN_RELU6 = os.environ.get('MSP_BN_RELU6', '1') != '0'
+
+
 class _ReLU6(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
@@ -136,7 +141,35 @@ class _ReLU6(torch.autograd.Function):
         return dx
 
 
+class _BNReLU6(torch.autograd.Function):
+    """relu6(materialize(d)) for a deferred BN output without ReLU in ONE pass (``bn_act_apply_relu6``: the
+    affine and the clamp before the single bf16 rounding -- bitwise the two-pass result); backward: the
+    ReLU6 mask of the output, passed to the deferred alias like ``ops.bn._Materialize``."""
+
+    @staticmethod
+    def forward(ctx, t, stats):
+        C = require()
+        t = t.contiguous()
+        Cp = t.shape[-1]
+        y = torch.empty_like(t)
+        C.bn_act_apply_relu6(t, stats, y, t.numel() // Cp, Cp)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        C = require()
+        (y,) = ctx.saved_tensors
+        dx = torch.empty_like(y)
+        C.relu6_bwd(g.contiguous(), y, dx)
+        return dx, None
+
+
 def relu6(x):
-    """``nn.ReLU6`` (MobileNetV2) on an NHWC bf16 map (a ``ops.bn.Deferred`` input is materialised first)."""
-    from .bn import materialize
+    """``nn.ReLU6`` (MobileNetV2) on an NHWC bf16 map; a ``ops.bn.Deferred`` input (BN without ReLU, not yet
+    materialised) takes the one-pass BN + ReLU6 apply (env MSP_BN_RELU6=0: materialise, then ReLU6)."""
+    from .bn import Deferred, materialize, need_stats
+    if _BN_RELU6 and isinstance(x, Deferred) and x.z is None and not x.relu:
+        need_stats([x])
+        return _BNReLU6.apply(x.t, x.stats)
     return _ReLU6.apply(materialize(x))

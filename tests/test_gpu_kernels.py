@@ -839,3 +839,28 @@ def test_relu6_forward_backward(gpu):
     y.backward(g)
     assert torch.equal(y, ref)
     assert torch.equal(xf.grad, xr.grad)
+
+
+def test_bn_relu6_one_pass_matches_two_pass(gpu, monkeypatch):
+    """MobileNetV2's BN -> ReLU6 as ONE apply pass (ops.elementwise._BNReLU6, bn_act_apply_relu6) is bitwise
+    the materialised BN output followed by the ReLU6 pass, forward and backward."""
+    from medical_segmentation_pytorch_amd.ops import elementwise as E
+    from medical_segmentation_pytorch_amd.ops.bn import Deferred
+    torch.manual_seed(6)
+    P, Cp, C = 3 * 29 * 31, 24, 20
+    t0 = (torch.randn(P, Cp, device=gpu) * 3).to(torch.bfloat16)
+    t0[:, C:] = 0
+    stats = torch.zeros(4, Cp, device=gpu)
+    stats[0, :C] = torch.rand(C, device=gpu) * 2 + 0.5
+    stats[1, :C] = torch.randn(C, device=gpu) * 2
+    g = torch.randn(P, Cp, device=gpu).to(torch.bfloat16)
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(E, '_BN_RELU6', fused)
+        t = t0.clone().requires_grad_(True)
+        y = E.relu6(Deferred(t, stats, False))
+        y.backward(g)
+        out.append((y.detach(), t.grad))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert out[0][0].max().item() == 6.0 and out[0][0].min().item() == 0.0
