@@ -690,17 +690,12 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
   if (KS > kFbMaxKS) return false;
   double best = 1e30;
   bool found = false;
-  static int force_cw = -1;   // env MSP_FB_CW: 4 / 8 forces the compute-wave layout of 512-pixel tiles (A/B)
-  if (force_cw < 0) {
-    const char* e = getenv("MSP_FB_CW");
-    force_cw = e == nullptr ? 0 : atoi(e);
-  }
   // (128-pixel tiles: only the 34-channel level's dilated / wide halos, which fit no larger double buffer)
   for (int tp = 512; tp >= (cb == 3 && !fwd ? 128 : 256); tp /= 2) {
     if (tp == 128 && found) break;
     // (cb 3 backward: the 9 x 4 weight-gradient accumulators of 3 units need the 256-register budget of CW 4)
-    const int cw = (tp <= 256 || (cb == 3 && !fwd)) ? 4
-                   : (force_cw == 4 || force_cw == 8 ? force_cw : (g.Go == 1 ? 8 : 4));
+    // (8 compute waves for one output group, 4 for the Go = 2 pair: profiles/r05/fused_bwd_cw_and_knockouts_bs320.txt)
+    const int cw = (tp <= 256 || (cb == 3 && !fwd)) ? 4 : (g.Go == 1 ? 8 : 4);
     const int nj = tp / (16 * cw);
     if (cb == 3 && !fwd && tp == 512) continue;   // (never fits the LDS; no instantiation)
     for (int tw = 16; tw <= 64; tw *= 2) {

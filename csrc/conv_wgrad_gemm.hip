@@ -320,31 +320,20 @@ constexpr WgCfg kWgCfgs[] = {
 constexpr int kNumWgCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 
 int g_wg_mode = -1;   // env MSP_WGRAD_GEMM: 0 off (the conv.hip kernels), 1 auto (default), 2 every eligible conv
-int g_wg_cfg = -2;    // env MSP_WGRAD_GEMM_CFG: force a configuration (A/B); -1 planner
-long g_wg_blocks = -1;   // env MSP_WGRAD_GEMM_BLOCKS: grid size target for 4-wave tiles (8-wave: half).  Default 512
-// (round 5 sweep, profiles/r05/wgrad_blocks_sweep.txt: 256 / 512 / 768 / 1024 -> R101 bs64 1371 / 1456 / 1397 / 1390,
-// FPN-R101 1532 / 1600 / 1518 / 1498, DUCKNet-17 bs320 553 / 592 / 579 / 593 img/s)
-// env MSP_WGRAD_STAGE_COST: the planner's per-row staging cost (MAC units, wg_pick).  96 (round 5) picks the
-// 8-wave 256-wide tiles for the >= 136-channel 3x3 / 1x7 layers: conv_bench levels 3-6 wgrad 25.3 -> 22.4 ms
-// at bs320 against 24 (profiles/r05/wgrad_stage_cost_bs320.txt)
-double g_wg_stage_cost = -1;
+int g_wg_cfg = -1;    // conv_wgrad_gemm_force_cfg: force a configuration (tests / A-B); -1 planner
+// Grid size target for 4-wave tiles (8-wave: half): 512 (round 5 sweep, profiles/r05/wgrad_blocks_sweep.txt:
+// 256 / 512 / 768 / 1024 -> R101 bs64 1371 / 1456 / 1397 / 1390, FPN-R101 1532 / 1600 / 1518 / 1498,
+// DUCKNet-17 bs320 553 / 592 / 579 / 593 img/s)
+constexpr long g_wg_blocks = 512;
+// The planner's per-row staging cost (MAC units, wg_pick).  96 (round 5) picks the 8-wave 256-wide tiles for
+// the >= 136-channel 3x3 / 1x7 layers: conv_bench levels 3-6 wgrad 25.3 -> 22.4 ms at bs320 against 24
+// (profiles/r05/wgrad_stage_cost_bs320.txt)
+constexpr double g_wg_stage_cost = 96.0;
 
 void wg_env() {
   if (g_wg_mode < 0) {
     const char* e = getenv("MSP_WGRAD_GEMM");
     g_wg_mode = e == nullptr ? 1 : (e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1));
-  }
-  if (g_wg_cfg == -2) {
-    const char* e = getenv("MSP_WGRAD_GEMM_CFG");
-    g_wg_cfg = (e != nullptr && atoi(e) >= 0 && atoi(e) < kNumWgCfgs) ? atoi(e) : -1;
-  }
-  if (g_wg_blocks < 0) {
-    const char* e = getenv("MSP_WGRAD_GEMM_BLOCKS");
-    g_wg_blocks = (e != nullptr && atol(e) > 0) ? atol(e) : 512;
-  }
-  if (g_wg_stage_cost < 0) {
-    const char* e = getenv("MSP_WGRAD_STAGE_COST");
-    g_wg_stage_cost = (e != nullptr && atof(e) >= 0) ? atof(e) : 96.0;
   }
 }
 

@@ -133,6 +133,10 @@ class BaseTrainer:
                 # collective (a SyncBN exchange would count the skew against its deadline)
                 from ..utils.parallel import get_group
                 torch.distributed.barrier(group=get_group(config))
+        if self.accum_micro() != 0 and self.main_rank and self.logger:
+            self.logger.warning(f'training ended inside a gradient-accumulation group ({self.accum_micro()} of '
+                                f'{getattr(config, "accum_steps", 1)} micro-batches): their gradients were never '
+                                f'applied (make iters_per_epoch * total_epoch a multiple of accum_steps)')
         if config.use_tb and self.main_rank and self.writer is not None:
             self.writer.flush()
             self.writer.close()
@@ -165,6 +169,11 @@ class BaseTrainer:
     def parallel_model(self, config):
         self.model = parallel_model(config, self.model, self.local_rank, self.device, self.optimizer)
 
+    def accum_micro(self):
+        """Micro-batch index inside the current gradient-accumulation group (0: at a group boundary)."""
+        eng = getattr(self, 'engine', None)
+        return eng.micro if eng is not None else getattr(self, '_micro', 0)
+
     def train_one_epoch(self, config):
         raise NotImplementedError()
 
@@ -192,6 +201,9 @@ class BaseTrainer:
                 if hasattr(self.scaler, 'sync_optimizer_step'):   # fused fp16 Adam: restore its device step
                     self.scaler.sync_optimizer_step(self.optimizer)
                 self._pending_ema = ckpt.get('ema_state_dict')
+                if ckpt.get('accum_micro', 0) and self.main_rank and self.logger:
+                    self.logger.warning(f'checkpoint was saved {ckpt["accum_micro"]} micro-batches into a '
+                                        f'gradient-accumulation group; that partial group is restarted')
                 rng = ckpt.get('rng')
                 if rng is not None:
                     torch.set_rng_state(rng['torch'].cpu())
@@ -224,6 +236,9 @@ class BaseTrainer:
         }
         if config.ckpt_extra_state and not save_best:
             ckpt['train_itrs'] = self.train_itrs
+            # gradient accumulation: the micro-batch index at save time (the partial group's gradients are not
+            # saved: a resume restarts that group, and warns)
+            ckpt['accum_micro'] = int(self.accum_micro())
             ckpt['scaler'] = self.scaler.state_dict() if self.scaler.is_enabled() else None
             ckpt['ema_state_dict'] = _compact(self.ema_model.ema.state_dict())
             npst = np.random.get_state()

@@ -60,6 +60,11 @@ def available() -> bool:
     return _C is not None
 
 
+def stale() -> bool:
+    """True when a built extension exists but was refused by the provenance check (sources changed)."""
+    return _C is None and isinstance(_ERR, RuntimeError) and 'stale HIP extension' in str(_ERR)
+
+
 def require():
     if _C is None:
         so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_C.so')

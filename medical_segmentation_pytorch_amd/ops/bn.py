@@ -617,8 +617,6 @@ def _finalize_many(C, jobs, group, dev):
 
 # env MSP_TAIL_SPLIT=0: the partial pass as one six-branch launch (A/B)
 _TAIL_SPLIT = os.environ.get('MSP_TAIL_SPLIT', '1') != '0'
-# env MSP_TAIL_APPLY_SPLIT=1: the apply pass as 3-branch launches too (A/B)
-_TAIL_APPLY_SPLIT = os.environ.get('MSP_TAIL_APPLY_SPLIT', '0') == '1'
 
 
 class _DuckTail(torch.autograd.Function):
@@ -731,11 +729,8 @@ class _DuckTail(torch.autograd.Function):
                               ctx.relu_mask >> b0, tpart[b0:b1], P, Cp)
         coefs = finalize([(tpart[i], tb) for i in range(k)], list(range(k)))
         dys = [torch.empty_like(y_sum) for _ in range(k)]
-        astep = 3 if _TAIL_APPLY_SPLIT else k
-        for b0 in range(0, k, astep):
-            b1 = min(k, b0 + astep)
-            C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys[b0:b1], stats[b0:b1], coefs[b0:b1],
-                            ctx.relu_mask >> b0, dys[b0:b1], P, Cp)
+        # the apply pass as ONE k-branch launch (3-branch launches measured no faster, round 5)
+        C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, coefs, ctx.relu_mask, dys, P, Cp)
         for st in sts:
             if st.ready_hook is not None:
                 st.ready_hook([t for t in (st.weight, st.bias) if t is not None])

@@ -206,10 +206,9 @@ def _taps(tl):
 
 # env MSP_FUSED_BWD=0: the narrow stride-1 convs run the separate data- and weight-gradient kernels (A/B)
 FUSED_BWD = os.environ.get('MSP_FUSED_BWD', '1') != '0'
-# env MSP_DEFER_DY_SEPARATE=1: a deferred BN data-gradient may also be rebuilt by the SEPARATE halo data- and
-# weight-gradient kernels (each re-reads y; measured net-neutral -- profiles/r04/kernels_deferdy_*): off, so
-# outside the fused backward a deferred gradient is resolved (= the apply pass of the materialised path)
-DEFER_SEPARATE = os.environ.get('MSP_DEFER_DY_SEPARATE', '0') == '1'
+# A deferred BN data-gradient is NOT rebuilt by the separate halo data- and weight-gradient kernels (each
+# re-reads y; measured net-neutral in round 4 and -1.6 % in round 5: profiles/r04/kernels_deferdy_*,
+# profiles/r05/defer_dy_separate_ab_bs320.txt): outside the fused backward it is resolved (the apply pass)
 
 
 def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
@@ -280,8 +279,8 @@ def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     # Without a data-gradient launch (the first conv: its input is the image) the weight-gradient is dY's
     # only reader: rebuilding dY there reads (dz, y) once instead of the apply pass's read dz, y + write dy
     # + the weight-gradient's read dy -- 2 passes instead of 4, a win even where the halo kernels' re-read
-    # of y made deferral neutral (DEFER_SEPARATE).
-    ok = (DEFER_SEPARATE or not dgrad) and not plan.transposed and plan.stride == 1 and plan.bias is None
+    # of y made deferral neutral (see above).
+    ok = not dgrad and not plan.transposed and plan.stride == 1 and plan.bias is None
     if ok and dgrad:
         ok = bool(C.conv_uses_halo(dims_d, taps_d[0], taps_d[1], False, True))
     if ok:

@@ -27,7 +27,10 @@ _PACK_IDX = {}
 
 
 def _mfma_ok(C, CG, T):
-    return _MFMA and T == 9 and C % 16 == 0 and _MFMA_MINCG <= CG <= 64
+    # the MFMA kernels take a window of KW = max(16, CG) in {16, 32, 64} channels that holds whole groups:
+    # CG must divide 16 or be 32 / 64 (CG = 24, 48 would hit a kernel check, CG = 12 would straddle windows)
+    return (_MFMA and T == 9 and C % 16 == 0 and _MFMA_MINCG <= CG <= 64
+            and (16 % CG == 0 or CG in (32, 64)))
 
 
 def _mfma_pack_index(C, CG, T, trans, device):

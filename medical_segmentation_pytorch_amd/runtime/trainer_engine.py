@@ -52,6 +52,7 @@ class StepEngine:
         self.images, self.masks = static if static is not None else (None, None)
         self.graph = None       # the most recently captured graph (accum 1: THE step graph)
         self.graphs = {}        # (first, last) micro-step kind -> captured graph
+        self.graph_outs = {}    # (first, last) -> that graph's static (loss, kd) outputs
         self._pool = None
         self.micro = 0          # micro-step index inside the current optimizer step
         self.stepped = False    # whether the latest call ran the optimizer
@@ -155,11 +156,16 @@ class StepEngine:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with no_gc(), torch.cuda.graph(g, pool=self._pool, capture_error_mode=capture_mode()):
-                self.loss, self.kd = self.body(self.images, self.masks, first, last)
+                outs = self.body(self.images, self.masks, first, last)
             self._pool = g.pool()
             self.graphs[key] = g
+            # each micro-step kind (first / middle / last of an accumulation group) has its own graph and
+            # its own static loss / KD outputs: kept alive here (the shared pool cannot reuse them) and
+            # selected after every replay, so a replayed 'first' step never reports the 'last' graph's loss
+            self.graph_outs[key] = outs
             self.graph = g
         g.replay()
+        self.loss, self.kd = self.graph_outs[key]
         self.last_kd = self.kd
         return self.loss
 

@@ -97,6 +97,10 @@ def use_fused(config, model, device) -> bool:
     from ..runtime.fused_model import supports
     if config.engine == 'eager' or device.type != 'cuda':
         return False
+    if _ext.stale():
+        # engine='auto' must not fall back to the slow eager path silently on a GPU because the build is
+        # out of date: a benchmark or a training run would quietly switch engines
+        _ext.require()
     ok = supports(model) and _ext.available()
     if config.engine == 'fused' and not ok:
         _ext.require()

@@ -29,6 +29,7 @@ def ext():
     yield C
     C.conv_gemm_force_cfg(-1)
     C.conv_set_gemm(True)
+    C.conv_set_hgemm(True)
     C.conv_set_wgrad_gemm(1)
 
 
@@ -52,6 +53,7 @@ GEMM_CASES = [
 def test_gemm_conv_fwd_bwd(gpu, ext, case, cfg):
     n, h, w, ci, co, (kh, kw), s, pad, dil, groups, bias = case
     ext.conv_gemm_force_cfg(cfg)
+    ext.conv_set_hgemm(cfg < 0)   # a forced im2col configuration tests the im2col kernel on every shape
     torch.manual_seed(0)
     ms = [nn.Conv2d(ci, co, (kh, kw), s, pad, dil, bias=bias).to(gpu) for _ in range(groups)]
     br = [Branch(m.weight, g, 0, kh * kw) for g, m in enumerate(ms)]

@@ -126,9 +126,11 @@ def test_gradient_accumulation_graph_matches_eager_and_single_step(gpu):
     one, eager2, graph2 = mk(False, 1), mk(False, 2), mk(True, 2)
     for it in range(3):   # graph2: eager warm-up (calls 1-2), capture (3: first, 4: last), replays (5-6)
         one()
-        for _ in range(2):
-            eager2()
-            graph2()
+        for k in range(2):
+            le = eager2().detach().clone()
+            lg = graph2().detach().clone()
+            # every micro-step kind reports ITS graph's loss (not the last-captured graph's stale output)
+            assert torch.equal(le, lg), (it, k, 'graph micro-step loss != eager')
         torch.cuda.synchronize()
         assert graph2.engine.stepped and eager2.engine.stepped
         ps = [dict(s.model.named_parameters()) for s in (one, eager2, graph2)]
