@@ -49,6 +49,11 @@ def parse_args(argv=None):
                    help='KD teacher (e.g. smp-resnet101; BASELINE config #4 = --base-channel 34 --teacher smp-resnet101)')
     p.add_argument('--channels-last', action='store_true')
     p.add_argument('--no-graph', action='store_true')
+    p.add_argument('--graph-ddp', choices=['auto', 'on', 'off'], default='auto',
+                   help='capture the multi-rank step (bucket all-reduces + SyncBN RCCL calls) in the hipGraph: '
+                        'auto = on at per-GPU batch <= 64, where host launches would be exposed; at the bench batch '
+                        'the step is GPU-bound and runs uncaptured, so the comm evidence pass (eager per-bucket '
+                        'RCCL timings and knock-outs) can run')
     p.add_argument('--ddp', action='store_true',
                    help='run the distributed code path (process group, RCCL gradient buckets) even at WORLD_SIZE=1')
     p.add_argument('--data', choices=['augment', 'fixed'], default='augment',
@@ -258,7 +263,8 @@ def main(argv=None):
         if cuda:
             torch.cuda.set_device(dev_index)
         backend = os.environ.get('BENCH_DIST_BACKEND', 'nccl' if cuda else 'gloo')
-        # per-collective on-stream durations for the evidence pass (Work._get_duration)
+        # per-collective on-stream durations for the evidence pass (Work._get_duration; captured works
+        # carry timing events too: tools/dev/graph_rccl_probe.py runs with it set)
         os.environ.setdefault('TORCH_NCCL_ENABLE_TIMING', '1')
         kw = {'device_id': torch.device('cuda', dev_index)} if backend == 'nccl' else {}
         dist.init_process_group(backend, **kw)
@@ -274,10 +280,12 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     impl = args.impl
-    # multi-GPU steps run uncaptured (RCCL collectives outside any hipGraph); at the bench batch the step
-    # is GPU-bound, so the ~2k host launches per step are hidden behind the GPU (round 2: graph vs no
-    # graph within 1 %)
-    use_graph = cuda and not args.no_graph and not ddp
+    # multi-rank steps: the RCCL collectives are captured with the rest of the step when --graph-ddp is on
+    # (auto: per-GPU batch <= 64, where the ~2k host launches per step would be exposed); at the bench
+    # batch the step is GPU-bound (profiles/r06/ddp_graph: graph vs no graph within noise), so it runs
+    # uncaptured and the per-bucket RCCL evidence pass below can run
+    graph_ddp = args.graph_ddp == 'on' or (args.graph_ddp == 'auto' and args.batch <= 64)
+    use_graph = cuda and not args.no_graph and (not ddp or graph_ddp)
     total_steps = args.warmup + args.steps + 2 * args.comm_steps + 2
     save_dir = None
     if impl == 'fused':

@@ -142,8 +142,10 @@ class BaseConfig:
         self.cap_workers = True        # cap DataLoader workers at the host CPU count (ref: gpu_num*base_workers)
         self.teacher_base_channel = None
         self.graph_warmup = 3          # eager iterations before the hipGraph capture
-        self.bucketer_world1 = False   # attach the RCCL gradient bucketer at world size 1 too (bench --ddp
-                                       # evidence run); a step with a bucketer is never graph-captured
+        self.bucketer_world1 = False   # attach the RCCL gradient bucketer at world size 1 too (bench --ddp)
+        self.graph_collectives = True  # capture a step that issues torch.distributed collectives (gradient
+                                       # buckets, SyncBN over RCCL) in the hipGraph too (RCCL calls are graph
+                                       # nodes; tools/dev/graph_rccl_probe.py); False: such steps run eagerly
         self.val_fp32 = False          # validate the EMA model in fp32 eager PyTorch exactly as the reference
                                        # (core/seg_trainer.py:114); False: the bf16 fused executor (fast)
         self.progress_bar = True

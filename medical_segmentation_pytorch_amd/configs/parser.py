@@ -114,6 +114,7 @@ def get_parser():
     _flag(p, 'synthetic_num', type=int, nargs=3)
     _flag(p, 'synthetic_size', type=int)
     _flag(p, 'bucketer_world1', action='store_true')
+    _flag(p, 'no_graph_collectives', action='store_false', dest='graph_collectives')
     _flag(p, 'syncbn_comm', type=str, choices=['auto', 'ipc', 'rccl'])
     _flag(p, 'lr_scale', type=str, choices=['reference', 'sqrt', 'linear'])
     _flag(p, 'lr_ref_batch', type=int)

@@ -108,13 +108,15 @@ class SegTrainer(BaseTrainer):
     def _use_graph(self, config):
         # every loss (CE, device-side OHEM, BCE+Dice), the KD term and the fused fp16 GradScaler are
         # capture-safe; the eager teacher fallback is not.  A step that issues torch.distributed
-        # collectives (gradient buckets, SyncBN over RCCL) is never captured: the process group's watchdog
-        # polls the events of its works, and events recorded inside a capture abort it
-        # (hipErrorCapturedEvent).  At world size 1 no collective is attached, so the step is captured.
+        # collectives (gradient buckets, SyncBN over RCCL) is captured too when config.graph_collectives:
+        # torch 2.10's process group records captured RCCL calls as graph nodes and keeps their works off
+        # its watchdog (round 6: tools/dev/graph_rccl_probe.py, tests/test_gpu_distributed.py).  The
+        # bucket rebuild (first step) and every communicator init happen in the eager warm-up steps.
         kd_ok = not config.kd_training or isinstance(self.teacher_model, FusedModel)
         collectives = getattr(self.optimizer, 'bucketer', None) is not None or \
             (config.DDP and config.gpu_num > 1)
-        return self.fused and config.use_graph and kd_ok and not config.use_aux and not collectives
+        coll_ok = not collectives or getattr(config, 'graph_collectives', True)
+        return self.fused and config.use_graph and kd_ok and not config.use_aux and coll_ok
 
     def step_engine(self, config):
         """The fused engine's device step (:class:`runtime.trainer_engine.StepEngine`) -- the same object

@@ -194,7 +194,7 @@ class FusedStep:
     def __init__(self, model, images, masks, optimizer='adam', lr=1e-3, weight_decay=0.0, momentum=0.9,
                  total_steps=100000, pct_start=3 / 400, use_ema=False, use_graph=True, distributed=False,
                  syncbn=True, bucket_cap_mb=64.0, ignore_index=255, teacher=None, kd_temperature=4.0,
-                 kd_coef=1.0, feed=None, accum_steps=1):
+                 kd_coef=1.0, feed=None, accum_steps=1, bucket_world1=False):
         from ..utils.model_ema import ModelEmaV2
         from ..utils.optimizer import FusedOptimizer
         from ..utils.parallel import FusedModel
@@ -209,7 +209,7 @@ class FusedStep:
                                   device=dev)
         self.arena = self.opt.arena
         self.bucketer = None
-        if distributed and self.world > 1:
+        if distributed and (self.world > 1 or bucket_world1):   # bucket_world1: the RCCL path on one GPU (tests)
             self.bucketer = GradBucketer(self.arena, group, bucket_cap_mb)
             self.opt.attach_bucketer(self.bucketer)
         self.fm = FusedModel(model, group=stat_group(group) if syncbn else None, sinks=self.arena.sinks(),

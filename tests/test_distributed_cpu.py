@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2 and 4) tests of the distributed layer, CPU only."""
+"""Multi-process (gloo, world_size 2, 4 and 8 -- the 8-GPU node's rank count) tests of the distributed layer, CPU only."""
 import os
 import socket
 
@@ -88,7 +88,7 @@ def test_grad_bucketer_rebuilds_in_ready_order(compress):
         assert any(packed)                         # scrambled order: some buckets go through the staging buffer
 
 
-@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('world', [2, 4, 8])
 @pytest.mark.parametrize('compress', [None, 'bf16'])
 def test_grad_bucketer_allreduce(compress, world):
     """Bucketed all-reduce (SUM) of the grad arena; values sum_r (r+1)*(i+1) are exact in bf16 too."""
@@ -114,13 +114,13 @@ def _metric_sampler_worker(rank, world, port, q):
     dice = d.compute()
     # sampler sharding: disjoint, covering
     from torch.utils.data.distributed import DistributedSampler
-    s = DistributedSampler(list(range(12)), num_replicas=world, rank=rank, shuffle=True, seed=1)
+    s = DistributedSampler(list(range(24)), num_replicas=world, rank=rank, shuffle=True, seed=1)
     s.set_epoch(3)
     q.put((rank, iou.tolist(), dice.item(), list(s), logits.tolist(), tgt.tolist()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('world', [2, 4, 8])
 def test_distributed_metrics_and_sampler(world):
     """One confusion-matrix all-reduce gives every rank the pooled (exact) IoU / Dice; the sampler's shards
     are disjoint and cover the set (reference utils/parallel.py + torchmetrics sync)."""
@@ -138,7 +138,7 @@ def test_distributed_metrics_and_sampler(world):
         assert abs(r[2] - d.compute().item()) < 1e-6
     shards = [set(r[3]) for r in res]
     assert sum(len(s) for s in shards) == len(set().union(*shards))   # disjoint
-    assert set().union(*shards) == set(range(12))                      # covering
+    assert set().union(*shards) == set(range(24))                      # covering
 
 
 def _full_batch_worker(rank, world, port, q):
@@ -184,11 +184,12 @@ def _full_batch_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_bucketed_ddp_step_and_syncbn_equal_full_batch_world4():
+@pytest.mark.parametrize('world', [4, 8])
+def test_bucketed_ddp_step_and_syncbn_equal_full_batch(world):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    mp.spawn(_full_batch_worker, args=(4, _port(), q), nprocs=4, join=True)
-    res = [q.get() for _ in range(4)]
+    mp.spawn(_full_batch_worker, args=(world, _port(), q), nprocs=world, join=True)
+    res = [q.get() for _ in range(world)]
     assert all(ok_g for _, ok_g, _, _ in res), res
     assert all(ok_b for _, _, ok_b, _ in res), res
     assert all(nb > 1 for *_, nb in res)

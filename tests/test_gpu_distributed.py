@@ -152,13 +152,13 @@ def test_bench_rccl_path_world1(gpu, tmp_path):
     """The RCCL code path on the real backend: one rank over `nccl` (RCCL) with --ddp, so the process
     group, the bucketed gradient all-reduce of the arena (rebuilt in grad-ready order after step 1) and the
     step's RCCL calls all run on the GPU (one device -> world size 1; more ranks are the driver's 8-GPU
-    runs).  A step with collectives is never graph-captured."""
+    runs).  --graph-ddp off: the uncaptured step, whose per-bucket RCCL evidence pass this checks."""
     import json
     s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
            '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '1', '--ddp',
            '--steps', '3', '--warmup', '2', '--batch', '4', '--size', '64', '--train-images', '8',
-           '--val-images', '4']
+           '--val-images', '4', '--graph-ddp', 'off']
     r = subprocess.run(cmd, env=dict(os.environ), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     errs = [ln for ln in r.stderr.splitlines() if 'rror' in ln or 'what()' in ln or 'Exception' in ln][:20]
     assert r.returncode == 0, '\n'.join(errs) + '\n...\n' + r.stderr[-2000:]
@@ -189,3 +189,35 @@ def test_main_torchrun_world1_graph(gpu, tmp_path):
     log = open(tmp_path / 'save' / 'medseg_trainer.log').read()   # MyConfig.logger_name
     assert 'hipGraph capture on' in log and 'gradient bucketer off' in log, log[-2000:]
     assert os.path.isfile(tmp_path / 'save' / 'last.pth')
+
+
+def test_graph_captured_rccl_step_bitwise_world1(gpu, tmp_path):
+    """The multi-rank step captured in ONE hipGraph with its RCCL calls (gradient bucket all-reduces, the
+    bucketer attached at world 1) replays bitwise like the eager multi-rank step: parameters and every
+    step's loss (tools/graph_ddp_check.py under torchrun, the real `nccl` backend)."""
+    import json
+    s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'tools', 'graph_ddp_check.py')]
+    r = subprocess.run(cmd, env=dict(os.environ, GDC_STEPS='5'), capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert r.returncode == 0 and len(line) == 1, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads(line[0])
+    assert d['graph_captured'] and d['bucketer'] and d['buckets'] >= 1 and d['buckets_rebuilt'], d
+    assert all(d['losses_equal']) and d['n_mismatch'] == 0, d
+
+
+def test_bench_rccl_graph_world1(gpu, tmp_path):
+    """bench.py's multi-rank mode with --graph-ddp on: the RCCL step is hipGraph-captured and benches."""
+    import json
+    s = socket.socket(); s.bind(('127.0.0.1', 0)); port = s.getsockname()[1]; s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '1', '--ddp',
+           '--steps', '3', '--warmup', '2', '--batch', '4', '--size', '64', '--train-images', '8',
+           '--val-images', '4', '--graph-ddp', 'on']
+    r = subprocess.run(cmd, env=dict(os.environ), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    d = json.loads(line[0])
+    assert d['config']['hipgraph'] is True and d['value'] > 0 and d['n_gpus'] == 1
