@@ -1088,18 +1088,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_set_gemm", [](bool on) { conv_gemm_set(on ? 1 : 0); });
   m.def("conv_gemm_force_cfg", [](int64_t c) { conv_gemm_force_cfg((int)c); });
   m.def("conv_gemm_num_cfgs", []() { return conv_gemm_num_cfgs(); });
-  m.def("conv_set_hgemm", [](bool on) { conv_hgemm_set(on ? 1 : 0); });
-  m.def("conv_hgemm_force_cfg", [](int64_t c) { conv_hgemm_force_cfg((int)c); });
-  m.def("conv_hgemm_num_cfgs", []() { return conv_hgemm_num_cfgs(); });
-  m.def("conv_uses_hgemm", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
-    return conv_uses_hgemm(make_geom(dims, dy, dx));
-  });
-  m.def("conv_hgemm_plan", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
-    long v[8];
-    std::vector<int64_t> out;
-    if (conv_hgemm_plan_info(make_geom(dims, dy, dx), v)) out.assign(v, v + 8);
-    return out;
-  });
   m.def("conv_set_wgrad_gemm", [](int64_t mode) { conv_wgrad_gemm_set((int)mode); });
   m.def("conv_wgrad_gemm_force_cfg", [](int64_t c) { conv_wgrad_gemm_force_cfg((int)c); });
   m.def("conv_wgrad_gemm_num_cfgs", []() { return conv_wgrad_gemm_num_cfgs(); });

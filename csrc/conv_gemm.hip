@@ -61,9 +61,8 @@ DEVI void glds16(const void* src, uint32_t lds) {
   return;
 #endif
   unsigned keep;
-  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);   // (wave-uniform by contract; forces an SGPR)
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
@@ -124,8 +123,10 @@ struct GemmCfg {
 // between two LDS-DMAs makes the compiler drain every DMA in flight (vmcnt(0)) before it.
 struct TapGrid { int kw, y0, ys, x0, xs; };
 
-template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE>
-__global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, GemmGeom gg, TapGrid tg) {
+// OCC: the minimum blocks per CU the register allocation must allow (2: the planner's tiles; 3-4: the
+// small-LDS BK-32 tiles, round 6 occupancy A/B)
+template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE, int OCC = 2>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void conv_gemm_kernel(ConvArgs a, GemmGeom gg, TapGrid tg) {
   using C = GemmCfg<WM, WN, FM, FN, NS, BK>;
   constexpr int kRowB = C::ROWB, RPI = C::RPI;
   const ConvGeom& g = a.g;
@@ -416,376 +417,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvArgs a, 
   }
 }
 
-// =====================================================================================================
-// Halo-staged implicit GEMM (round 6): stride-1 multi-tap convs (3x3 d1/d2/d3, 1x7, 7x1) from 64 input
-// channels up -- the forward AND the data-gradient (flipped taps) of the reference's wide DUCK / residual
-// convs (reference models/ducknet.py:103-110,141-179, models/modules.py:73-85).
-//
-// Why: the im2col kernel above stages the B operand per (tap, channel) stage, so every input pixel goes
-// through TA/TD once per tap (9x for a 3x3): its knock-outs showed the loads, not the MFMAs, setting the
-// time (profiles/r05/gemm_knockouts_bs320.txt).  Here the B operand of one 64-channel chunk is staged ONCE
-// as a halo box (the tile's input pixels + the tap reach) and every tap reads it through a shifted LDS
-// address; only the weights (A) are staged per tap.
-//
-// Tiling.  The image width is cut into strips of TW columns (TW | W); a strip's pixels are walked in
-// (image, row, column) raster order ("stacked rows": R = n*H + h), and a tile is TPX consecutive pixels of
-// that order -- at the deep levels a tile spans several rows of one or two images.  The halo box = the
-// tile's stacked rows + the tap reach (ymin..ymax) x the strip's columns + the reach (xmin..xmax), loaded
-// from the real neighbouring pixels (or a zero page outside the tensor); taps that leave the image (row
-// or column) are masked per pixel on the READ (a zero LDS row), so a box row that belongs to the next image
-// is harmless.
-// LDS image: pixel e of the box at e*128 B, 16-B slot swizzled by key(e) = (L(e) >> 1) & 7 with
-// L = box_row*TW + box_col: for a fixed tap, consecutive tile pixels have consecutive L (and the box row
-// pitch HC = TW + xreach keeps the parity of L), so the 16 lanes of a ds_read_b128 group hit 16 distinct
-// bank slots.
-// Pipeline (4-wave blocks, two per CU -- the other block computes while one waits, as in the im2col
-// kernel): step = (channel chunk, tap).  The weights are double-buffered one step ahead (vmcnt(0) +
-// barrier per step); the halo box is single-buffered and reloaded at each chunk's first step.
-// (A first version ran 8-wave blocks at one per CU with both operands two steps ahead: the blocks' own
-// fill and drain -- 18 steps at 68 channels -- were exposed with nothing else on the CU: 2-3x slower.)
-// =====================================================================================================
-struct HgGeom {
-  int H, W, TW;       // image (stride 1: input == output size), strip width (divides W)
-  long NH;            // stacked rows = N*H
-  long slen;          // pixels per strip = NH*TW
-  int tps;            // tiles per strip
-  int n_co;
-  int HR, HC, HP;     // halo box rows, columns, pixels
-  int ymin, xmin;     // tap reach (lowest offsets)
-  int hbuf;           // bytes of the halo buffer
-  int abuf;           // bytes of one weight buffer
-  long ntiles;
-  int pxg;            // pixel tiles per block group (the group's blocks walk its tiles per co tile)
-};
-
-template <int WM, int WN, int FM, int FN>
-struct HgCfg {
-  static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int TCO = 32 * WM * FM, TPX = 32 * WN * FN;
-  static constexpr int A_INS = TCO / 8 / NW;   // weight DMA instructions per wave (8 rows each)
-  static_assert(NW == 4, "4-wave blocks, two per CU");
-  static_assert(TCO % (8 * NW) == 0, "every wave issues the same weight DMAs (counted waits)");
-  static_assert(TPX % 128 == 0 && WN % (TPX / 128) == 0, "128-pixel stat rows");
-};
-
-template <int WM, int WN, int FM, int FN, bool BNE>
-__global__ __launch_bounds__(256, 2) void conv_hgemm_kernel(ConvArgs a, HgGeom hg, TapGrid tg) {
-  using C = HgCfg<WM, WN, FM, FN>;
-  const ConvGeom& g = a.g;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t sbase = (uint32_t)(uintptr_t)(lds_u8_t*)smem;
-  // LDS: [A0 | A1 | A2 | H | zero row]
-  const uint32_t h_off = 3 * hg.abuf, z_off = 3 * hg.abuf + hg.hbuf;
-
-  // XCD-aware bijective remap (each XCD owns a contiguous wgid range), then groups of pxg pixel tiles: the
-  // group's blocks walk its pixel tiles for one co tile before the next co tile, so the blocks an XCD runs
-  // at a time share one co tile's weight rows in its L2 (the weights are re-staged per tap)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
-  const long span_g = (long)hg.n_co * hg.pxg;
-  const long grp = wgid / span_g;
-  const int rg = (int)(wgid - grp * span_g);
-  const int pg = (int)min((long)hg.pxg, hg.ntiles - grp * hg.pxg);
-  const int co_t = rg / pg;
-  const long tile = grp * hg.pxg + (rg - co_t * pg);
-  const int strip = (int)(tile / hg.tps);
-  const long v0 = (tile - (long)strip * hg.tps) * C::TPX;   // first pixel of the tile in the strip's raster
-  const int col0 = strip * hg.TW;
-  const long R0 = v0 / hg.TW;                               // first stacked row of the tile
-  const int co0 = co_t * C::TCO;
-  const int rows = g.Go * g.Cgo;
-  const int Cgi = g.Cgi, Gi = g.Gi, Cip = g.Gi * g.Cgi;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_page);
-
-  // zero row (masked taps read it); the barrier precedes every DMA
-  if (tid < 8) *reinterpret_cast<uint4*>(smem + z_off + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
-
-  auto gptr = [&](int q) {
-    const uint16_t* xb = a.x[0];
-#pragma unroll
-    for (int u = 1; u < kMaxGroups; ++u) xb = q == u ? a.x[u] : xb;
-    return xb;
-  };
-
-  // ---- weight DMA roles: instruction j fills rows 8*(j*NW + wave) + lane/8; physical slot lane%8 holds
-  // logical slot ls = (lane%8) ^ swz(row), swz(row) = (row >> 1) & 7 (independent of j: NW even)
-  const int a_ls = (lane & 7) ^ (((8 * wave + (lane >> 3)) >> 1) & 7);
-  const uint16_t* a_src[C::A_INS];
-#pragma unroll
-  for (int j = 0; j < C::A_INS; ++j) {
-    const int co = co0 + 8 * (j * C::NW + wave) + (lane >> 3);
-    a_src[j] = a.w + (long)(co < rows ? co : 0) * g.Kp;
-  }
-  // weights of one 64-wide K step: taps t0 .. t0 + 64/ch - 1 of chunk (group gi, channels c0 .. c0+ch-1) --
-  // the lane's k = 8*a_ls is tap t0 + 8*a_ls / ch, channel c0 + 8*a_ls % ch -- into weight buffer b
-  auto stage_a = [&](int t0, int gi, int c0, int ch, int b) {
-    const int kt = t0 + (8 * a_ls) / ch, kc = c0 + (8 * a_ls) % ch;
-    const int kcol = kt * Cip + gi * Cgi + kc;
-    const bool ok = kt < g.T && kc < Cgi;
-#pragma unroll
-    for (int j = 0; j < C::A_INS; ++j) {
-      if (8 * (j * C::NW + wave) < C::TCO)   // (wave-uniform)
-        glds16(ok ? (const void*)(a_src[j] + kcol) : (const void*)zero,
-               sbase + b * hg.abuf + (8 * (j * C::NW + wave)) * 128);
-    }
-  };
-  // the halo box of chunk (gi, c0, ch): instruction gq covers box pixels 8*gq .. +7, one 16-B slot per lane
-  const float inv_hc = 1.f / (float)hg.HC;
-  auto stage_h = [&](int gi, int c0, int ch) {
-    const uint16_t* xg = gptr(gi);
-    for (int gq = wave; 8 * gq < hg.HP; gq += C::NW) {
-      const int e = 8 * gq + (lane >> 3);
-      const uint16_t* src = zero;
-      if (e < hg.HP) {
-        const int hr = fdiv(e, hg.HC, inv_hc);
-        const int hc = e - hr * hg.HC;
-        const int ls = (lane & 7) ^ (((hr * hg.TW + hc) >> 1) & 7);
-        const long R = R0 + hg.ymin + hr;
-        const int col = col0 + hg.xmin + hc;
-        if (R >= 0 && R < hg.NH && (unsigned)col < (unsigned)hg.W && 8 * ls < ch && c0 + 8 * ls < Cgi)
-          src = xg + (R * hg.W + col) * Cgi + c0 + 8 * ls;
-      }
-      glds16(src, sbase + h_off + gq * 1024);
-    }
-  };
-
-  // ---- B fragment geometry (per lane, per fragment column j): box index / swizzle base at the lowest
-  // tap, and the mask of taps that stay inside the image
-  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int lr = lane & 31, lh = lane >> 5;
-  int b_hid[FN], b_L[FN];
-  uint32_t b_vm[FN];
-  long b_m[FN];   // output pixel (flat NHW index), -1 past the strip
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int p = (wn * FN + j) * 32 + lr;
-    const long v = v0 + p;
-    b_vm[j] = 0u;
-    b_m[j] = -1;
-    const long R = v / hg.TW;
-    const int x = (int)(v - R * hg.TW);
-    const int hr0 = (int)(R - R0), hc0 = x;
-    b_hid[j] = hr0 * hg.HC + hc0;
-    b_L[j] = hr0 * hg.TW + hc0;
-    if (v < hg.slen) {
-      const int h = (int)(R % hg.H);
-      const int col = col0 + x;
-      b_m[j] = R * hg.W + col;
-      uint32_t vm = 0u;
-      int tr = 0, tc = 0;
-      for (int t = 0; t < g.T; ++t) {
-        const int ih = h + tg.y0 + tr * tg.ys, iw = col + tg.x0 + tc * tg.xs;
-        if ((unsigned)ih < (unsigned)hg.H && (unsigned)iw < (unsigned)hg.W) vm |= 1u << t;
-        if (++tc == tg.kw) { tc = 0; ++tr; }
-      }
-      b_vm[j] = vm;
-    }
-  }
-  const int a_row0 = (wm * FM * 32 + lr) * 128;
-  const int a_key = (lr >> 1) & 7;   // == swz(row) of every fragment row (row bases are multiples of 32)
-
-  f32x16_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // ---- the K walk: chunks of 64 channels per input group (a narrower tail chunk rounded up to 16 / 32;
-  // 48 to 64 -- the channels past Cgi stage as zeros on the B side); every step is 64 deep: one tap of a
-  // 64-wide chunk, 2 taps of a 32-wide one, 4 taps of a 16-wide one (one branch-free MFMA block: a
-  // separate narrow-step path made the compiler copy every accumulator at the merge, each step)
-  const int nch = (Cgi + 63) / 64;
-  const int nchunks = Gi * nch;
-  const int T = g.T;
-  auto chunk_w = [&](int c0_) { const int r = Cgi - c0_; return r >= 33 ? 64 : (r > 16 ? 32 : 16); };
-  int gi = 0, c0 = 0, ch = chunk_w(0);
-  int u = 0, nu = (T * ch + 63) / 64;   // step in chunk, steps in chunk
-  long nsteps = 0;
-  for (int cc = 0; cc < nchunks; ++cc) nsteps += (T * chunk_w((cc % nch) * 64) + 63) / 64;
-  // the walk two steps ahead (weights are issued two steps before use: 3 buffers, counted waits)
-  int c2 = 0, u2 = 0, gi2 = 0, c02 = 0, ch2 = ch, nu2 = nu;
-  auto adv2 = [&]() {
-    if (++u2 == nu2) {
-      u2 = 0; ++c2;
-      gi2 = c2 / nch; c02 = (c2 - gi2 * nch) * 64; ch2 = chunk_w(c02); nu2 = (T * ch2 + 63) / 64;
-    }
-  };
-  stage_h(0, 0, ch);
-  stage_a(0, 0, 0, ch, 0);
-  adv2();
-  if (nsteps > 1) stage_a(u2 * (64 / ch2), gi2, c02, ch2, 1);
-  adv2();
-  int c = 0, ab = 0;
-  for (long i = 0; i < nsteps; ++i) {
-    // this step's weights were issued two steps ago: only the next step's (issued last step) stay in flight
-    if (i + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::A_INS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (u == 0 && c > 0) {   // a new chunk: every wave is done with the previous box -> reload it
-      stage_h(gi, c0, ch);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const int t0 = u * (64 / ch);
-    // the weights of step i + 2 (buffer (i + 2) % 3: its last reader was step i - 1)
-    if (i + 2 < nsteps) {
-      stage_a(u2 * (64 / ch2), gi2, c02, ch2, ab == 0 ? 2 : ab - 1);
-      adv2();
-    }
-    // ---- MFMAs of this step: k-step s reads tap t0 + 16*s / ch at chunk slot (16*s % ch) / 8 + lh
-    const uint8_t* Ab = smem + ab * hg.abuf;
-    int b_addr[4][FN];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int ts = t0 + (16 * s) / ch, slot = ((16 * s) % ch) / 8 + lh;
-      const int tr = ts / tg.kw, tc = ts - (ts / tg.kw) * tg.kw;
-      const int dyo = tg.y0 + tr * tg.ys - hg.ymin, dxo = tg.x0 + tc * tg.xs - hg.xmin;
-      const int dH = dyo * hg.HC + dxo, dL = dyo * hg.TW + dxo;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const bool ok = ts < T && ((b_vm[j] >> (ts & 31)) & 1u);
-        const int key = ((b_L[j] + dL) >> 1) & 7;
-        b_addr[s][j] = ok ? (int)(h_off + (b_hid[j] + dH) * 128 + ((slot ^ key) << 4)) : (int)z_off;
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint4 af[FM], bfr[FN];
-      const int asl = ((2 * s + lh) ^ a_key) << 4;
-#pragma unroll
-      for (int ii = 0; ii < FM; ++ii) af[ii] = *reinterpret_cast<const uint4*>(Ab + a_row0 + ii * 32 * 128 + asl);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(smem + b_addr[s][j]);
-#pragma unroll
-      for (int ii = 0; ii < FM; ++ii)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[ii][j] = mfma32(af[ii], bfr[j], acc[ii][j]);
-    }
-    // ---- advance the walk
-    ab = ab == 2 ? 0 : ab + 1;
-    if (++u == nu) {
-      u = 0;
-      ++c;
-      gi = c / nch;
-      c0 = (c - gi * nch) * 64;
-      ch = chunk_w(c0);
-      nu = (T * ch + 63) / 64;
-    }
-  }
-  __syncthreads();   // every wave is done with the stages before the epilogue reuses them
-  // ---- epilogue (as conv_gemm_kernel; pixel m from the strip raster)
-  float* s_st = reinterpret_cast<float*>(smem);   // [WN][2][TCO]
-  const bool stats = a.stat_part != nullptr;
-#pragma unroll
-  for (int ii = 0; ii < FM; ++ii) {
-    const int rb = wm * FM * 32 + ii * 32;
-    uint16_t* yb[4];
-    int cl4[4];
-    float cs[16], cq[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int cb = co0 + rb + 8 * q + 4 * lh;
-      const int og = cb < rows ? cb / g.Cgo : 0;
-      cl4[q] = cb - og * g.Cgo;
-      uint16_t* yg = a.y[0];
-#pragma unroll
-      for (int u = 1; u < kMaxGroups; ++u) yg = og == u ? a.y[u] : yg;
-      yb[q] = cb < rows ? yg + cl4[q] : nullptr;
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) { cs[e] = 0.f; cq[e] = 0.f; }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const long m = b_m[j];
-      if (m < 0) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (yb[q] == nullptr) continue;
-        uint16_t* yp = yb[q] + m * g.Cgo;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[ii][j][4 * q + r];
-        if (a.bias != nullptr) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = cl4[q] + r < g.Cgo_l ? v[r] + a.bias[cl4[q] + r] : 0.f;
-        }
-        if (!BNE && a.accum) {
-          const uint2 ov = *reinterpret_cast<const uint2*>(yp);
-          v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
-          v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
-        }
-        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-        st_stream8(yp, lo, hi);
-        const float w4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-        if constexpr (BNE) {
-          const int cb = cl4[q];
-          const uint2 yy = *reinterpret_cast<const uint2*>(a.bn_y + m * g.Cgo + cb);
-          const float4 sc = *reinterpret_cast<const float4*>(a.bn_coef + cb);
-          const float4 sh = *reinterpret_cast<const float4*>(a.bn_coef + g.Cgo + cb);
-          const float4 mu = *reinterpret_cast<const float4*>(a.bn_coef + 2 * g.Cgo + cb);
-          const float y4[4] = {__uint_as_float(yy.x << 16), __uint_as_float(yy.x & 0xffff0000u),
-                               __uint_as_float(yy.y << 16), __uint_as_float(yy.y & 0xffff0000u)};
-          const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w};
-          const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float gr = (!a.bn_relu || fmaf(y4[r], s4[r], h4[r]) > 0.f) ? w4[r] : 0.f;
-            cs[4 * q + r] += gr;
-            cq[4 * q + r] = fmaf(gr, y4[r] - m4[r], cq[4 * q + r]);
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            cs[4 * q + r] += w4[r];
-            cq[4 * q + r] = fmaf(w4[r], w4[r], cq[4 * q + r]);
-          }
-        }
-      }
-    }
-    if (stats) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float s = row16_sum(cs[e]), q = row16_sum(cq[e]);
-        s += __shfl_xor(s, 16, 64);
-        q += __shfl_xor(q, 16, 64);
-        if (lr == 0) {
-          const int row = rb + 8 * (e >> 2) + 4 * lh + (e & 3);
-          s_st[(wn * 2 + 0) * C::TCO + row] = s;
-          s_st[(wn * 2 + 1) * C::TCO + row] = q;
-        }
-      }
-    }
-  }
-  if (stats) {
-    __syncthreads();
-    // one partial row per 128-pixel half of the tile; every row written (an empty half writes zeros)
-    constexpr int HALVES = C::TPX / 128, WPH = WN / HALVES;
-    for (int e = tid; e < HALVES * C::TCO; e += C::NT) {
-      const int hb2 = e / C::TCO, cc = e - hb2 * C::TCO;
-      const int co = co0 + cc;
-      if (co >= rows) continue;
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WPH; ++w) {
-        const int wv = hb2 * WPH + w;
-        s += s_st[(wv * 2 + 0) * C::TCO + cc];
-        q += s_st[(wv * 2 + 1) * C::TCO + cc];
-      }
-      const long srow = tile * HALVES + hb2;
-      a.stat_part[(srow * 2 + 0) * rows + co] = s;
-      a.stat_part[(srow * 2 + 1) * rows + co] = q;
-    }
-  }
-}
-
 // ---- configurations ------------------------------------------------------------------------------
 // (WM, WN, FM, FN): TCO = 32*WM*FM co rows x TPX = 32*WN*FN pixels per block
 struct CfgId { int wm, wn, fm, fn, ns, bk; };
@@ -804,11 +435,16 @@ constexpr CfgId kCfgs[] = {
     {2, 2, 3, 2, 4, 32},   // 192 x 128, 4 stages (80 KB)
     {2, 2, 4, 2, 3, 32},   // 256 x 128, 3 stages (72 KB)
     {2, 2, 2, 2, 5, 32},   // 128 x 128, 5 stages (80 KB)
+    // round 6: a small-LDS tile at four blocks per CU -- the planner's pick for short-K launches (see
+    // gemm_pick_cfg; 192 x 128 / 128 x 128 3-stage / 64 x 128 tiles at 3-4 blocks per CU measured slower at
+    // every level 3-6 shape: profiles/r06/gemm_occupancy_bs320.txt)
+    {2, 2, 2, 2, 2, 32},   // 128 x 128, 2 stages (32 KB), 4 blocks / CU
     // (8-wave 128 x 256 tiles at 3 x 64-wide stages, one block per CU, measured 15-35 % slower than the
     // planner's tiles at every level 3-6 shape: profiles/r05/gemm_cfg_8wave_3stage_bs320.txt)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
-constexpr int kPlannerCfgs = 5;   // the planner's candidates (the rest: conv_gemm_force_cfg A/B only)
+constexpr int kPlannerCfgs = 5;   // the planner's row-tile candidates (5-8: conv_gemm_force_cfg A/B only)
+constexpr int kOccCfg = 9;        // the four-blocks-per-CU tile (short K)
 constexpr int kGemmTPX = 128;   // stat partial rows = pixel tiles of 128 (a 256-pixel tile writes two rows)
 
 int g_gemm_mode = -1;     // env MSP_CONV_GEMM: 0 off, else on (default on)
@@ -823,8 +459,12 @@ void gemm_env() {
   }
 }
 
-// co-tile choice: minimise (padded MFMA rows) + (pixel-operand re-staging per extra co tile)
-int gemm_pick_cfg(int rows) {
+// co-tile choice: minimise (padded MFMA rows) + (pixel-operand re-staging per extra co tile).  Then the
+// occupancy rule (round 6, profiles/r06/gemm_occupancy_bs320.txt): a launch of <= 12 BK-64 stages is bound by
+// its blocks' fill and drain, which two blocks per CU cannot overlap -- the 32-KB tile at four blocks per CU
+// wins there (L3 3x3 / d3 / 1x7 -9..-17 %, 1x1 shortcuts -11..-34 %) unless its 128-row tile pads the rows
+// more than 1.35x the planner's tile (L3 fused-2, L4 3x3: 144 / 136 rows); longer K keeps the 2-block tiles.
+int gemm_pick_cfg(int rows, int nk64) {
   if (g_gemm_cfg >= 0) return g_gemm_cfg;
   int best = 0;
   double best_cost = 1e30;
@@ -834,6 +474,8 @@ int gemm_pick_cfg(int rows) {
     const double cost = (double)tiles * (tco + 48.0);   // + the B-operand staging each co tile repeats
     if (cost < best_cost - 1e-9) { best_cost = cost; best = c; }
   }
+  const int tb = 32 * kCfgs[best].wm * kCfgs[best].fm, to = 32 * kCfgs[kOccCfg].wm * kCfgs[kOccCfg].fm;
+  if (nk64 <= 12 && (double)cdiv(rows, to) * to <= 1.35 * cdiv(rows, tb) * tb) return kOccCfg;
   return best;
 }
 
@@ -853,7 +495,7 @@ bool tap_grid(const ConvGeom& g, TapGrid& tg) {
   return false;
 }
 
-template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE>
+template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE, int OCC = 2>
 void launch_gemm(const ConvArgs& a, hipStream_t s) {
   using C = GemmCfg<WM, WN, FM, FN, NS, BK>;
   const ConvGeom& g = a.g;
@@ -865,13 +507,13 @@ void launch_gemm(const ConvArgs& a, hipStream_t s) {
   const long blocks = (long)cdiv(gg.M, C::TPX) * gg.n_co;
   static bool attr = false;
   if (!attr) {   // > 64 KB dynamic LDS: opted into once per instantiation, before any graph capture
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE, OCC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   TapGrid tg;
   (void)tap_grid(g, tg);   // conv_gemm_ok checked it
-  hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
+  hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE, OCC>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
                      tg);
 }
 
@@ -887,136 +529,12 @@ int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
     case 6: launch_gemm<2, 2, 3, 2, 4, 32, BNE>(a, s); return 0;
     case 7: launch_gemm<2, 2, 4, 2, 3, 32, BNE>(a, s); return 0;
     case 8: launch_gemm<2, 2, 2, 2, 5, 32, BNE>(a, s); return 0;
-    case 9: launch_gemm<2, 4, 2, 2, 3, 64, BNE>(a, s); return 0;
-    case 10: launch_gemm<1, 8, 4, 1, 3, 64, BNE>(a, s); return 0;
-  }
-  return 1;
-}
-
-// ---- halo-staged GEMM: configurations and planner ------------------------------------------------
-struct HgCfgId { int wm, wn, fm, fn; };
-constexpr HgCfgId kHgCfgs[] = {
-    {2, 2, 2, 2},   // 128 x 128
-    {2, 2, 3, 2},   // 192 x 128
-    {1, 4, 3, 1},   //  96 x 128
-    {1, 4, 5, 1},   // 160 x 128
-    {2, 2, 1, 2},   //  64 x 128
-    {1, 4, 7, 1},   // 224 x 128
-    {2, 2, 4, 2},   // 256 x 128
-    {1, 4, 3, 2},   //  96 x 256
-    {2, 2, 2, 4},   // 128 x 256
-};
-constexpr int kNumHgCfgs = sizeof(kHgCfgs) / sizeof(kHgCfgs[0]);
-constexpr int kHgLds = 80 * 1024;   // two blocks per CU
-int g_hg_mode = 1;     // conv_hgemm_set: 0 off (im2col GEMM for every wide conv), 1 on
-int g_hg_cfg = -1;     // conv_hgemm_force_cfg: one configuration for every launch (tests / A-B), -1 planner
-
-long igcd(long a, long b) { while (b) { const long t = a % b; a = b; b = t; } return a; }
-
-// the halo path's plan for one conv: false if the conv is not eligible or no configuration fits the LDS
-bool hg_plan(const ConvGeom& g, int& cfg_out, HgGeom& hg, TapGrid& tg) {
-  if (!g_hg_mode || g.stride != 1 || g.T < 2 || g.T > 32 || g.OH != g.IH || g.OW != g.IW) return false;
-  if (g.Cgi < 64 || g.Cgi % 8 != 0) return false;
-  if (!tap_grid(g, tg)) return false;
-  int ymin = 1 << 20, ymax = -(1 << 20), xmin = 1 << 20, xmax = -(1 << 20);
-  for (int t = 0; t < g.T; ++t) {
-    ymin = std::min(ymin, g.dy[t]); ymax = std::max(ymax, g.dy[t]);
-    xmin = std::min(xmin, g.dx[t]); xmax = std::max(xmax, g.dx[t]);
-  }
-  const int H = g.IH, W = g.IW, rows = g.Go * g.Cgo;
-  const long NH = (long)g.N * H;
-  const int nchunks = g.Gi * ((g.Cgi + 63) / 64);
-  double best = 1e300;
-  bool found = false;
-  for (int c = 0; c < kNumHgCfgs; ++c) {
-    if (g_hg_cfg >= 0 && c != g_hg_cfg) continue;
-    const int tco = 32 * kHgCfgs[c].wm * kHgCfgs[c].fm, tpx = 32 * kHgCfgs[c].wn * kHgCfgs[c].fn;
-    for (int TW = 1; TW <= W; ++TW) {
-      if (W % TW != 0 || (TW < 8 && TW != W)) continue;
-      const long gc = igcd(tpx, TW);
-      const int span = (int)((TW - gc + tpx - 1) / TW) + 1;   // stacked rows one tile touches (worst case)
-      const int HR = span + (ymax - ymin), HC = TW + (xmax - xmin);
-      const long HP = (long)HR * HC;
-      const long hbuf = (HP + 7) / 8 * 1024, abuf = (long)tco * 128;
-      if (3 * abuf + hbuf + 128 > kHgLds) continue;
-      const int n_co = cdiv(rows, tco);
-      const long tps = ((long)NH * TW + tpx - 1) / tpx;
-      const long ntiles = (long)(W / TW) * tps;
-      const long blocks = ntiles * n_co;
-      if (blocks >= (1L << 31)) continue;
-      // per-block cycle model at 2 blocks per CU (each gets half the CU): per (chunk, tap) step the larger
-      // of the MFMA time (2048 MAC/clk/CU) and the weight DMA (64 B/clk/CU), a halo reload per chunk (its
-      // bytes + a latency the other block covers only partly), + the epilogue's stores
-      const double mf = (double)tco * tpx * 2.0 / 32.0 * 2.0, ld = 2.0 * tco * 2.0;
-      const double reload = 2.0 * HP * 2.0 + 600.0;
-      const double blk = (double)nchunks * (g.T * std::max(mf, ld) + reload) + (double)tco * tpx * 2.0 / 32.0 + 1500.0;
-      const double cost = (double)((blocks + 511) / 512) * blk;
-      if (cost < best * (1.0 - 1e-9)) {
-        best = cost;
-        found = true;
-        cfg_out = c;
-        hg.H = H; hg.W = W; hg.TW = TW; hg.NH = NH; hg.slen = NH * TW; hg.tps = (int)tps; hg.n_co = n_co;
-        hg.HR = HR; hg.HC = HC; hg.HP = (int)HP; hg.ymin = ymin; hg.xmin = xmin;
-        hg.hbuf = (int)hbuf; hg.abuf = (int)abuf; hg.ntiles = ntiles;
-        hg.pxg = (int)std::min<long>(64, ntiles);
-      }
-    }
-  }
-  return found;
-}
-
-template <int WM, int WN, int FM, int FN, bool BNE>
-void launch_hgemm(const ConvArgs& a, const HgGeom& hg, const TapGrid& tg, hipStream_t s) {
-  using C = HgCfg<WM, WN, FM, FN>;
-  const size_t lds = 3 * (size_t)hg.abuf + (size_t)hg.hbuf + 128;
-  static bool attr = false;
-  if (!attr) {   // > 64 KB dynamic LDS: opted into once per instantiation, before any graph capture
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_hgemm_kernel<WM, WN, FM, FN, BNE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kHgLds);
-    attr = true;
-  }
-  const long blocks = hg.ntiles * hg.n_co;
-  hipLaunchKernelGGL((conv_hgemm_kernel<WM, WN, FM, FN, BNE>), dim3((unsigned)blocks), dim3(C::NT), lds, s, a, hg, tg);
-}
-
-template <bool BNE>
-int dispatch_hgemm(const ConvArgs& a, int cfg, const HgGeom& hg, const TapGrid& tg, hipStream_t s) {
-  switch (cfg) {
-    case 0: launch_hgemm<2, 2, 2, 2, BNE>(a, hg, tg, s); return 0;
-    case 1: launch_hgemm<2, 2, 3, 2, BNE>(a, hg, tg, s); return 0;
-    case 2: launch_hgemm<1, 4, 3, 1, BNE>(a, hg, tg, s); return 0;
-    case 3: launch_hgemm<1, 4, 5, 1, BNE>(a, hg, tg, s); return 0;
-    case 4: launch_hgemm<2, 2, 1, 2, BNE>(a, hg, tg, s); return 0;
-    case 5: launch_hgemm<1, 4, 7, 1, BNE>(a, hg, tg, s); return 0;
-    case 6: launch_hgemm<2, 2, 4, 2, BNE>(a, hg, tg, s); return 0;
-    case 7: launch_hgemm<1, 4, 3, 2, BNE>(a, hg, tg, s); return 0;
-    case 8: launch_hgemm<2, 2, 2, 4, BNE>(a, hg, tg, s); return 0;
+    case 9: launch_gemm<2, 2, 2, 2, 2, 32, BNE, 4>(a, s); return 0;
   }
   return 1;
 }
 
 }  // namespace
-
-void conv_hgemm_set(int on) { g_hg_mode = on ? 1 : 0; }
-void conv_hgemm_force_cfg(int cfg) { g_hg_cfg = (cfg >= 0 && cfg < kNumHgCfgs) ? cfg : -1; }
-int conv_hgemm_num_cfgs() { return kNumHgCfgs; }
-bool conv_hgemm_plan_info(const ConvGeom& g, long* out) {
-  int cfg;
-  HgGeom hg;
-  TapGrid tg;
-  if (!(conv_gemm_ok(g, false) && hg_plan(g, cfg, hg, tg))) return false;
-  const long v[8] = {cfg, 32L * kHgCfgs[cfg].wm * kHgCfgs[cfg].fm, 32L * kHgCfgs[cfg].wn * kHgCfgs[cfg].fn, hg.TW,
-                     hg.HP, hg.n_co, hg.ntiles, 3L * hg.abuf + hg.hbuf + 128};
-  for (int i = 0; i < 8; ++i) out[i] = v[i];
-  return true;
-}
-
-bool conv_uses_hgemm(const ConvGeom& g) {
-  int cfg;
-  HgGeom hg;
-  TapGrid tg;
-  return conv_gemm_ok(g, false) && hg_plan(g, cfg, hg, tg);
-}
 
 // Eligibility: a forward (or stride-1 data-gradient) conv whose every input group is >= 64 channels
 // wide, no transposed indexing (phase-decomposed elsewhere) and no deferred-BN input prologue (the
@@ -1035,31 +553,13 @@ void conv_gemm_set(int on) { gemm_env(); g_gemm_mode = on ? 1 : 0; }
 void conv_gemm_force_cfg(int cfg) { gemm_env(); g_gemm_cfg = (cfg >= 0 && cfg < kNumCfgs) ? cfg : -1; }
 int conv_gemm_num_cfgs() { return kNumCfgs; }
 
-long conv_gemm_stat_blocks(const ConvGeom& g) {
-  int cfg;
-  HgGeom hg;
-  TapGrid tg;
-  if (hg_plan(g, cfg, hg, tg)) return hg.ntiles * (32 * kHgCfgs[cfg].wn * kHgCfgs[cfg].fn / 128);
-  return cdiv((long)g.N * g.OH * g.OW, kGemmTPX);
-}
+long conv_gemm_stat_blocks(const ConvGeom& g) { return cdiv((long)g.N * g.OH * g.OW, kGemmTPX); }
 
 int conv_gemm(const ConvArgs& a, hipStream_t s) {
   gemm_env();
   for (int i = 0; i < a.g.Gi; ++i)
     if (a.xc[i] != nullptr) return 2;   // no prologue on this path (see conv_gemm_ok)
-  {
-    int hcfg;
-    HgGeom hg;
-    TapGrid tg;
-    if (hg_plan(a.g, hcfg, hg, tg))
-      return a.bn_y != nullptr ? dispatch_hgemm<true>(a, hcfg, hg, tg, s) : dispatch_hgemm<false>(a, hcfg, hg, tg, s);
-  }
-  const int cfg = gemm_pick_cfg(a.g.Go * a.g.Cgo);
+  const int cfg = gemm_pick_cfg(a.g.Go * a.g.Cgo, cdiv(a.g.Kp, 64));
   return a.bn_y != nullptr ? dispatch_gemm<true>(a, cfg, s) : dispatch_gemm<false>(a, cfg, s);
 }
 
-int conv_gemm_cfg_tco(int rows) {
-  gemm_env();
-  const int c = gemm_pick_cfg(rows);
-  return 32 * kCfgs[c].wm * kCfgs[c].fm;
-}

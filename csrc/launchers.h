@@ -103,14 +103,6 @@ int conv_gemm(const ConvArgs& a, hipStream_t s);
 void conv_gemm_set(int on);
 void conv_gemm_force_cfg(int cfg);   // tests / A-B: one tile configuration for every launch (-1: planner)
 int conv_gemm_num_cfgs();
-int conv_gemm_cfg_tco(int rows);
-// the halo-staged GEMM (stride-1 multi-tap wide convs; conv_gemm picks it when its planner fits)
-void conv_hgemm_set(int on);
-void conv_hgemm_force_cfg(int cfg);   // tests / A-B: one halo tile configuration (-1: planner)
-int conv_hgemm_num_cfgs();
-bool conv_uses_hgemm(const ConvGeom& g);
-// the plan: {cfg, TCO, TPX, strip width, halo pixels, co tiles, pixel tiles, LDS bytes}; false if not eligible
-bool conv_hgemm_plan_info(const ConvGeom& g, long* out);
 // dw: fp32 [Go*Cgo][T*Cip] (overwritten)
 int conv_plan_selfcheck(int verbose);   // host-only launch-planner invariants (sanitizer harness)
 int conv_wgrad_replicas(const ConvGeom& g, bool trans, bool bwd = false, bool pro = false);   // bwd: see conv_wgrad

@@ -29,7 +29,6 @@ def ext():
     yield C
     C.conv_gemm_force_cfg(-1)
     C.conv_set_gemm(True)
-    C.conv_set_hgemm(True)
     C.conv_set_wgrad_gemm(1)
 
 
@@ -48,12 +47,11 @@ GEMM_CASES = [
 ]
 
 
-@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize('case', GEMM_CASES)
 def test_gemm_conv_fwd_bwd(gpu, ext, case, cfg):
     n, h, w, ci, co, (kh, kw), s, pad, dil, groups, bias = case
     ext.conv_gemm_force_cfg(cfg)
-    ext.conv_set_hgemm(cfg < 0)   # a forced im2col configuration tests the im2col kernel on every shape
     torch.manual_seed(0)
     ms = [nn.Conv2d(ci, co, (kh, kw), s, pad, dil, bias=bias).to(gpu) for _ in range(groups)]
     br = [Branch(m.weight, g, 0, kh * kw) for g, m in enumerate(ms)]
@@ -152,7 +150,7 @@ WGRAD_CASES = [
 ]
 
 
-@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize('cfg', [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize('prologue', [False, True])
 @pytest.mark.parametrize('case', WGRAD_CASES)
 def test_wgrad_gemm(gpu, ext, case, prologue, cfg):

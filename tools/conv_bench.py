@@ -62,8 +62,7 @@ def main():
     ap.add_argument('--halo', type=int, default=1, help='1: halo-tiled stride-1 kernel where eligible, 0: gather only')
     ap.add_argument('--split', type=int, default=1, help='halo split-bank tile image: 0 never, 1 occupancy-preserving '
                     '(default), 2 wherever it fits (csrc/conv.hip halo_phys)')
-    ap.add_argument('--hgemm', type=int, default=1, help='1: halo-staged GEMM for stride-1 multi-tap wide convs, '
-                    '0: the im2col LDS-DMA GEMM')
+    ap.add_argument('--gemm-cfg', type=int, default=-1, help='force one LDS-DMA GEMM tile configuration (A/B)')
     ap.add_argument('--only', default='', help='substring filter on layer names')
     ap.add_argument('--levels', default='', help='comma list of levels to run (e.g. 3,4,5,6)')
     ap.add_argument('--prologue', action='store_true',
@@ -74,7 +73,7 @@ def main():
     C = _ext.require()
     C.conv_set_halo(bool(a.halo))
     C.conv_set_halo_split(a.split)
-    C.conv_set_hgemm(bool(a.hgemm))
+    C.conv_gemm_force_cfg(a.gemm_cfg)
     res = []
     tot = {'fwd': 0.0, 'dgrad': 0.0, 'wgrad': 0.0}
     for name, lvl, ci, co, k, s, p, d, groups in layers():
@@ -119,16 +118,13 @@ def main():
             xm = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
             wm = torch.randn(co * groups, ci, *k, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
             row['miopen_fwd_ms'] = round(timeit(lambda: F.conv2d(xm, wm, None, s, p, d), a.iters), 4)
-        row['hgemm_fwd'] = list(C.conv_hgemm_plan(dims, dy, dx))   # cfg, TCO, TPX, TW, HP, co tiles, tiles, LDS
-        row['hgemm_dgrad'] = list(C.conv_hgemm_plan(dims_d, bdy, bdx))
         row['halo_fwd'] = bool(C.conv_uses_halo(dims, dy, dx, False))
         row['halo_dgrad'] = bool(C.conv_uses_halo(dims_d, bdy, bdx, s > 1))
         res.append(row)
         tot['fwd'] += t_f; tot['dgrad'] += t_d; tot['wgrad'] += t_w
         print(f"{name:28s} fwd {t_f:7.3f} ms ({row['fwd_tflops']:6.1f} TF)  dgrad {t_d:7.3f} ({row['dgrad_tflops']:6.1f})"
               f"  wgrad {t_w:7.3f} ({row['wgrad_tflops']:6.1f})" +
-              (f"  miopen-fwd {row['miopen_fwd_ms']:7.3f}" if a.miopen else '') +
-              (f"  hg {row['hgemm_fwd'][:5]}" if row['hgemm_fwd'] else ''), flush=True)
+              (f"  miopen-fwd {row['miopen_fwd_ms']:7.3f}" if a.miopen else ''), flush=True)
     print(json.dumps({'batch': a.batch, 'size': a.size, 'halo': a.halo, 'split': a.split, 'layers': res, 'totals_ms': tot}))
 
 
