@@ -64,6 +64,7 @@ def parse_args(argv=None):
                    help='synthetic train split size (per rank; a larger --batch spans several epochs of it)')
     p.add_argument('--val-images', type=int, default=32, help='held-out synthetic val split for the Dice (0 = skip)')
     p.add_argument('--lr', type=float, default=1e-3, help='Adam lr per GPU (reference: 0.1 * base_lr * gpu_num)')
+    p.add_argument('--seed', type=int, default=1, help='trainer random_seed (model init, data order; MyConfig: 1)')
     p.add_argument('--comm-steps', type=int, default=3,
                    help='multi-GPU evidence pass after the timed region (0 = off): per-bucket RCCL timings, SyncBN '
                         'exchange count/time, and the step time with every collective knocked out')
@@ -300,6 +301,7 @@ def main(argv=None):
                            device_index=dev_index if (not ddp or same_dev) else None, teacher_name=args.teacher,
                            use_graph=use_graph, dist_backend=os.environ.get('BENCH_DIST_BACKEND') if ddp else None,
                            world=world, dist_world1_bucketer=ddp)
+        cfg.random_seed = args.seed
         if not cuda:
             cfg.base_workers = 0   # CPU rehearsal: batches built in-process
         step = TrainerStep(cfg, fixed=args.data == 'fixed')
