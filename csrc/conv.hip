@@ -1731,6 +1731,14 @@ void conv_set_phase(int on) { g_phase_mode = on ? 1 : 0; }
 static void conv_igemm_phased(const ConvArgs& a, int mi, hipStream_t s) {
   const ConvGeom& g = a.g;
   const int st = g.stride, Cip = g.Gi * g.Cgi;
+  // kernel width of the packed tap table (t = r*KW + c): T over the number of distinct row offsets
+  int nrow = 0;
+  for (int t = 0; t < g.T; ++t) {
+    bool seen = false;
+    for (int u = 0; u < t; ++u) seen |= g.dy[u] == g.dy[t];
+    nrow += seen ? 0 : 1;
+  }
+  const int KW = nrow > 0 ? g.T / nrow : 1;
   for (int py = 0; py < st; ++py)
     for (int px = 0; px < st; ++px) {
       PhaseArgs pa{};
@@ -1752,6 +1760,13 @@ static void conv_igemm_phased(const ConvArgs& a, int mi, hipStream_t s) {
       pa.Kloop = (tv * Cip + 31) / 32 * 32;
       ConvGeom gp = b.g;
       gp.OH = pa.OHp; gp.OW = pa.OWp;
+      // wide inputs (>= 64 channels): the phase as a stride-1 conv on the LDS-DMA GEMM kernel, which stores
+      // into the phase's pixels of the full output (round 6; the gather kernel stays for narrow inputs)
+      if (tv > 0) {
+        ConvArgs bg = b;
+        bg.g.OH = pa.OHp; bg.g.OW = pa.OWp; bg.g.stride = 1;
+        if (conv_gemm_phase(bg, pa.tA, KW, st, py, px, g.OH, g.OW, s) == 0) continue;
+      }
       dispatch_phase(b, pa, mi, conv_pick_wpx(gp, mi, 4), s);
     }
 }

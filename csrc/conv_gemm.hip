@@ -91,6 +91,11 @@ DEVI void kpos_advance(KPos& p, int by, int Cgi, int Gi) {
 struct GemmGeom {
   long M, OHW;
   int n_co, nk;
+  // phase output map (the phase-decomposed strided data-gradient, conv_gemm_phase): GEMM pixel m of the
+  // OHp x OWp phase grid stores at (py + ps*oh, px + ps*ow) of the full OH x OW output; ps = 0: identity
+  int ps, py, px, OWp;
+  long OHWp, OW, OHWf;
+  long apitch;   // packed weight row pitch (= Kp; a phase launch walks K = its own taps, rows keep the full pitch)
 };
 
 // BK = k per stage (64 or 32): one staged row (co or pixel) is BK bf16 = ROWB bytes, one DMA instruction
@@ -121,7 +126,12 @@ struct GemmCfg {
 // (dy, dx) = (y0 + r * ys, x0 + c * xs) -- forward taps (r*dil - pad) and data-gradient taps (pad - r*dil)
 // alike.  Kept as scalars so that the DMA address generation reads NO memory: an LDS or global read
 // between two LDS-DMAs makes the compiler drain every DMA in flight (vmcnt(0)) before it.
-struct TapGrid { int kw, y0, ys, x0, xs; };
+struct TapGrid {
+  int kw, y0, ys, x0, xs;
+  // packed-weight tap of grid tap (tr, tc): (ar0 + tr*ars)*akw + ac0 + tc*acs -- the identity (= tr*kw + tc)
+  // except for a phase launch, whose taps are a strided subset of the packed data-gradient taps
+  int akw, ar0, ars, ac0, acs;
+};
 
 // OCC: the minimum blocks per CU the register allocation must allow (2: the planner's tiles; 3-4: the
 // small-LDS BK-32 tiles, round 6 occupancy A/B)
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_gemm_kernel(ConvArgs a
 #pragma unroll
   for (int j = 0; j < C::A_INS; ++j) {
     const int co = co0 + RPI * (j * C::NW + wave) + lane / C::SLOTS;
-    a_src[j] = a.w + (long)(co < rows ? co : 0) * g.Kp + 8 * ls;
+    a_src[j] = a.w + (long)(co < rows ? co : 0) * gg.apitch + 8 * ls;
 #ifdef GK_KO_AMISS   // (profiling knock-out: every A row reads row 0 -- L2-resident)
     a_src[j] = a.w + 8 * ls;
 #endif
@@ -218,10 +228,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_gemm_kernel(ConvArgs a
     return xb;
   };
 
+  const int Cip_ = Gi * Cgi;
   auto stage = [&](int kt, uint32_t sb) {
     const int kb = kt * BK;
-#pragma unroll
-    for (int j = 0; j < C::A_INS; ++j) glds16(a_src[j] + kb, sb + (RPI * (j * C::NW + wave)) * kRowB);
     // the (group | tap) after the current one
     int g1 = g0 + 1, t1 = t0, tr1 = tr0, tc1 = tc0;
     long toff1 = toff0;
@@ -233,6 +242,13 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_gemm_kernel(ConvArgs a
     }
     const int rem0 = Cgi - cl0;
     const bool nx = 8 * ls >= rem0;   // (per lane)
+    // A: packed column of the lane's k -- contiguous, shifted by the tap remap of a phase launch (uniform
+    // per tap; past the last tap the contiguous continuation: finite weights times a zero B operand)
+    const int dA0 = ((tg.ar0 + tr0 * tg.ars) * tg.akw + tg.ac0 + tc0 * tg.acs - t0) * Cip_;
+    const int dA1 = t1 < g.T ? ((tg.ar0 + tr1 * tg.ars) * tg.akw + tg.ac0 + tc1 * tg.acs - t1) * Cip_ : dA0;
+    const int ka = kb + (nx ? dA1 : dA0);
+#pragma unroll
+    for (int j = 0; j < C::A_INS; ++j) glds16(a_src[j] + ka, sb + (RPI * (j * C::NW + wave)) * kRowB);
     const int t = nx ? t1 : t0;
     const uint16_t* base = (nx ? gptr(g1) : gptr(g0)) + (nx ? toff1 + (8 * ls - rem0) : toff0 + (cl0 + 8 * ls));
     const bool tin = t < 32;
@@ -329,8 +345,13 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_gemm_kernel(ConvArgs a
     for (int e = 0; e < 16; ++e) { cs[e] = 0.f; cq[e] = 0.f; }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const long m = px0 + wn * FN * 32 + j * 32 + lr;
+      long m = px0 + wn * FN * 32 + j * 32 + lr;
       if (m >= gg.M) continue;
+      if (gg.ps) {   // phase launch: the phase-grid pixel's place in the full output
+        const long n = m / gg.OHWp, r = m - n * gg.OHWp;
+        const long oh = r / gg.OWp, ow = r - oh * gg.OWp;
+        m = n * gg.OHWf + (gg.py + gg.ps * oh) * gg.OW + gg.px + gg.ps * ow;
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (yb[q] == nullptr) continue;
@@ -495,8 +516,16 @@ bool tap_grid(const ConvGeom& g, TapGrid& tg) {
   return false;
 }
 
+// phase launch of a strided data-gradient (conv_gemm_phase): the output map and the A tap remap; the
+// identity for every other launch
+struct GemmPhase {
+  int ps = 0, py = 0, px = 0, OHf = 0, OWf = 0;
+  long apitch = 0;   // 0: g.Kp
+  int akw = 0, ar0 = 0, ars = 1, ac0 = 0, acs = 1;   // akw 0: identity remap
+};
+
 template <int WM, int WN, int FM, int FN, int NS, int BK, bool BNE, int OCC = 2>
-void launch_gemm(const ConvArgs& a, hipStream_t s) {
+void launch_gemm(const ConvArgs& a, const GemmPhase& ph, hipStream_t s) {
   using C = GemmCfg<WM, WN, FM, FN, NS, BK>;
   const ConvGeom& g = a.g;
   GemmGeom gg;
@@ -504,6 +533,9 @@ void launch_gemm(const ConvArgs& a, hipStream_t s) {
   gg.M = (long)g.N * gg.OHW;
   gg.n_co = cdiv(g.Go * g.Cgo, C::TCO);
   gg.nk = cdiv(g.Kp, BK);
+  gg.ps = ph.ps; gg.py = ph.py; gg.px = ph.px; gg.OWp = g.OW;
+  gg.OHWp = gg.OHW; gg.OW = ph.OWf; gg.OHWf = (long)ph.OHf * ph.OWf;
+  gg.apitch = ph.apitch > 0 ? ph.apitch : g.Kp;
   const long blocks = (long)cdiv(gg.M, C::TPX) * gg.n_co;
   static bool attr = false;
   if (!attr) {   // > 64 KB dynamic LDS: opted into once per instantiation, before any graph capture
@@ -513,40 +545,60 @@ void launch_gemm(const ConvArgs& a, hipStream_t s) {
   }
   TapGrid tg;
   (void)tap_grid(g, tg);   // conv_gemm_ok checked it
+  if (ph.akw > 0) {
+    tg.akw = ph.akw; tg.ar0 = ph.ar0; tg.ars = ph.ars; tg.ac0 = ph.ac0; tg.acs = ph.acs;
+  } else {
+    tg.akw = tg.kw; tg.ar0 = 0; tg.ars = 1; tg.ac0 = 0; tg.acs = 1;
+  }
   hipLaunchKernelGGL((conv_gemm_kernel<WM, WN, FM, FN, NS, BK, BNE, OCC>), dim3((unsigned)blocks), dim3(C::NT), C::LDS, s, a, gg,
                      tg);
 }
 
 template <bool BNE>
-int dispatch_gemm(const ConvArgs& a, int cfg, hipStream_t s) {
+int dispatch_gemm(const ConvArgs& a, int cfg, const GemmPhase& ph, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_gemm<2, 2, 3, 2, 2, 64, BNE>(a, s); return 0;
-    case 1: launch_gemm<2, 2, 2, 2, 2, 64, BNE>(a, s); return 0;
-    case 2: launch_gemm<1, 4, 3, 1, 2, 64, BNE>(a, s); return 0;
-    case 3: launch_gemm<1, 4, 5, 1, 2, 64, BNE>(a, s); return 0;
-    case 4: launch_gemm<2, 2, 1, 2, 2, 64, BNE>(a, s); return 0;
-    case 5: launch_gemm<2, 2, 2, 2, 4, 32, BNE>(a, s); return 0;
-    case 6: launch_gemm<2, 2, 3, 2, 4, 32, BNE>(a, s); return 0;
-    case 7: launch_gemm<2, 2, 4, 2, 3, 32, BNE>(a, s); return 0;
-    case 8: launch_gemm<2, 2, 2, 2, 5, 32, BNE>(a, s); return 0;
-    case 9: launch_gemm<2, 2, 2, 2, 2, 32, BNE, 4>(a, s); return 0;
+    case 0: launch_gemm<2, 2, 3, 2, 2, 64, BNE>(a, ph, s); return 0;
+    case 1: launch_gemm<2, 2, 2, 2, 2, 64, BNE>(a, ph, s); return 0;
+    case 2: launch_gemm<1, 4, 3, 1, 2, 64, BNE>(a, ph, s); return 0;
+    case 3: launch_gemm<1, 4, 5, 1, 2, 64, BNE>(a, ph, s); return 0;
+    case 4: launch_gemm<2, 2, 1, 2, 2, 64, BNE>(a, ph, s); return 0;
+    case 5: launch_gemm<2, 2, 2, 2, 4, 32, BNE>(a, ph, s); return 0;
+    case 6: launch_gemm<2, 2, 3, 2, 4, 32, BNE>(a, ph, s); return 0;
+    case 7: launch_gemm<2, 2, 4, 2, 3, 32, BNE>(a, ph, s); return 0;
+    case 8: launch_gemm<2, 2, 2, 2, 5, 32, BNE>(a, ph, s); return 0;
+    case 9: launch_gemm<2, 2, 2, 2, 2, 32, BNE, 4>(a, ph, s); return 0;
   }
   return 1;
 }
 
 }  // namespace
 
-// Eligibility: a forward (or stride-1 data-gradient) conv whose every input group is >= 64 channels
-// wide, no transposed indexing (phase-decomposed elsewhere) and no deferred-BN input prologue (the
-// callers materialise wide deferred inputs: one normalise pass beats a per-k-step transform).
-bool conv_gemm_ok(const ConvGeom& g, bool trans) {
-  gemm_env();
-  if (!g_gemm_mode || trans) return false;
-  if (g.Cgi < 64 || g.Cgi % 8 != 0 || g.T > 30) return false;   // the DMA k walk needs >= 64 channels   // tap bitmask per pixel (stage())
+// (no transposed indexing -- phase-decomposed elsewhere -- and no deferred-BN input prologue: the callers
+// materialise wide deferred inputs, one normalise pass beats a per-k-step transform)
+// min_c: the narrowest input group the DMA K walk takes -- a stage may cross one (group | tap) boundary, so
+// Cgi >= the stage width: 64 for every tile, 32 with the 32-wide-stage tiles (gemm_tile_for)
+static bool gemm_geom_ok(const ConvGeom& g, int min_c) {
+  if (g.Cgi < min_c || g.Cgi % 8 != 0 || g.T > 30) return false;   // (T <= 30: the per-pixel tap bitmask)
   TapGrid tg;
   if (!tap_grid(g, tg)) return false;
   const long M = (long)g.N * g.OH * g.OW;
   return M >= 1 && (long)cdiv(M, kGemmTPX) * cdiv(g.Go * g.Cgo, 64) < (1L << 31);
+}
+
+// Eligibility: a forward (or stride-1 data-gradient) conv whose every input group is >= 64 channels wide --
+// or >= 32 for a STRIDED forward (the 40-channel level's 3x3 s2 downsampling conv), which runs a 32-wide
+// stage tile; narrower stride-1 convs keep the fused narrow / halo kernels
+bool conv_gemm_ok(const ConvGeom& g, bool trans) {
+  gemm_env();
+  if (!g_gemm_mode || trans) return false;
+  return gemm_geom_ok(g, g.stride > 1 ? 32 : 64);
+}
+
+// the tile of a launch: the planner's (or the forced) tile, moved to the 32-wide-stage tile when the input
+// groups are narrower than its 64-wide stages
+static int gemm_tile_for(const ConvGeom& g) {
+  const int cfg = gemm_pick_cfg(g.Go * g.Cgo, cdiv(g.Kp, 64));
+  return (g.Cgi < 64 && kCfgs[cfg].bk == 64) ? kOccCfg : cfg;
 }
 
 void conv_gemm_set(int on) { gemm_env(); g_gemm_mode = on ? 1 : 0; }
@@ -559,7 +611,38 @@ int conv_gemm(const ConvArgs& a, hipStream_t s) {
   gemm_env();
   for (int i = 0; i < a.g.Gi; ++i)
     if (a.xc[i] != nullptr) return 2;   // no prologue on this path (see conv_gemm_ok)
-  const int cfg = gemm_pick_cfg(a.g.Go * a.g.Cgo, cdiv(a.g.Kp, 64));
-  return a.bn_y != nullptr ? dispatch_gemm<true>(a, cfg, s) : dispatch_gemm<false>(a, cfg, s);
+  const int cfg = gemm_tile_for(a.g);
+  const GemmPhase ph;
+  return a.bn_y != nullptr ? dispatch_gemm<true>(a, cfg, ph, s) : dispatch_gemm<false>(a, cfg, ph, s);
+}
+
+// One phase (py, px) of a stride-s transposed conv (the strided data-gradient) as a stride-1 GEMM conv over
+// the phase's output sub-grid: `a` carries the phase geometry (OH/OW = the sub-grid, taps = the phase's
+// valid taps divided by s, stride 1) and the FULL packed weights; tA[v] = the packed tap of phase tap v.
+// Returns 0, or 1 when the phase is not a GEMM launch (the caller runs the gather kernel): narrow input,
+// irregular taps, a packed-tap subset that is not a strided grid, or no taps.
+int conv_gemm_phase(const ConvArgs& a0, const int* tA, int KW, int s_, int py, int px, int OHf, int OWf,
+                    hipStream_t s) {
+  gemm_env();
+  ConvArgs a = a0;
+  ConvGeom& g = a.g;
+  const long apitch = g.Kp;                            // the full packed rows
+  g.Kp = (g.T * g.Gi * g.Cgi + 31) / 32 * 32;          // K of this phase's taps
+  if (g.T < 1 || !g_gemm_mode || !gemm_geom_ok(g, 32) || a.bn_y != nullptr || a.stat_part != nullptr) return 1;
+  for (int i = 0; i < g.Gi; ++i)
+    if (a.xc[i] != nullptr || a.gy[i] != nullptr) return 1;
+  TapGrid tg;
+  if (!tap_grid(g, tg)) return 1;
+  GemmPhase ph;
+  ph.ps = s_; ph.py = py; ph.px = px; ph.OHf = OHf; ph.OWf = OWf; ph.apitch = apitch;
+  const int kh = g.T / tg.kw;
+  ph.akw = KW;
+  ph.ar0 = tA[0] / KW; ph.ac0 = tA[0] % KW;
+  ph.ars = kh > 1 ? tA[tg.kw] / KW - ph.ar0 : 0;
+  ph.acs = tg.kw > 1 ? tA[1] % KW - ph.ac0 : 0;
+  for (int v = 0; v < g.T; ++v)   // the packed taps must form that strided grid
+    if (tA[v] != (ph.ar0 + (v / tg.kw) * ph.ars) * KW + ph.ac0 + (v % tg.kw) * ph.acs) return 1;
+  const int cfg = gemm_tile_for(g);
+  return dispatch_gemm<false>(a, cfg, ph, s) == 0 ? 0 : 2;
 }
 

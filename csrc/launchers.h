@@ -100,6 +100,9 @@ const char* conv_error_string(int rc);
 bool conv_gemm_ok(const ConvGeom& g, bool trans);
 long conv_gemm_stat_blocks(const ConvGeom& g);
 int conv_gemm(const ConvArgs& a, hipStream_t s);
+// one phase of a phase-decomposed strided data-gradient on the GEMM kernel (0), or 1: not eligible (gather)
+int conv_gemm_phase(const ConvArgs& a, const int* tA, int KW, int s_, int py, int px, int OHf, int OWf,
+                    hipStream_t s);
 void conv_gemm_set(int on);
 void conv_gemm_force_cfg(int cfg);   // tests / A-B: one tile configuration for every launch (-1: planner)
 int conv_gemm_num_cfgs();

@@ -99,6 +99,17 @@ class ConvPlan:
                                                        [t[1] for t in taps], self.transposed and self.stride > 1))
         return cache[key]
 
+    def uses_gemm(self, n, ih, iw):
+        """Whether the forward of this plan runs the LDS-DMA GEMM kernel (no deferred-BN input prologue there)."""
+        cache = self.__dict__.setdefault('_gemm_cache', {})
+        key = (n, ih, iw)
+        if key not in cache:
+            oh, ow = self.out_hw(ih, iw)
+            taps = self.taps_bwd if self.transposed else self.taps_fwd
+            cache[key] = bool(require().conv_uses_gemm(self.fwd_dims(n, ih, iw, oh, ow), [t[0] for t in taps],
+                                                       [t[1] for t in taps], self.transposed and self.stride > 1))
+        return cache[key]
+
     def stat_blocks(self, n, ih, iw):
         oh, ow = self.out_hw(ih, iw)
         taps = self.taps_bwd if self.transposed else self.taps_fwd
@@ -617,7 +628,7 @@ def conv(plan: ConvPlan, xs, want_stats=False, bn_handle=None):
         # (shared by all consumers through Deferred.z) is cheaper -- measured: L3-L5 fused-8 forward
         # +0.6 ms each with the per-k-step prologue vs ~0.05 ms for the pass.
         n, ih, iw, _ = xs[0].shape
-        if not plan.uses_halo(n, ih, iw) and plan.Cgi >= 64:
+        if plan.uses_gemm(n, ih, iw) or (not plan.uses_halo(n, ih, iw) and plan.Cgi >= 64):
             xs = [materialize(x) for x in xs]
     xs = [x.z if isinstance(x, Deferred) and x.z is not None else x for x in xs]
     ts, coefs, mask = split_inputs(xs)
