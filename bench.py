@@ -286,6 +286,8 @@ def main(argv=None):
     # batch the step is GPU-bound (profiles/r06/ddp_graph: graph vs no graph within noise), so it runs
     # uncaptured and the per-bucket RCCL evidence pass below can run
     graph_ddp = args.graph_ddp == 'on' or (args.graph_ddp == 'auto' and args.batch <= 64)
+    if ddp and dist.get_backend() != 'nccl':   # gloo collectives run on the host: never captured
+        graph_ddp = False
     use_graph = cuda and not args.no_graph and (not ddp or graph_ddp)
     total_steps = args.warmup + args.steps + 2 * args.comm_steps + 2
     save_dir = None

@@ -115,7 +115,10 @@ class SegTrainer(BaseTrainer):
         kd_ok = not config.kd_training or isinstance(self.teacher_model, FusedModel)
         collectives = getattr(self.optimizer, 'bucketer', None) is not None or \
             (config.DDP and config.gpu_num > 1)
-        coll_ok = not collectives or getattr(config, 'graph_collectives', True)
+        # (RCCL only: gloo collectives run on the host and cannot be captured -- the same-GPU gloo rehearsal)
+        nccl = torch.distributed.is_available() and torch.distributed.is_initialized() and \
+            torch.distributed.get_backend() == 'nccl'
+        coll_ok = not collectives or (getattr(config, 'graph_collectives', True) and nccl)
         return self.fused and config.use_graph and kd_ok and not config.use_aux and coll_ok
 
     def step_engine(self, config):

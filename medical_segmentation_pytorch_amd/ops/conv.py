@@ -219,7 +219,9 @@ def _taps(tl):
 FUSED_BWD = os.environ.get('MSP_FUSED_BWD', '1') != '0'
 # A deferred BN data-gradient is NOT rebuilt by the separate halo data- and weight-gradient kernels (each
 # re-reads y; measured net-neutral in round 4 and -1.6 % in round 5: profiles/r04/kernels_deferdy_*,
-# profiles/r05/defer_dy_separate_ab_bs320.txt): outside the fused backward it is resolved (the apply pass)
+# profiles/r05/defer_dy_separate_ab_bs320.txt): outside the fused backward it is resolved (the apply pass).
+# A module constant (no env knob): tests/test_gpu_deferred_dy.py sets it to keep that kernel path covered.
+DEFER_SEPARATE = False
 
 
 def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
@@ -290,8 +292,8 @@ def _bwd_operands(grads, plan, dims_d, taps_d, dims_w, taps_w, dgrad=True):
     # Without a data-gradient launch (the first conv: its input is the image) the weight-gradient is dY's
     # only reader: rebuilding dY there reads (dz, y) once instead of the apply pass's read dz, y + write dy
     # + the weight-gradient's read dy -- 2 passes instead of 4, a win even where the halo kernels' re-read
-    # of y made deferral neutral (see above).
-    ok = not dgrad and not plan.transposed and plan.stride == 1 and plan.bias is None
+    # of y made deferral neutral (DEFER_SEPARATE).
+    ok = (DEFER_SEPARATE or not dgrad) and not plan.transposed and plan.stride == 1 and plan.bias is None
     if ok and dgrad:
         ok = bool(C.conv_uses_halo(dims_d, taps_d[0], taps_d[1], False, True))
     if ok:
