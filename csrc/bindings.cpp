@@ -803,6 +803,16 @@ void relu6_t(const at::Tensor& x, const at::Tensor& y) {
   relu6(bf(x), bf(y), x.numel(), cur_stream());
 }
 
+void bn_aug_mask_t(const at::Tensor& x, const at::Tensor& stats, const at::Tensor& out, int64_t C) {
+  CHECK_BF16(x); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.size(-1) == 8 && out.numel() == x.numel(),
+              "bn_aug_mask: contiguous 8-channel pixels, out like x");
+  TORCH_CHECK(C >= 1 && C <= 4, "bn_aug_mask: 1 <= C <= 4 (2C channels of 8)");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() >= 16 && stats.size(-1) == 8,
+              "bn_aug_mask: stats fp32 [>=2][8]");
+  bn_aug_mask(bf(x), f32(stats), bf(out), x.numel() / 8, (int)C, cur_stream());
+}
+
 void relu6_bwd_t(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx) {
   CHECK_BF16(dy); CHECK_BF16(y); CHECK_BF16(dx);
   TORCH_CHECK(dy.numel() == y.numel() && dx.numel() == y.numel() && y.numel() % 8 == 0, "relu6_bwd: shapes");
@@ -1122,6 +1132,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gconv_fwd", &gconv_fwd_t);
   m.def("relu6", &relu6_t);
   m.def("relu6_bwd", &relu6_bwd_t);
+  m.def("bn_aug_mask", &bn_aug_mask_t);
   m.def("gconv_dgrad", &gconv_dgrad_t);
   m.def("gconv_wgrad_slices", &gconv_wgrad_slices_t);
   m.def("gconv_wgrad", &gconv_wgrad_t);

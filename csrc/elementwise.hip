@@ -116,6 +116,29 @@ __global__ __launch_bounds__(kBlock) void relu6_kernel(const uint16_t* __restric
   }
 }
 
+// The first DUCK block's in_bn over the (8-channel padded) image, augmented for its gamma / beta gradients
+// (ops.bn.aug_in_bn): out[p] = [relu(s*x + h) for c < C, (s*x + h > 0) for the next C channels, 0 ...].
+// The first convs read it in place of the deferred z (their weights for channels >= C are zero), and their
+// weight-gradient slabs then also hold the correlations of dY with the ReLU mask.
+__global__ __launch_bounds__(kBlock) void bn_aug_mask_kernel(const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                             uint16_t* __restrict__ out, long npix, int C) {
+  for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < npix; i += (long)gridDim.x * kBlock) {
+    float v[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + i * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e < C) {
+        const float a = fmaf(v[e], st[e], st[8 + e]);
+        o[e] = fmaxf(a, 0.f);
+        o[e + C] = a > 0.f ? 1.f : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(out + i * 8) = pack8(o);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void relu6_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                            uint16_t* __restrict__ dx, long nvec) {
   for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long)gridDim.x * kBlock) {
@@ -172,6 +195,10 @@ void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hi
 
 void relu6(const uint16_t* x, uint16_t* y, long n_elem, hipStream_t s) {
   hipLaunchKernelGGL(relu6_kernel, dim3(grid_for(n_elem / 8)), dim3(kBlock), 0, s, x, y, n_elem / 8);
+}
+
+void bn_aug_mask(const uint16_t* x, const float* stats, uint16_t* out, long npix, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_aug_mask_kernel, dim3(grid_for(npix)), dim3(kBlock), 0, s, x, stats, out, npix, C);
 }
 
 void relu6_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n_elem, hipStream_t s) {

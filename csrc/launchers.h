@@ -180,6 +180,8 @@ void up2_add(const uint16_t* low, const uint16_t* skip, uint16_t* out, int N, in
 void pool2_sum(const uint16_t* g, uint16_t* out, int N, int h, int w, int Cp, hipStream_t s);
 // coefs (nullable): deferred-BN prologue per input (ld = Cp, the channel width of every input)
 void relu6(const uint16_t* x, uint16_t* y, long n_elem, hipStream_t s);   // min(max(x, 0), 6)
+// 8-channel pixels: out = [relu(s*x + h) (C ch), (s*x + h > 0) (C ch), 0 ...], C <= 4; stats [4][8] rows scale, shift
+void bn_aug_mask(const uint16_t* x, const float* stats, uint16_t* out, long npix, int C, hipStream_t s);
 void relu6_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n_elem, hipStream_t s);
 void add_n(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,
            long n_elem, int Cp, hipStream_t s);

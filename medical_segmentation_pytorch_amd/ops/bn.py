@@ -72,6 +72,18 @@ class Deferred:
         return self.t.device
 
 
+def aug_in_bn(d: 'Deferred', C: int):
+    """The first DUCK block's in_bn over the image, augmented: a plain 8-channel tensor
+    ``[relu(bn(x)) (C channels), relu mask (C channels), 0 ...]`` built from the Deferred's scale / shift in one
+    pass (``bn_aug_mask``).  It is NOT connected to autograd: the convs that read it (their weights for
+    channels >= C are zero, so their outputs are exactly those on z) skip their data-gradient, and in_bn's
+    gamma / beta gradients come from their weight-gradient slabs instead (``ops.conv.InBnAug``)."""
+    need_stats([d])
+    out = torch.empty_like(d.t)
+    require().bn_aug_mask(d.t.detach().contiguous(), d.stats, out, C)
+    return out
+
+
 def split_inputs(xs):
     """(tensors, prologue coefficient list or [], relu bitmask) of a list of Tensor | Deferred."""
     ts, cs, mask = [], [], 0

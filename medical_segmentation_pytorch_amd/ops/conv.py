@@ -464,8 +464,43 @@ class _ConvFn(torch.autograd.Function):
         return tuple(out)
 
 
-def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None):
-    """``bk``: the BN-backward prologue kwargs of the dY groups (see :func:`_bwd_operands`)."""
+class InBnAug:
+    """The first DUCK block's in_bn gradient shortcut (see :func:`ops.bn.aug_in_bn`).  The block's first convs
+    read ``[z, m, 0..]`` (z = relu(bn(x)), m its ReLU mask, C channels each) and need no data-gradient: the image
+    needs none, and in_bn's parameters get theirs from the weight-gradient slabs.  With G_z / G_m the slab
+    channels of z / m (correlations of dY with z / m) and W the bf16 weights the forward used,
+        dbeta = sum W * G_m = sum_pixels dz * m,
+        sum W * G_z = sum_pixels dz * z = gamma * dgamma + beta * dbeta,
+    so dgamma = (sum W * G_z - beta * dbeta) / gamma.  Exact up to fp32 summation order: the usual path's dz
+    is rounded to bf16 before its BN backward sums, this one sums fp32 correlations."""
+
+    def __init__(self, st, C):
+        self.st, self.C = st, C
+        self.s_z = self.s_m = None
+
+    def add(self, w, g):
+        """w: a branch's weights [co, C, T_b] (fp32 view); g: its slab channels [co, 2C, T_b] fp32."""
+        wb = w.detach().to(torch.bfloat16).float()
+        sz = (wb * g[:, :self.C]).sum(dim=(0, 2))
+        sm = (wb * g[:, self.C:2 * self.C]).sum(dim=(0, 2))
+        self.s_z = sz if self.s_z is None else self.s_z + sz
+        self.s_m = sm if self.s_m is None else self.s_m + sm
+
+    def finish(self):
+        st = self.st
+        gam, bet = st.weight.detach().float(), st.bias.detach().float()
+        dbeta = self.s_m
+        dgamma = torch.where(gam.abs() > 1e-12, (self.s_z - bet * dbeta) / gam, torch.zeros_like(gam))
+        st.weight_sink.add_(dgamma)
+        st.bias_sink.add_(dbeta)
+        self.s_z = self.s_m = None
+        if st.ready_hook is not None:
+            st.ready_hook([st.weight, st.bias])
+
+
+def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None, aug=None):
+    """``bk``: the BN-backward prologue kwargs of the dY groups (see :func:`_bwd_operands`); ``aug``: an
+    :class:`InBnAug` collecting the z / mask channels of the slabs."""
     C = require()
     bk = bk or {}
     coefs, rmask = pro
@@ -495,6 +530,13 @@ def _conv_wgrad(plan: ConvPlan, gys, xs, shape, dev, pro=([], 0), bk=None):
     nrep = C.conv_wgrad_replicas(dims, dy, dx, False, bool(bk), bool(coefs))   # split-K dW slabs, summed in fixed order
     dwp = torch.empty(nrep * plan.rows * KT, dtype=torch.float32, device=dev)
     C.conv_wgrad(gys, xs, dwp, dims, dy, dx, False, coefs, rmask, **bk)
+    if aug is not None:   # channels [0, 2C) of every branch's slab rows (z, then the ReLU mask)
+        c2 = 2 * aug.C
+        for b in plan.branches:
+            g = torch.empty(plan.co_l, c2, b.T, dtype=torch.float32, device=dev)
+            C.unpack_wgrad(dwp[b.out_group * plan.Cgo * KT:], g.view(-1), plan.co_l, c2, b.T, plan.Cip, KT,
+                           b.t_base, 0, c2 * b.T, b.T, False, nrep, plan.rows * KT)
+            aug.add(b.weight.view(plan.co_l, aug.C, b.T), g)
     return _unpack_slabs(plan, dwp, nrep, need)
 
 
@@ -527,9 +569,10 @@ class _MultiConvFn(torch.autograd.Function):
     then runs each plan's weight gradient.  Stride-1, single input group, no bias."""
 
     @staticmethod
-    def forward(ctx, plans, want_stats, pro, x, *weights):
+    def forward(ctx, plans, want_stats, pro, aug, x, *weights):
         C = require()
         ctx.set_materialize_grads(False)
+        ctx.aug = aug
         x = x.contiguous()
         coefs, rmask = pro
         n, ih, iw, _ = x.shape
@@ -568,10 +611,10 @@ class _MultiConvFn(torch.autograd.Function):
             dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, plan.Kp_d, plan.stride]
             dy, dx = _taps(plan.taps_bwd)
             gys, bwd = _bwd_operands(gys, plan, dims_d, (dy, dx), plan.fwd_dims(n, ih, iw, oh, ow),
-                                     _taps(plan.taps_fwd), dgrad=ctx.needs_input_grad[3])
+                                     _taps(plan.taps_fwd), dgrad=ctx.needs_input_grad[4])
             bk = {} if bwd is None else dict(gy=bwd[0], gs=bwd[1], gk=bwd[2], grelu=bwd[3])
             per_plan.append((gys, bk, bwd))
-            if ctx.needs_input_grad[3]:
+            if ctx.needs_input_grad[4]:
                 wd, Kp_d = plan.pack_dgrad(dev)
                 first = dxt is None
                 if first:
@@ -580,20 +623,23 @@ class _MultiConvFn(torch.autograd.Function):
         wgrads = []
         for plan, (gys, bk, bwd) in zip(ctx.plans, per_plan):
             oh, ow = plan.out_hw(ih, iw)
-            wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro, bk)
+            wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro, bk, aug=ctx.aug)
             if bwd is not None:
                 from .bn import claim_deferred
                 for d in bwd[4]:
                     claim_deferred(d)
             if plan.ready_hook is not None:
                 plan.ready_hook([b.weight for b in plan.branches])
-        ctx.plans = None
-        return (None, None, None, dxt) + tuple(wgrads)
+        if ctx.aug is not None:
+            ctx.aug.finish()
+        ctx.plans = ctx.aug = None
+        return (None, None, None, None, dxt) + tuple(wgrads)
 
 
-def conv_multi(plans, x, want_stats=False):
+def conv_multi(plans, x, want_stats=False, aug=None):
     """Several stride-1 single-group plans on the same input ``x`` (tensor or Deferred) as one node;
-    returns [(outputs, stat partials)] per plan."""
+    returns [(outputs, stat partials)] per plan.  ``aug``: ``x`` is :func:`ops.bn.aug_in_bn`'s tensor and
+    ``aug`` the :class:`InBnAug` that turns the weight-gradient slabs into in_bn's gradients."""
     from .bn import Deferred, materialize, split_inputs
     for p in plans:
         assert p.stride == 1 and p.Gi == 1 and not p.transposed and p.bias is None
@@ -604,7 +650,7 @@ def conv_multi(plans, x, want_stats=False):
     x = x.z if isinstance(x, Deferred) and x.z is not None else x
     (t,), coefs, mask = split_inputs([x])
     weights = [b.weight for p in plans for b in p.branches]
-    out = _MultiConvFn.apply(plans, want_stats, (coefs, mask), t, *weights)
+    out = _MultiConvFn.apply(plans, want_stats, (coefs, mask), aug, t, *weights)
     res, o = [], 0
     ngo = sum(p.Go for p in plans)
     for i, p in enumerate(plans):

@@ -24,8 +24,8 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, bn_act, duck_tail, flush_pending, materialize
-from ..ops.conv import Branch, ConvPlan, PackProgram, conv, conv_multi
+from ..ops.bn import BNSpec, BNState, BwdStatsHandle, Deferred, aug_in_bn, bn_act, duck_tail, flush_pending, materialize
+from ..ops.conv import Branch, ConvPlan, InBnAug, PackProgram, conv, conv_multi
 from ..ops.elementwise import add_n, from_fm, relu6, to_fm, up2_add
 from ..ops.gconv import gconv
 from ..ops.pool import maxpool, res_tail, up2_cat
@@ -40,6 +40,10 @@ _DEFER_BN = os.environ.get('MSP_DEFER_BN', '1') != '0'
 _DUCK_TAIL = os.environ.get('MSP_DUCK_TAIL', '1') != '0'
 # env MSP_DUCK_MULTI=0 launches the separated branch's 1x7 on its own (its dgrad then adds through autograd)
 _MULTI = os.environ.get('MSP_DUCK_MULTI', '1') != '0'
+# The first DUCK block (in_bn over the image): its convs read [z, relu mask] and skip their data-gradient;
+# in_bn's gamma / beta gradients come from the weight-gradient slabs (ops.conv.InBnAug).  A module constant
+# the GPU test toggles to compare against the data-gradient path.
+_AUG_INBN = True
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 # env MSP_FUSED_DECODERS=0 keeps every non-Unet smp decoder on the hybrid (eager decoder) path (A/B)
@@ -339,8 +343,18 @@ class FusedExecutor(SmpDecoders):
         # into dL/dxb as well -- no autograd add pass for xb's gradient at all)
         sep_plan = self.plan_conv(b6[0][0])
         multi = _MULTI and sep_plan.stride == 1 and sep_plan.bias is None
+        aug = None
+        if multi and training and _AUG_INBN and len(xs) == 1 and isinstance(xs[0], torch.Tensor) and \
+                not xs[0].requires_grad and isinstance(xb, Deferred) and xb.relu:
+            # in_bn over an input that needs no gradient (the image): the InBnAug shortcut
+            st = self.bn(m.in_bn[0])
+            nf = m.in_bn[0].num_features
+            if (xb.t.shape[-1] == 8 and 2 * nf <= 8 and st.weight_sink is not None and st.bias_sink is not None
+                    and all(c.in_channels == nf for c in allc + [b6[0][0]])):
+                aug = InBnAug(st, nf)
+                xb = aug_in_bn(xb, nf)
         if multi:
-            outs = conv_multi(plans + [sep_plan], xb, want_stats=training)
+            outs = conv_multi(plans + [sep_plan], xb, want_stats=training, aug=aug)
             sep_y, sep_part = outs[-1][0][0], outs[-1][1]
             outs = outs[:-1]
         else:

@@ -267,3 +267,35 @@ def test_decoders_fully_fused(arch):
     from medical_segmentation_pytorch_amd.runtime.fused_model import eager_parts
     m = _smp(arch, 'resnet18')
     assert fused_decoder_kind(m) is not None and eager_parts(m) == []
+
+
+def test_first_duck_in_bn_shortcut(gpu, monkeypatch):
+    """The first DUCK block's in_bn over the image (ops.conv.InBnAug): its convs read [z, relu mask] and skip
+    the data-gradient launch; in_bn's gamma / beta gradients come from the weight-gradient slabs.  Every
+    other gradient is bitwise the data-gradient path's; in_bn's agree to fp32 summation order (the usual
+    path sums a bf16-rounded dz)."""
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    from medical_segmentation_pytorch_amd.runtime.bench_step import synthetic_batch
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep
+    torch.manual_seed(0)
+    base = DuckNet(2, 3, 17).to(gpu).train()
+    x, t = synthetic_batch(2, 96, gpu)
+    first = base.down_stages()[0].duck.in_bn[0]
+    names = {n for n, p in base.named_parameters() if p is first.weight or p is first.bias}
+    assert len(names) == 2
+    res, calls = {}, []
+    real = fused_model.aug_in_bn
+    monkeypatch.setattr(fused_model, 'aug_in_bn', lambda *a: calls.append(1) or real(*a))
+    for on in (False, True):
+        monkeypatch.setattr(fused_model, '_AUG_INBN', on)
+        s = FusedStep(copy.deepcopy(base), x.clone(), t.clone(), lr=1e-3, use_graph=False, total_steps=10)
+        s()
+        torch.cuda.synchronize()
+        res[on] = {n: p.grad.detach().float().clone() for n, p in s.model.named_parameters()}
+        assert len(calls) == int(on)
+    for n, a in res[False].items():
+        b = res[True][n]
+        if n in names:
+            assert ((a - b).norm() / a.norm().clamp_min(1e-12)).item() < 2e-2, (n, a, b)
+        else:
+            assert torch.equal(a, b), n
