@@ -428,9 +428,10 @@ class _ConvFn(torch.autograd.Function):
             wd, Kp_d = plan.pack_dgrad(dev)
             dxs = [torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev) for _ in range(plan.Gi)]
             h = ctx.bn_handle
-            if in_place and not trans and plan.Gi == 1 and (h is None or h.y is None):
-                # dL/dx = this dgrad + the parked identity-branch gradient, summed in the epilogue
-                C.conv_fwd(gys, wd, [parked], None, None, dims_d, dy, dx, False, accumulate=True, **bk)
+            if in_place and plan.Gi == 1 and (h is None or h.y is None):
+                # dL/dx = this dgrad + the parked gradient of x's other reader, summed in the epilogue (a
+                # strided data-gradient too: every phase launch adds into its own output pixels)
+                C.conv_fwd(gys, wd, [parked], None, None, dims_d, dy, dx, trans, accumulate=True, **bk)
                 dxs, parked = [parked], None
             elif h is not None and h.y is not None and not trans:
                 # dL/dx is the BN output's gradient: emit the BN backward partials in the epilogue

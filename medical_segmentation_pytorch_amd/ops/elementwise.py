@@ -58,7 +58,7 @@ class _Up2Add(torch.autograd.Function):
     """nearest-2x(low) + skip  (reference models/ducknet.py:82-84); pro = deferred-BN prologues."""
 
     @staticmethod
-    def forward(ctx, pro, low, skip):
+    def forward(ctx, pro, park, low, skip):
         C = require()
         low, skip = low.contiguous(), skip.contiguous()
         n, h, w, cp = low.shape
@@ -66,6 +66,7 @@ class _Up2Add(torch.autograd.Function):
         out = torch.empty_like(skip)
         C.up2_add(low, skip, out, n, h, w, cp, pro[0], pro[1])
         ctx.shape = (n, h, w, cp)
+        ctx.skip_ref = skip if park else None
         return out
 
     @staticmethod
@@ -77,7 +78,14 @@ class _Up2Add(torch.autograd.Function):
         g = g.contiguous()
         dlow = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=g.device)
         C.pool2_sum(g, dlow, n, h, w, cp)
-        return None, dlow, g
+        if ctx.skip_ref is not None and ctx.needs_input_grad[3]:
+            # the skip's other reader (the encoder's downsample conv) adds its data-gradient to g in its
+            # epilogue (ops.conv.park_input_grad) -- no autograd bf16 add of the two contributions
+            from .conv import park_input_grad
+            park_input_grad(ctx.skip_ref, g)
+            ctx.skip_ref = None
+            return None, None, dlow, None
+        return None, None, dlow, g
 
 
 class _AddN(torch.autograd.Function):
@@ -103,11 +111,16 @@ def from_fm(fm, c):
     return _FromFM.apply(fm, c)
 
 
-def up2_add(low, skip):
-    """``low``/``skip``: tensors or ``ops.bn.Deferred`` (normalise+ReLU applied while loading)."""
-    from .bn import split_inputs
+def up2_add(low, skip, park_skip=False):
+    """``low``/``skip``: tensors or ``ops.bn.Deferred`` (normalise+ReLU applied while loading).
+    ``park_skip``: the caller guarantees that exactly one other reader of ``skip`` exists, one of our
+    convs, whose backward runs after this op's: dL/dskip is parked for it instead of returned."""
+    from .bn import Deferred, split_inputs
+    # a skip already materialised (its other reader took the normalise pass) is read as that tensor: one
+    # read either way, and a parked gradient is keyed by the tensor the other reader saw
+    skip = skip.z if isinstance(skip, Deferred) and skip.z is not None else skip
     (lt, st), coefs, mask = split_inputs([low, skip])
-    return _Up2Add.apply((coefs, mask), lt, st)
+    return _Up2Add.apply((coefs, mask), bool(park_skip), lt, st)
 
 
 def add_n(*xs):

@@ -44,6 +44,8 @@ _MULTI = os.environ.get('MSP_DUCK_MULTI', '1') != '0'
 # in_bn's gamma / beta gradients come from the weight-gradient slabs (ops.conv.InBnAug).  A module constant
 # the GPU test toggles to compare against the data-gradient path.
 _AUG_INBN = True
+# DUCKNet skips: the decoder's share of dL/dskip is parked for the downsample conv (ops.elementwise.up2_add)
+_PARK_SKIP = True
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 # env MSP_FUSED_DECODERS=0 keeps every non-Unet smp decoder on the hybrid (eager decoder) path (A/B)
@@ -439,7 +441,9 @@ class FusedExecutor(SmpDecoders):
         for k, blk in enumerate(mids):
             x = self.residual(blk, x, training, single_out=k + 1 < len(mids))
         for st, skip in zip(model.up_stages(), reversed(skips)):
-            x = up2_add(x, skip)
+            # the skip's other reader is the encoder's downsample conv, whose backward runs after every
+            # decoder node (it needs the mid blocks' gradient): it adds dL/dskip in its epilogue
+            x = up2_add(x, skip, park_skip=training and _PARK_SKIP)
             x = self.duck(st.duck, [x], training)
         return self.head(model.seg_head, x, model.num_class)
 

@@ -299,3 +299,29 @@ def test_first_duck_in_bn_shortcut(gpu, monkeypatch):
             assert ((a - b).norm() / a.norm().clamp_min(1e-12)).item() < 2e-2, (n, a, b)
         else:
             assert torch.equal(a, b), n
+
+
+def test_ducknet_skip_grad_parked(gpu, monkeypatch):
+    """DUCKNet skips (ops.elementwise.up2_add(park_skip=True)): the decoder's share of dL/dskip is added by
+    the encoder's downsample conv in its data-gradient epilogue (strided phases included) instead of an
+    autograd bf16 add.  Same forward; gradients within bf16 rounding of the add path (one rounding fewer)."""
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    from medical_segmentation_pytorch_amd.runtime.bench_step import synthetic_batch
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep
+    torch.manual_seed(0)
+    base = DuckNet(2, 3, 17).to(gpu).train()
+    x, t = synthetic_batch(2, 96, gpu)
+    res, losses = {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(fused_model, '_PARK_SKIP', on)
+        s = FusedStep(copy.deepcopy(base), x.clone(), t.clone(), lr=1e-3, use_graph=False, total_steps=10)
+        losses[on] = float(s().detach())
+        torch.cuda.synchronize()
+        res[on] = {n: p.grad.detach().float().clone() for n, p in s.model.named_parameters()}
+    assert losses[True] == losses[False]
+    # a lost or doubled skip gradient moves every encoder parameter's gradient by O(1); one rounding fewer
+    # per skip moves them by bf16 noise, largest where the backward ends (the first DUCK's in_bn)
+    rel = {n: ((a - res[True][n]).norm() / a.norm().clamp_min(1e-12)).item() for n, a in res[False].items()}
+    worst = sorted(rel.items(), key=lambda kv: -kv[1])[:5]
+    assert worst[0][1] < 6e-2, worst
+    assert sorted(rel.values())[len(rel) // 2] < 5e-3, worst
