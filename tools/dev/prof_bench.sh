@@ -13,4 +13,5 @@ cd "$root"
 python3 tools/rocpd_summary.py "$db" --steps 5 --window --top 90 > "$root/gpurun_out/prof_$tag.txt" 2>&1
 python3 tools/rocpd_summary.py "$db" --steps 5 --window --group >> "$root/gpurun_out/prof_$tag.txt" 2>&1
 python3 tools/rocpd_timeline.py "$db" --steps 4 > "$root/gpurun_out/prof_${tag}_timeline.txt" 2>&1
+python3 tools/rocpd_summary.py "$db" --sequence > "$root/gpurun_out/prof_${tag}_sequence.txt" 2>&1 || true
 [ "${KEEP_DB:-0}" = 1 ] || rm -rf "$root/gpurun_out/prof_$tag"   # (raw DB: gpurun copies back at most 64 MiB)

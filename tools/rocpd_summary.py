@@ -5,6 +5,8 @@ Usage: python tools/rocpd_summary.py path/to/results.db [--top 40] [--steps N] [
 ``--group`` buckets kernels into families (conv fwd / dgrad / wgrad / BN / elementwise ...).
 ``--window``: only the last ``--steps`` steady-state steps, marker to marker (the once-per-step fused
 optimizer kernel, ``--marker``) -- excludes warmup / graph-capture work (e.g. the setup copies).
+``--sequence``: instead, every launch of the last step in issue order (index, ms, grid, name) -- which
+launch of a kernel family is which layer.
 """
 import argparse
 import collections
@@ -31,8 +33,22 @@ def main():
     ap.add_argument('--group', action='store_true')
     ap.add_argument('--window', action='store_true')
     ap.add_argument('--marker', default=r'adam_kernel|sgd_kernel|Adam')
+    ap.add_argument('--sequence', action='store_true')
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
+    if a.sequence:
+        try:
+            seq = db.execute('select name, start, end, grid_size_x, workgroup_size_x from kernels order by start').fetchall()
+        except sqlite3.OperationalError:
+            seq = [r + (0, 0) for r in db.execute('select name, start, end from kernels order by start').fetchall()]
+        marks = [i for i, r in enumerate(seq) if re.search(a.marker, r[0])]
+        if len(marks) < 2:
+            raise SystemExit('--sequence: marker found fewer than 2 times')
+        for i, (name, s0, e0, gx, wx) in enumerate(seq[marks[-2] + 1:marks[-1] + 1]):
+            nm = re.sub(r'\(anonymous namespace\)::', '', name)
+            nm = re.sub(r'\((ConvArgs|FusedBwdArgs|WgradPtrs|unsigned|float|long|const|\(anon).*$', '', nm)
+            print(f'{i:5d} {(e0 - s0) / 1e6:8.3f} {gx // max(wx, 1):7d}  {nm[:110]}')
+        return
     rows = db.execute('select name, start, end from kernels order by start').fetchall()
     if a.window:
         marks = [i for i, r in enumerate(rows) if re.search(a.marker, r[0])]
