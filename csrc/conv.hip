@@ -652,6 +652,9 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
         if constexpr (BWD) sz[u] = make_uint4(0, 0, 0, 0);
         if (y_ok[cb] && oy < g.OH && ox < g.OW) {
           const long po = yoff + (oy * g.OW + ox) * g.Cgo;
+#ifdef DW_KO_LOAD   // (profiling knock-out builds only: no staging loads)
+          if (po < 0)
+#endif
           sv[u] = *reinterpret_cast<const uint4*>(y_base[cb] + po);
           if constexpr (BWD) {
             if (z_base[cb] != nullptr) {
@@ -667,6 +670,9 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
           const int iy = y0 + hy + tl.ey0, ix = x0 + hx + tl.ex0;
           sd[u] = NCB * SUB + dw_elem(hy * tl.HWd + hx, vv >> 1, 2 * (vv & 1));
           if (x_ok && (unsigned)iy < (unsigned)g.IH && (unsigned)ix < (unsigned)g.IW) {
+#ifdef DW_KO_LOAD
+            if (iy < 0)
+#endif
             sv[u] = *reinterpret_cast<const uint4*>(xim + (iy * g.IW + ix) * g.Cgi);
             sx |= 1u << u;
           }
@@ -696,6 +702,15 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
     // per-pair / per-half branches split every read -> wait -> MFMA into its own basic block, so nothing
     // overlapped inside a wave (2 waves/SIMD: 53 % of wave cycles waiting, MFMA busy 0.19).
     auto frags = [&](int sl, uint4 (&fa)[NCB][2], uint4 (&fb)[NPW]) {
+#ifdef DW_KO_LDSREAD   // (profiling knock-out: fragments from registers, no transposed LDS reads)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[cb][i] = make_uint4(sl + cb, i, lane, (unsigned)tix);
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) fb[j] = make_uint4(sl, j, lane, (unsigned)tix);
+      return;
+#endif
       const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
@@ -718,8 +733,17 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-          for (int i = 0; i < 2; ++i) acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb[j], acc[cb][i][j]);
+          for (int i = 0; i < 2; ++i) {
+#ifdef DW_KO_MFMA   // (profiling knock-out: no MFMAs; the fragments stay live)
+            acc[cb][i][j][0] += __uint_as_float(fa[cb][i].x ^ fb[j].y);
+#else
+            acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb[j], acc[cb][i][j]);
+#endif
+          }
     };
+#ifdef DW_KO_SLICES   // (profiling knock-out: staging only -- no fragment reads, no MFMAs)
+    continue;
+#endif
     constexpr int NB = DWB(NPW, NCB) ? 2 : 1;
     uint4 fa[NB][NCB][2], fb[NB][NPW];
     if constexpr (NB == 2) {
@@ -1990,7 +2014,10 @@ int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, c
   if (W.halo) {
     const size_t lds = wgrad_halo_lds(W.tl, W.ncb);
     dim3 grid((unsigned)W.nsplit, W.gy, W.gz);
-    const int npw = cdiv(2 * g.T, kDwWaves);
+    // (tap, 16-channel half) pairs per wave: an input of <= 16 channels (the 8-channel image) has one half
+    // per tap -- sizing it for two left 15 of 24 pair slots idle (first DUCK: 8.9 ms per step)
+    const int nhv = std::min(2, cdiv(g.Gi * g.Cgi, 16));
+    const int npw = cdiv(nhv * g.T, kDwWaves);
     const int ncb = W.ncb;
     // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU) is opted into once per instantiation, before any
     // graph capture (the first call of every shape runs eagerly)
