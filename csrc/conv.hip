@@ -21,6 +21,7 @@
 // Channel GROUPS (launchers.h): the logical input/output channel dims may be split over up to 8
 // separate NHWC tensors; group pointers are staged in LDS and selected per lane per k-step.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "launchers.h"
@@ -533,7 +534,7 @@ DEVI int dw_elem(int pix, int half, int sub4) {   // element offset of (pixel, 1
 // BN-backward prologue -- the same bwd8 as bn_act_bwd_apply, so dY is bit-identical)
 template <int NPW, int NCB, bool BWD = false>
 __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_kernel(WgradPtrs P, float* __restrict__ dw, ConvGeom g,
-                                                              DwTile tl, int KT, long ntiles) {
+                                                              DwTile tl, int KT, long ntiles, int z0) {
   constexpr int NST = dw_stage(NCB);
   constexpr int LDT = DW_CH * NCB;                        // BWD table row length (the block's co rows)
   __shared__ float s_bt[BWD ? 5 * LDT : 1];
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, p4 = lr & 3;
-  const int co0 = blockIdx.y * DW_CH * NCB, ci0 = blockIdx.z * DW_CH;
+  const int co0 = blockIdx.y * DW_CH * NCB, ci0 = (blockIdx.z + z0) * DW_CH;   // z0: this launch's first ci chunk
   const int rows = g.Go * g.Cgo, Cip = g.Gi * g.Cgi;
   if (tid < kMaxTaps) s_tap[tid] = make_int2(g.dy[tid] - tl.ey0, g.dx[tid] - tl.ex0);
   if constexpr (BWD) {   // [5][LDT]: scale, shift (+inf: no ReLU test), k1, k2, k3 of the block's co rows
@@ -599,20 +600,37 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
   int offA[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) { offA[i][0] = dw_elem(plo, i, p4); offA[i][1] = dw_elem(phi, i, p4); }
-  // B (halo) read offsets per owned (tap, ci16) pair: slice sl adds rows_per_slice*sl*HWd*32.
-  // Only the 16-channel halves that hold real channels are paired (a 40-channel input's second chunk
-  // has one); pair slots past npairs read a valid address and are never stored.
-  const int nhv = min(2, (Cip - ci0 + 15) >> 4);
-  const int npairs = nhv * g.T;
+  // B (halo) read offsets per owned pair: slice sl adds rows_per_slice*sl*HWd*32.  A pair is a (tap, full
+  // 16-channel half) or -- for a half with 8 real channels (a 24-channel input's second half, an 8-channel
+  // input, a 40-channel input's second chunk) -- TWO taps of that half packed into one 16-wide fragment:
+  // source lanes p4 0-1 address tap 2pp, lanes 2-3 tap 2pp+1, so the transposed read puts tap 2pp's 8
+  // channels in columns 0-7 and tap 2pp+1's in 8-15 (dw_pairs, the host's slot count).  Pair slots past
+  // npairs read a valid address and are never stored.
+  const int R = min(DW_CH, Cip - ci0);
+  const int nfull = R >> 4, nfp = nfull * g.T;
+  const int npairs = nfp + ((R & 15) ? (g.T + 1) >> 1 : 0);
   int offB[NPW][2];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
     const int pr = wave + kDwWaves * j;
-    const int t = pr < npairs ? pr / nhv : 0, cf = pr < npairs ? pr - t * nhv : 0;
+    int t = 0, cf = 0, sub = p4;
+    if (pr < nfp) {
+      t = pr / nfull;
+      cf = pr - t * nfull;
+    } else if (pr < npairs) {
+      const int ta = 2 * (pr - nfp), tb = ta + (p4 >> 1);
+      t = tb < g.T ? tb : ta;
+      cf = nfull;
+      sub = p4 & 1;
+    }
     const int2 d = s_tap[t];
-    offB[j][0] = dw_elem((ry_lo + d.x) * tl.HWd + cx_lo + d.y, cf, p4);
-    offB[j][1] = dw_elem((ry_hi + d.x) * tl.HWd + cx_hi + d.y, cf, p4);
+    offB[j][0] = dw_elem((ry_lo + d.x) * tl.HWd + cx_lo + d.y, cf, sub);
+    offB[j][1] = dw_elem((ry_hi + d.x) * tl.HWd + cx_hi + d.y, cf, sub);
   }
+  // slots holding a pair (wave-uniform): the slice loop runs only those -- a 40-channel input's second
+  // chunk has 5 pairs for 24 slots
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int live = npairs > wv ? min(NPW, (npairs - wv + kDwWaves - 1) / kDwWaves) : 0;
 
   f32x4_t acc[NCB][2][NPW];
 #pragma unroll
@@ -701,66 +719,73 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
     // `rows`, whose staged dY is zero) accumulates into registers that are never stored.  Measured: the
     // per-pair / per-half branches split every read -> wait -> MFMA into its own basic block, so nothing
     // overlapped inside a wave (2 waves/SIMD: 53 % of wave cycles waiting, MFMA busy 0.19).
-    auto frags = [&](int sl, uint4 (&fa)[NCB][2], uint4 (&fb)[NPW]) {
+    // L: the wave's live pair slots (compile-time per call below)
+    auto slices = [&](auto LC) {
+      constexpr int L = decltype(LC)::value;
+      auto frags = [&](int sl, uint4 (&fa)[NCB][2], uint4 (&fb)[L]) {
 #ifdef DW_KO_LDSREAD   // (profiling knock-out: fragments from registers, no transposed LDS reads)
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb)
+        for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[cb][i] = make_uint4(sl + cb, i, lane, (unsigned)tix);
+          for (int i = 0; i < 2; ++i) fa[cb][i] = make_uint4(sl + cb, i, lane, (unsigned)tix);
 #pragma unroll
-      for (int j = 0; j < NPW; ++j) fb[j] = make_uint4(sl, j, lane, (unsigned)tix);
-      return;
+        for (int j = 0; j < L; ++j) fb[j] = make_uint4(sl, j, lane, (unsigned)tix);
+        return;
 #endif
-      const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const uint2 lo = tr_read(&sY[cb * SUB + sa + offA[i][0]]);
-          const uint2 hi = tr_read(&sY[cb * SUB + sa + offA[i][1]]);
-          fa[cb][i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        }
-#pragma unroll
-      for (int j = 0; j < NPW; ++j) {
-        const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
-        const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
-        fb[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      }
-    };
-    auto mma = [&](const uint4 (&fa)[NCB][2], const uint4 (&fb)[NPW]) {
-#pragma unroll
-      for (int j = 0; j < NPW; ++j)
+        const int sa = sl * 32 * DW_CH, sb = sl * rows_per_slice * tl.HWd * DW_CH;
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-#ifdef DW_KO_MFMA   // (profiling knock-out: no MFMAs; the fragments stay live)
-            acc[cb][i][j][0] += __uint_as_float(fa[cb][i].x ^ fb[j].y);
-#else
-            acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb[j], acc[cb][i][j]);
-#endif
+            const uint2 lo = tr_read(&sY[cb * SUB + sa + offA[i][0]]);
+            const uint2 hi = tr_read(&sY[cb * SUB + sa + offA[i][1]]);
+            fa[cb][i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
           }
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const uint2 lo = tr_read(&sX[sb + offB[j][0]]);
+          const uint2 hi = tr_read(&sX[sb + offB[j][1]]);
+          fb[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+      };
+      auto mma = [&](const uint4 (&fa)[NCB][2], const uint4 (&fb)[L]) {
+#pragma unroll
+        for (int j = 0; j < L; ++j)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+#ifdef DW_KO_MFMA   // (profiling knock-out: no MFMAs; the fragments stay live)
+              acc[cb][i][j][0] += __uint_as_float(fa[cb][i].x ^ fb[j].y);
+#else
+              acc[cb][i][j] = mfma16x16x32(fa[cb][i], fb[j], acc[cb][i][j]);
+#endif
+            }
+      };
+      constexpr int NB = DWB(L, NCB) ? 2 : 1;
+      uint4 fa[NB][NCB][2], fb[NB][L];
+      if constexpr (NB == 2) {
+        frags(0, fa[0], fb[0]);
+#pragma unroll
+        for (int sl = 0; sl < NSL; ++sl) {
+          if (sl + 1 < NSL) frags(sl + 1, fa[(sl + 1) & 1], fb[(sl + 1) & 1]);
+          mma(fa[sl & 1], fb[sl & 1]);
+        }
+      } else {   // register-bound variants: one set (the scheduler still hoists reads across slices)
+        constexpr int UNR = L * NCB >= 9 ? 1 : NSL;   // <3,3> spills when unrolled
+#pragma unroll UNR
+        for (int sl = 0; sl < NSL; ++sl) {
+          frags(sl, fa[0], fb[0]);
+          mma(fa[0], fb[0]);
+        }
+      }
     };
 #ifdef DW_KO_SLICES   // (profiling knock-out: staging only -- no fragment reads, no MFMAs)
     continue;
 #endif
-    constexpr int NB = DWB(NPW, NCB) ? 2 : 1;
-    uint4 fa[NB][NCB][2], fb[NB][NPW];
-    if constexpr (NB == 2) {
-      frags(0, fa[0], fb[0]);
-#pragma unroll
-      for (int sl = 0; sl < NSL; ++sl) {
-        if (sl + 1 < NSL) frags(sl + 1, fa[(sl + 1) & 1], fb[(sl + 1) & 1]);
-        mma(fa[sl & 1], fb[sl & 1]);
-      }
-    } else {   // register-bound variants: one set (the scheduler still hoists reads across slices)
-      constexpr int UNR = NPW * NCB >= 9 ? 1 : NSL;   // <3,3> spills when unrolled
-#pragma unroll UNR
-      for (int sl = 0; sl < NSL; ++sl) {
-        frags(sl, fa[0], fb[0]);
-        mma(fa[0], fb[0]);
-      }
-    }
+    // (one slice-loop variant: a second one -- fewer slots for waves with dead ones -- spills the <3,2> / <3,3>
+    // kernels; chunks with fewer pairs get their own launch instead, conv_wgrad)
+    if (live > 0) slices(std::integral_constant<int, NPW>{});
   }
   // deterministic split-K: block x writes its partial dW tile into slab x (plain stores, every needed
   // element exactly once per slab); unpack_wgrad sums the nsplit slabs in fixed order
@@ -769,8 +794,15 @@ __global__ __launch_bounds__(64 * kDwWaves, DW_MIN_WAVES) void conv_wgrad_halo_k
   for (int j = 0; j < NPW; ++j) {
     const int pr = wave + kDwWaves * j;
     if (pr >= npairs) continue;
-    const int t = pr / nhv, cf = pr - t * nhv;
-    const int ci = ci0 + 16 * cf + lr;
+    int t, ci;
+    if (pr < nfp) {
+      t = pr / nfull;
+      ci = ci0 + 16 * (pr - t * nfull) + lr;
+    } else {   // packed pair: columns 0-7 tap 2pp, 8-15 tap 2pp+1 (past the last tap: never stored)
+      t = 2 * (pr - nfp) + (lr >> 3);
+      if (t >= g.T) continue;
+      ci = ci0 + 16 * nfull + (lr & 7);
+    }
     if (ci >= Cip) continue;
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb)
@@ -2013,31 +2045,45 @@ int conv_wgrad(const uint16_t* const* dy, const uint16_t* const* x, float* dw, c
   const WgradPlan W = wgrad_plan(g, trans, bwd);
   if (W.halo) {
     const size_t lds = wgrad_halo_lds(W.tl, W.ncb);
-    dim3 grid((unsigned)W.nsplit, W.gy, W.gz);
-    // (tap, 16-channel half) pairs per wave: an input of <= 16 channels (the 8-channel image) has one half
-    // per tap -- sizing it for two left 15 of 24 pair slots idle (first DUCK: 8.9 ms per step)
-    const int nhv = std::min(2, cdiv(g.Gi * g.Cgi, 16));
-    const int npw = cdiv(nhv * g.T, kDwWaves);
+    // pair slots per wave of ci chunk z (the kernel's pair table): full 16-channel halves one tap each, a
+    // half with 8 real channels two taps (24-channel L1: 14 pairs, 2 slots instead of 3; the 8-channel image:
+    // 5 pairs, 1 slot).  Consecutive chunks with the same count share a launch: a 40-channel input's second
+    // chunk (5 pairs) runs 1 slot per wave instead of the first chunk's 3.
+    auto chunk_npw = [&](int z) {
+      const int R = std::min(DW_CH, g.Gi * g.Cgi - z * DW_CH);
+      return cdiv((R >> 4) * g.T + ((R & 15) ? (g.T + 1) / 2 : 0), kDwWaves);
+    };
     const int ncb = W.ncb;
     // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU) is opted into once per instantiation, before any
     // graph capture (the first call of every shape runs eagerly)
+    auto launch = [&](int npw, int z0, int nz) -> bool {
+      dim3 grid((unsigned)W.nsplit, W.gy, nz);
 #define HW_(N_, C_, B_)                                                                                  \
-    if (npw == N_ && ncb == C_ && bwd == B_) {                                                          \
-      static bool lds_attr = false;                                                                     \
-      if (!lds_attr) {                                                                                  \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_halo_kernel<N_, C_, B_>),   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwMaxLds);               \
-        lds_attr = true;                                                                                \
-      }                                                                                                 \
-      hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_, B_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, W.tl, \
-                         KT, W.ntiles);                                                                 \
-      return 0;                                                                                         \
-    }
-    HW_(1, 1, false) HW_(2, 1, false) HW_(3, 1, false) HW_(1, 2, false) HW_(2, 2, false) HW_(3, 2, false)
-    HW_(1, 3, false) HW_(2, 3, false) HW_(3, 3, false)
-    HW_(1, 1, true) HW_(2, 1, true) HW_(3, 1, true) HW_(1, 2, true) HW_(2, 2, true) HW_(3, 2, true)
+      if (npw == N_ && ncb == C_ && bwd == B_) {                                                        \
+        static bool lds_attr = false;                                                                   \
+        if (!lds_attr) {                                                                                \
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_halo_kernel<N_, C_, B_>), \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kDwMaxLds);             \
+          lds_attr = true;                                                                              \
+        }                                                                                               \
+        hipLaunchKernelGGL((conv_wgrad_halo_kernel<N_, C_, B_>), grid, dim3(64 * kDwWaves), lds, s, P, dw, g, \
+                           W.tl, KT, W.ntiles, z0);                                                     \
+        return true;                                                                                    \
+      }
+      HW_(1, 1, false) HW_(2, 1, false) HW_(3, 1, false) HW_(1, 2, false) HW_(2, 2, false) HW_(3, 2, false)
+      HW_(1, 3, false) HW_(2, 3, false) HW_(3, 3, false)
+      HW_(1, 1, true) HW_(2, 1, true) HW_(3, 1, true) HW_(1, 2, true) HW_(2, 2, true) HW_(3, 2, true)
 #undef HW_
-    return 6;
+      return false;
+    };
+    for (int z = 0; z < W.gz;) {
+      const int npw = chunk_npw(z);
+      int z1 = z + 1;
+      while (z1 < W.gz && chunk_npw(z1) == npw) ++z1;
+      if (!launch(npw, z, z1 - z)) return 6;
+      z = z1;
+    }
+    return 0;
   }
   dim3 grid(W.gx, W.gy, (unsigned)W.nsplit);
 #define WG(CO_, K_)                                                                                  \
