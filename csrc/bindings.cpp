@@ -1202,7 +1202,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("batched_gemm", &batched_gemm_t);
   m.def("softmax_all", &softmax_all_t);
   m.def("softmax_all_bwd", &softmax_all_bwd_t);
-  m.def("conv_set_fwd_fused", [](bool on) { conv_set_fwd_fused(on ? 1 : 0); });
+  m.def("conv_set_fwd_fused", [](int64_t mode) { conv_set_fwd_fused((int)mode); });   // 0 / 1 / 2 (see conv_bwd.hip)
   m.def("conv_fwd_fused_ok", [](std::vector<int64_t> dims, std::vector<int64_t> dy, std::vector<int64_t> dx) {
     return conv_fwd_fused_ok(make_geom(dims, dy, dx));
   });

@@ -1838,7 +1838,7 @@ int conv_igemm(const ConvArgs& a, bool trans, hipStream_t s) {
   if (bwd && (trans || conv_gemm_ok(a.g, trans))) return 7;
   if (conv_gemm_ok(a.g, trans)) return conv_gemm(a, s);
   // the 17-channel level's forward convs: persistent staging / compute-wave kernel (conv_bwd.hip)
-  if (!trans && !bwd && a.bn_y == nullptr && !a.accum && a.g.Gi == 1 && a.g.Go == 1 && conv_fwd_fused_ok(a.g))
+  if (!trans && !bwd && a.bn_y == nullptr && !a.accum && a.g.Gi == 1 && a.g.Go <= 2 && conv_fwd_fused_ok(a.g))
     return conv_fwd_fused(a, s);
   HaloGeom hg;
   if (halo_enabled() && conv_halo_ok(a.g, trans, hg, bwd)) {

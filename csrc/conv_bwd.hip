@@ -72,7 +72,8 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
 }
 
 // CB: 16-channel blocks of the data-gradient rows and of both weight-gradient operands: 2 (<= 32 channels, the
-// 17-channel level) or 3 (<= 48: the 34-channel level, Go = 1, CW = 4, 256-pixel tiles)
+// 17-channel level) or 3 (<= 48: the 34-channel level, Go = 1, CW = 4, 256-pixel tiles); forward mode also 5 (the
+// 34-channel level's 3x3 + 1x1 pair: 2 x 40 stacked output rows)
 template <int CW, int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false, bool FWD = false, int CB = 2>
 __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
   constexpr int kFbWaves = CW, kFbThreads = fb_threads(CW), kFbTapGroups = CW;
@@ -418,12 +419,19 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       // (their latency under the MFMAs), the second's ahead of the first block's epilogue
       uint2 yy[2][NJ];   // row blocks i and i + 1 (a ring: at most two in flight)
       // per-image element offset of column j's output pixel (-1: outside the image; one image < 2^31 elements)
-      auto pix = [&](int j) -> int {
+      auto pixi = [&](int j) -> int {   // per-image pixel index of column j (-1: outside the image)
         const int p = (wave * NJ + j) * 16 + lr;
         const int ty = ty0 + (p >> fg.tw_shift), tx = tx0 + (p & (fg.TW - 1));
-        return (ty < a.H && tx < a.W) ? (ty * a.W + tx) * Ci : -1;
+        return (ty < a.H && tx < a.W) ? ty * a.W + tx : -1;
       };
-      uint16_t* const dxo_im = a.dxo + imoff * Ci;   // this tile's image
+      auto pix = [&](int j) -> int {
+        const int pp = pixi(j);
+        return pp >= 0 ? pp * Ci : -1;
+      };
+      // FWD: output pitch opitch; a Go = 2 pair's rows >= co_split store into the second output tensor
+      const int opitch = FWD ? a.opitch : Ci;
+      uint16_t* const dxo_im = a.dxo + imoff * opitch;   // this tile's image
+      uint16_t* const dxo2_im = FWD && a.co_split > 0 ? a.dxo2 + imoff * opitch : nullptr;
       const uint16_t* const bny_im = BNE ? a.bn_y + imoff * Ci : nullptr;
       auto load_y = [&](int i) {
 #pragma unroll
@@ -463,6 +471,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         if (BNE && !lds_y && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
+        const bool og2 = FWD && a.co_split > 0 && cb >= a.co_split;   // (4-row blocks never straddle the split)
+        uint16_t* const obase = og2 ? dxo2_im + (cb - a.co_split) : dxo_im + cb;
         float sc[4], sh[4], mu[4];
         if (BNE) {
 #pragma unroll
@@ -474,8 +484,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const int pm = pix(j);
-          if (pm < 0) continue;
+          const int pp = pixi(j);
+          if (pp < 0) continue;
           f32x4_t v = acc[i][j];
           if (FWD) {
 #pragma unroll
@@ -483,7 +493,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
           }
           const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
 #ifndef FB_KO_STORE   // (profiling knock-out builds only)
-          *reinterpret_cast<uint2*>(dxo_im + pm + cb) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(obase + pp * opitch) = make_uint2(lo, hi);
 #endif
           if (FWD) {   // the output's BN statistics, of the stored (bf16) values
             const float g4[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
@@ -670,11 +680,16 @@ size_t fb_lds(const FusedBwdGeom& fg) {
 // fwd: the forward mode (conv_fwd_fused): x staged in the dY slots, no x tile, any tap set (the halo is the
 // forward taps' extent; the kernel gets the negated taps so that its data-gradient offsets walk them)
 static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
-  // Go == 2: the ResidualBlock's 3x3 + 1x1 pair (the 1x1 at one tap of the 3x3's grid, FusedBwdArgs::t1)
-  if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > (fwd ? 1 : 2) || g.OH != g.IH || g.OW != g.IW) return false;
-  // <= 32 channels: 2 sixteen-channel blocks; <= 48 (the 34-channel level): 3, one output group only
-  const int cb = std::max(g.Cgi, g.Cgo) > 32 ? 3 : 2;
-  if (g.Cgi > 48 || g.Cgo > 48 || (cb == 3 && g.Go != 1) || g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2)
+  // Go == 2: the ResidualBlock's 3x3 + 1x1 pair (the 1x1 at one tap of the 3x3's grid, FusedBwdArgs::t1) --
+  // backward: two dY groups; forward: one staged input, the two groups' outputs as stacked kernel rows
+  if (g.stride != 1 || g.Gi != 1 || g.Go < 1 || g.Go > 2 || g.OH != g.IH || g.OW != g.IW) return false;
+  const int orows = fwd ? g.Go * g.Cgo : g.Cgo;   // the kernel's data-gradient rows (fwd: output channels)
+  // <= 32 channels: 2 sixteen-channel blocks; <= 48 (the 34-channel level, the 24-channel pair's forward): 3;
+  // <= 80 (forward only: the 40-channel pair's two stacked output groups): 5
+  const int mc = std::max(g.Cgi, orows);
+  const int cb = mc > 48 ? 5 : (mc > 32 ? 3 : 2);
+  if (g.Cgi > 48 || orows > (fwd ? 80 : 48) || (cb == 5 && orows <= 64) || (cb == 3 && !fwd && g.Go != 1) ||
+      g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2)
     return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
   for (int t = 0; t < g.T; ++t) {
@@ -684,9 +699,10 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
     ey0 = std::min(ey0, g.dy[t]); ey1 = std::max(ey1, g.dy[t]);
     ex0 = std::min(ex0, g.dx[t]); ex1 = std::max(ex1, g.dx[t]);
   }
-  const int C8g = (fwd ? g.Cgi : g.Cgo) / 8, C8y = g.Go * C8g, C8x = fwd ? 0 : g.Cgi / 8;
+  const int Gy = fwd ? 1 : g.Go;   // staged dY groups (fwd: the one input)
+  const int C8g = (fwd ? g.Cgi : g.Cgo) / 8, C8y = Gy * C8g, C8x = fwd ? 0 : g.Cgi / 8;
   const int py = 8 * ((C8y & 1) ? C8y : C8y + 1), px = fwd ? 0 : 8 * ((C8x & 1) ? C8x : C8x + 1);
-  const int KS = (g.T * C8g + (g.Go == 2 ? C8g : 0) + 3) / 4;
+  const int KS = (g.T * C8g + (Gy == 2 ? C8g : 0) + 3) / 4;
   if (KS > kFbMaxKS) return false;
   double best = 1e30;
   bool found = false;
@@ -695,9 +711,10 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
     if (tp == 128 && found) break;
     // (cb 3 backward: the 9 x 4 weight-gradient accumulators of 3 units need the 256-register budget of CW 4)
     // (8 compute waves for one output group, 4 for the Go = 2 pair: profiles/r05/fused_bwd_cw_and_knockouts_bs320.txt)
-    const int cw = (tp <= 256 || (cb == 3 && !fwd)) ? 4 : (g.Go == 1 ? 8 : 4);
+    // (cb 5: the 5 x NJ data-gradient accumulators exceed the 168-register cap of CW 8)
+    const int cw = (tp <= 256 || (cb == 3 && !fwd) || cb == 5) ? 4 : (Gy == 1 ? 8 : 4);
     const int nj = tp / (16 * cw);
-    if (cb == 3 && !fwd && tp == 512) continue;   // (never fits the LDS; no instantiation)
+    if ((cb == 3 && !fwd && tp == 512) || (cb == 5 && nj != 4)) continue;   // (no instantiation)
     for (int tw = 16; tw <= 64; tw *= 2) {
       const int th = tp / tw;
       FusedBwdGeom c{};
@@ -777,14 +794,15 @@ static bool fwd_fused_enabled() {
     const char* e = getenv("MSP_CONV_FWD_FUSED");
     g_fwd_fused = (e != nullptr && e[0] == '0') ? 0 : 1;
   }
-  return g_fwd_fused == 1;
+  return g_fwd_fused >= 1;
 }
 
-void conv_set_fwd_fused(int on) { g_fwd_fused = on ? 1 : 0; }
+// (tests / A-B: 0 off, 1 on, 2 on for single-output convs only -- the Go = 2 pair back on the halo kernel)
+void conv_set_fwd_fused(int on) { g_fwd_fused = on == 2 ? 2 : (on ? 1 : 0); }
 
 bool conv_fwd_fused_ok(const ConvGeom& g) {
   FusedBwdGeom fg;
-  return fwd_fused_enabled() && fb_plan(g, fg, true);
+  return fwd_fused_enabled() && (g.Go == 1 || g_fwd_fused == 1) && fb_plan(g, fg, true);
 }
 
 long conv_fwd_fused_blocks(const ConvGeom& g) {
@@ -796,7 +814,8 @@ long conv_fwd_fused_blocks(const ConvGeom& g) {
 int conv_fwd_fused(const ConvArgs& ca, hipStream_t s) {
   const ConvGeom& g = ca.g;
   FusedBwdGeom fg;
-  if (!fb_plan(g, fg, true) || g.Gi != 1 || g.Go != 1 || ca.bn_y != nullptr || ca.accum) return 8;
+  if (!fb_plan(g, fg, true) || g.Gi != 1 || g.Go > 2 || ca.bn_y != nullptr || ca.accum) return 8;
+  if (g.Go == 2 && ca.bias != nullptr) return 8;   // (the pair has no bias; bias4 indexes one group)
   FusedBwdArgs a{};
   a.dz = ca.x[0];          // the staged operand (the data-gradient's dY slots)
   a.x = ca.x[0];
@@ -805,11 +824,14 @@ int conv_fwd_fused(const ConvArgs& ca, hipStream_t s) {
   a.wd = ca.w;             // forward packing [rows][Kp], k = t * Cgi + ci: the data-gradient's [Ci][T * Co]
   a.Kp = g.Kp;
   a.dxo = ca.y[0];
-  a.stat_part = ca.stat_part;
+  a.dxo2 = g.Go == 2 ? ca.y[1] : nullptr;
+  a.co_split = g.Go == 2 ? g.Cgo : 0;
+  a.opitch = g.Cgo;
+  a.stat_part = ca.stat_part;   // [blocks][2][Go * Cgo]: the stacked rows
   a.bias = ca.bias;
   a.Co_l = g.Cgo_l;
   a.N = g.N; a.H = g.IH; a.W = g.IW; a.T = g.T; a.Go = 1;
-  a.Ci = g.Cgo;            // kernel rows = output channels
+  a.Ci = g.Go * g.Cgo;     // kernel rows = output channels (a pair: both groups, stacked)
   a.Co = g.Cgi;            // staged channels = input channels
   for (int t = 0; t < g.T; ++t) { a.dy[t] = -g.dy[t]; a.dx[t] = -g.dx[t]; }
   fb_unit_order(a, fg);
@@ -831,6 +853,7 @@ int conv_fwd_fused(const ConvArgs& ca, hipStream_t s) {
   }
   FF_(8, 4, false, 2) FF_(8, 4, true, 2) FF_(4, 8, false, 2) FF_(4, 8, true, 2) FF_(4, 4, false, 2) FF_(4, 4, true, 2)
   FF_(8, 4, false, 3) FF_(8, 4, true, 3) FF_(4, 4, false, 3) FF_(4, 4, true, 3)
+  FF_(4, 4, false, 5) FF_(4, 4, true, 5)
 #undef FF_
   return 8;
 }

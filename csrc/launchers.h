@@ -321,9 +321,13 @@ struct FusedBwdArgs {
   float* dw;
   int N, H, W, Ci, Co, T;
   int dy[9], dx[9];
-  // forward mode (conv_fwd_fused): per-output-channel bias (nullable) over the Co_l logical channels
+  // forward mode (conv_fwd_fused): per-output-channel bias (nullable) over the Co_l logical channels;
+  // opitch = the output tensors' channel pitch.  co_split > 0: two output groups (the ResidualBlock's 3x3 +
+  // 1x1 pair, stacked rows): rows >= co_split go to dxo2 at channel row - co_split.
   const float* bias;
   int Co_l;
+  uint16_t* dxo2;
+  int co_split, opitch;
   // data-gradient K-unit order (set by conv_bwd_fused): unit index, or -1 for a zero-weight padding unit.  Paired k-groups (0/1, 2/3) share a ds_read_b128 lane group: units paired with
   // equal slot offsets mod 16 read conflict-free.
   short uperm[96];

@@ -223,3 +223,69 @@ def test_fused_forward_vs_fp32_conv(gpu, case):
     p = part.sum(0)
     assert _rel(p[0, :co], s_ref) < 1e-3, _rel(p[0, :co], s_ref)
     assert _rel(p[1, :co], q_ref) < 1e-3, _rel(p[1, :co], q_ref)
+
+
+PAIR_FWD_CASES = [
+    # n, h, w, ci, co, prologue  (ResidualBlock 3x3 + 1x1 pair: co <= 24 -> 48 stacked rows, three 16-row blocks)
+    (3, 40, 56, 17, 17, True),
+    (2, 37, 45, 24, 24, False),
+    (2, 33, 70, 8, 17, True),
+    # the 34-channel level's pair: 2 x 40 = 80 stacked rows, five 16-row blocks
+    (2, 36, 52, 34, 34, True),
+    (2, 29, 43, 40, 40, False),
+]
+
+
+@pytest.mark.parametrize('case', PAIR_FWD_CASES)
+def test_fused_pair_forward_vs_fp32_conv(gpu, case):
+    """The ResidualBlock's 3x3 + 1x1 pair (one Go = 2 plan, the 1x1 at the centre tap) on the fused kernel's
+    forward mode (48 or 80 stacked output rows): both output tensors and the stacked BN-statistics rows against fp32 convs, and the halo kernel."""
+    from medical_segmentation_pytorch_amd.ops._ext import require
+    from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, _taps
+    from medical_segmentation_pytorch_amd.ops.fm import cpad
+    C = require()
+    n, h, w, ci, co, pro = case
+    g = torch.Generator(device=gpu).manual_seed(33)
+    W3 = torch.randn(co, ci, 3, 3, device=gpu, generator=g) * 0.2
+    W1 = torch.randn(co, ci, 1, 1, device=gpu, generator=g) * 0.3
+    plan = ConvPlan(3, 3, ci, co, [Branch(W3, 0, 0, 9), Branch(W1, 1, 4, 1)], padding=(1, 1), Go=2)
+    cp, cq = cpad(ci), cpad(co)
+    dims = plan.fwd_dims(n, h, w, h, w)
+    dy, dx = _taps(plan.taps_fwd)
+    assert C.conv_fwd_fused_ok(dims, dy, dx), 'the pair must take the fused forward'
+    x = torch.zeros(n, h, w, cp, device=gpu, dtype=torch.bfloat16)
+    x[..., :ci] = torch.randn(n, h, w, ci, device=gpu, generator=g).to(torch.bfloat16)
+    coefs, rmask = [None], 0
+    xin = x[..., :ci].permute(0, 3, 1, 2).float()
+    if pro:
+        st = torch.zeros(4, cp, device=gpu)
+        st[0, :ci] = torch.rand(ci, device=gpu, generator=g) + 0.5
+        st[1, :ci] = torch.randn(ci, device=gpu, generator=g) * 0.3
+        coefs, rmask = [st], 1
+        xin = _bf(torch.relu(xin * st[0, :ci].view(1, -1, 1, 1) + st[1, :ci].view(1, -1, 1, 1)))
+    refs = [F.conv2d(xin, _bf(W3), None, 1, 1), F.conv2d(xin, _bf(W1), None, 1, 0)]
+    outs = {}
+    for fused in (True, False):
+        C.conv_set_fwd_fused(fused)
+        try:
+            ys = [torch.full((n, h, w, cq), float('nan'), device=gpu, dtype=torch.bfloat16) for _ in range(2)]
+            part = torch.empty(C.conv_stat_blocks(dims, dy, dx), 2, plan.rows, device=gpu)
+            C.conv_fwd([x], plan.pack_fwd(gpu), ys, None, part, dims, dy, dx, False, coefs, rmask)
+            torch.cuda.synchronize()
+            outs[fused] = (ys, part)
+        finally:
+            C.conv_set_fwd_fused(True)
+    ys, part = outs[True]
+    p = part.sum(0)
+    for gi, (y, ref) in enumerate(zip(ys, refs)):
+        got = y[..., :co].permute(0, 3, 1, 2).float()
+        assert torch.isfinite(got).all()
+        assert _rel(got, ref) < 1e-2, (gi, _rel(got, ref))
+        if cq > co:
+            assert y[..., co:].float().abs().max().item() == 0.0
+        yh = outs[False][0][gi]
+        assert _rel(got, yh[..., :co].permute(0, 3, 1, 2).float()) < 5e-3
+        s_ref, q_ref = got.sum((0, 2, 3)), (got * got).sum((0, 2, 3))
+        o = gi * cq
+        assert _rel(p[0, o:o + co], s_ref) < 1e-3, (gi, _rel(p[0, o:o + co], s_ref))
+        assert _rel(p[1, o:o + co], q_ref) < 1e-3, (gi, _rel(p[1, o:o + co], q_ref))
