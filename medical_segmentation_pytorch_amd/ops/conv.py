@@ -230,7 +230,7 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
     prologue) are staged once per tile; the BN epilogue of the data-gradient (BwdStatsHandle) runs in it too.
     Returns (dxs, wgrads) or None when the shape is not eligible."""
     if not (FUSED_BWD and need_dx and not plan.transposed and plan.stride == 1 and plan.Gi == 1 and plan.Go <= 2
-            and plan.bias is None and plan.Cgi <= 32 and plan.Cgo <= 32 and 2 <= plan.T <= 9
+            and plan.bias is None and plan.Cgi <= 48 and plan.Cgo <= 48 and 2 <= plan.T <= 9
             and all(b.weight.requires_grad for b in plan.branches)):
         return None
     t1 = -1
