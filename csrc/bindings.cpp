@@ -1015,7 +1015,7 @@ void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy,
                       const c10::optional<at::Tensor>& stat_part, const at::Tensor& dw, std::vector<int64_t> dims,
                       std::vector<int64_t> dy, std::vector<int64_t> dx, const c10::optional<at::Tensor>& dz2,
                       const c10::optional<at::Tensor>& gy2, const c10::optional<at::Tensor>& gs2,
-                      const c10::optional<at::Tensor>& gk2, bool grelu2, int64_t t1) {
+                      const c10::optional<at::Tensor>& gk2, bool grelu2, int64_t t1, bool accumulate) {
   ConvGeom g = make_geom(dims, dy, dx);
   const int64_t nblk = conv_bwd_fused_blocks(g);
   TORCH_CHECK(nblk > 0, "conv_bwd_fused: shape not eligible");
@@ -1066,6 +1066,7 @@ void conv_bwd_fused_t(const at::Tensor& dz, const c10::optional<at::Tensor>& gy,
   }
   a.bn_relu = bn_relu ? 1 : 0;
   a.dw = f32(dw);
+  a.accum = accumulate ? 1 : 0;
   const int rc = conv_bwd_fused(a, g, cur_stream());
   TORCH_CHECK(rc == 0, "conv_bwd_fused: launch failed (", rc, ")");
 }
@@ -1210,7 +1211,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("grelu"), py::arg("x"), py::arg("xc"), py::arg("xrelu"), py::arg("wd"), py::arg("Kp_d"), py::arg("dxo"),
         py::arg("bn_y"), py::arg("bn_coef"), py::arg("bn_relu"), py::arg("stat_part"), py::arg("dw"), py::arg("dims"),
         py::arg("dy"), py::arg("dx"), py::arg("dz2") = py::none(), py::arg("gy2") = py::none(),
-        py::arg("gs2") = py::none(), py::arg("gk2") = py::none(), py::arg("grelu2") = false, py::arg("t1") = -1);
+        py::arg("gs2") = py::none(), py::arg("gk2") = py::none(), py::arg("grelu2") = false, py::arg("t1") = -1,
+        py::arg("accumulate") = false);
   m.def("comm_buffer_bytes", &comm_buffer_bytes);
   m.def("comm_alloc", &comm_alloc_t);
   m.def("comm_open", &comm_open_t);

@@ -72,7 +72,7 @@ DEVI uint4 fb_ldg4(const uint16_t* p) {   // global_load (never FLAT: see conv.h
 }
 
 // CB: 16-channel blocks of the data-gradient rows and of both weight-gradient operands: 2 (<= 32 channels, the
-// 17-channel level) or 3 (<= 48: the 34-channel level, Go = 1, CW = 4, 256-pixel tiles); forward mode also 5 (the
+// 17-channel level) or 3 (<= 48: the 34-channel level, CW = 4, 256-pixel tiles; 128 for the Go = 2 pair); forward mode also 5 (the
 // 34-channel level's 3x3 + 1x1 pair: 2 x 40 stacked output rows)
 template <int CW, int NJ, bool BWD, bool XPRO, bool BNE, bool GO2 = false, bool FWD = false, int CB = 2>
 __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(FusedBwdArgs a, FusedBwdGeom fg) {
@@ -88,7 +88,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   const int wp = 32 * fg.KS + 8;                           // weight row pitch (elements; +16 B: bank spread)
   uint16_t* const s_w = lds0 + 2 * pair;                   // [CH rows][wp] data-gradient weights, per block
   float* s_stat = reinterpret_cast<float*>(s_w + CH * wp);   // [waves][2][CH]
-  __shared__ float s_bt[BWD ? 5 * 64 : 1];    // dY rebuild table (stacked groups): scale, shift (+inf: no
+  constexpr int BTS = 2 * CH;                 // rebuild-table row: two stacked dY groups of <= CH channels
+  __shared__ float s_bt[BWD ? 5 * BTS : 1];   // dY rebuild table (stacked groups): scale, shift (+inf: no
                                               // ReLU), k1, k2, k3
   __shared__ float s_xt[XPRO ? 2 * CH : 1];   // x prologue: scale, shift
   __shared__ float s_bn[BNE ? 5 * CH : 1];    // BN1 backward partials: scale, shift (+inf: no ReLU), mean,
@@ -106,16 +107,16 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
   const int nU0 = T * C8g, nU = nU0 + (Go == 2 ? C8g : 0);   // data-gradient K units (tap, 8 channels)
   const int nWU = T + (Go == 2 ? 1 : 0);                     // weight-gradient (group, tap) units
   if constexpr (BWD) {
-    for (int c = tid; c < 64; c += kFbThreads) {
+    for (int c = tid; c < BTS; c += kFbThreads) {
       const int g = c >= Co ? 1 : 0, cl = c - g * Co;
       const float* gs = g ? a.gs2 : a.gs;
       const float* gk = g ? a.gk2 : a.gk;
       const bool on = c < Go * Co && (g ? a.gy2 : a.gy) != nullptr;
       s_bt[c] = on ? gs[cl] : 0.f;
-      s_bt[64 + c] = (on && (g ? a.grelu2 : a.grelu)) ? gs[Co + cl] : INFINITY;
-      s_bt[128 + c] = on ? gk[cl] : 0.f;
-      s_bt[192 + c] = on ? gk[Co + cl] : 0.f;
-      s_bt[256 + c] = on ? gk[2 * Co + cl] : 0.f;
+      s_bt[BTS + c] = (on && (g ? a.grelu2 : a.grelu)) ? gs[Co + cl] : INFINITY;
+      s_bt[2 * BTS + c] = on ? gk[cl] : 0.f;
+      s_bt[3 * BTS + c] = on ? gk[Co + cl] : 0.f;
+      s_bt[4 * BTS + c] = on ? gk[2 * Co + cl] : 0.f;
     }
   }
   if constexpr (XPRO) {
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
 #pragma unroll
       for (int r = 0; r < 5; ++r)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) cfy[8 * r + e] = s_bt[64 * r + 8 * c8y + e];
+        for (int e = 0; e < 8; ++e) cfy[8 * r + e] = s_bt[BTS * r + 8 * c8y + e];
     } else if constexpr (FWD && XPRO) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { cfy[e] = s_xt[8 * c8y + e]; cfy[8 + e] = s_xt[CH + 8 * c8y + e]; }
@@ -490,6 +491,10 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
           if (FWD) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += bias4[i][r];
+          } else if (a.accum) {   // (block-uniform) sibling launches' data-gradients into one tensor
+            const uint2 ov = *reinterpret_cast<const uint2*>(obase + pp * opitch);
+            v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
+            v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
           const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
 #ifndef FB_KO_STORE   // (profiling knock-out builds only)
@@ -688,7 +693,7 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
   // <= 80 (forward only: the 40-channel pair's two stacked output groups): 5
   const int mc = std::max(g.Cgi, orows);
   const int cb = mc > 48 ? 5 : (mc > 32 ? 3 : 2);
-  if (g.Cgi > 48 || orows > (fwd ? 80 : 48) || (cb == 5 && orows <= 64) || (cb == 3 && !fwd && g.Go != 1) ||
+  if (g.Cgi > 48 || orows > (fwd ? 80 : 48) || (cb == 5 && orows <= 64) ||
       g.Cgi % 8 || g.Cgo % 8 || g.T > kFbMaxT || g.T < 2)
     return false;
   int ey0 = 0, ey1 = 0, ex0 = 0, ex1 = 0;
@@ -714,7 +719,7 @@ static bool fb_plan(const ConvGeom& g, FusedBwdGeom& fg, bool fwd) {
     // (cb 5: the 5 x NJ data-gradient accumulators exceed the 168-register cap of CW 8)
     const int cw = (tp <= 256 || (cb == 3 && !fwd) || cb == 5) ? 4 : (Gy == 1 ? 8 : 4);
     const int nj = tp / (16 * cw);
-    if ((cb == 3 && !fwd && tp == 512) || (cb == 5 && nj != 4)) continue;   // (no instantiation)
+    if ((cb == 3 && !fwd && (tp == 512 || (Gy == 2 && nj != 2))) || (cb == 5 && nj != 4)) continue;   // (no instantiation)
     for (int tw = 16; tw <= 64; tw *= 2) {
       const int th = tp / tw;
       FusedBwdGeom c{};
@@ -782,6 +787,8 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   FB4_(4, 8, false, false, 2) FB4_(4, 8, true, false, 2) FB4_(4, 4, false, false, 2) FB4_(4, 4, true, false, 2)
   FB4_(4, 8, false, true, 2) FB4_(4, 8, true, true, 2) FB4_(4, 4, false, true, 2) FB4_(4, 4, true, true, 2)
   FB4_(4, 4, false, false, 3) FB4_(4, 4, true, false, 3) FB4_(4, 2, false, false, 3) FB4_(4, 2, true, false, 3)
+  // the 34-channel level's Go = 2 pair (two stacked 40-channel dY groups: only 128-pixel tiles fit the LDS)
+  FB4_(4, 2, false, true, 3) FB4_(4, 2, true, true, 3)
 #undef FB4_
 #undef FB_
   return 8;

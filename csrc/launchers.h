@@ -328,6 +328,9 @@ struct FusedBwdArgs {
   int Co_l;
   uint16_t* dxo2;
   int co_split, opitch;
+  // backward: dx += this launch's data-gradient (the DUCK first convs' sibling launches sum into one dL/dx;
+  // a BN epilogue then sees the summed values)
+  int accum;
   // data-gradient K-unit order (set by conv_bwd_fused): unit index, or -1 for a zero-weight padding unit.  Paired k-groups (0/1, 2/3) share a ds_read_b128 lane group: units paired with
   // equal slot offsets mod 16 read conflict-free.
   short uperm[96];

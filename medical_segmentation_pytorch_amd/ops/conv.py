@@ -224,11 +224,12 @@ FUSED_BWD = os.environ.get('MSP_FUSED_BWD', '1') != '0'
 DEFER_SEPARATE = False
 
 
-def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
+def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev, dxt=None, pro=None, bn_handle=None):
     """Data- and weight-gradient of a narrow stride-1 single-group conv in ONE kernel (csrc/conv_bwd.hip):
     dY (rebuilt from a deferred BN data-gradient when one arrives) and x (through the forward's deferred-BN
     prologue) are staged once per tile; the BN epilogue of the data-gradient (BwdStatsHandle) runs in it too.
-    Returns (dxs, wgrads) or None when the shape is not eligible."""
+    ``dxt``: add the data-gradient into this tensor (sibling launches over one input, :class:`_MultiConvFn`);
+    ``pro`` / ``bn_handle`` default to ``ctx``'s.  Returns (dxs, wgrads) or None when the shape is not eligible."""
     if not (FUSED_BWD and need_dx and not plan.transposed and plan.stride == 1 and plan.Gi == 1 and plan.Go <= 2
             and plan.bias is None and plan.Cgi <= 48 and plan.Cgo <= 48 and 2 <= plan.T <= 9
             and all(b.weight.requires_grad for b in plan.branches)):
@@ -249,11 +250,13 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
     from .bn import claim_deferred, peek_deferred
     d = peek_deferred(gys[0])
     d2 = peek_deferred(gys[1]) if plan.Go == 2 else None
-    coefs, rmask = ctx.pro
+    coefs, rmask = ctx.pro if pro is None else pro
     xc = coefs[0] if coefs else None
     wd, Kp_d = plan.pack_dgrad(dev)
-    dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
-    h = ctx.bn_handle
+    accumulate = dxt is not None
+    if not accumulate:
+        dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
+    h = ctx.bn_handle if pro is None else bn_handle
     bne = h is not None and h.y is not None
     part = torch.empty(nblk, 2, plan.Cgi, dtype=torch.float32, device=dev) if bne else None
     dwp = torch.empty(nblk * plan.rows * plan.T * plan.Cip, dtype=torch.float32, device=dev)
@@ -266,7 +269,7 @@ def _fused_bwd(ctx, plan, gys, xs, shape, need_dx, dev):
                      dz2=(d2.dz if d2 is not None else gys[1]) if plan.Go == 2 else None,
                      gy2=d2.y if d2 is not None else None, gs2=d2.stats if d2 is not None else None,
                      gk2=d2.coef if d2 is not None else None, grelu2=bool(d2.relu) if d2 is not None else False,
-                     t1=t1)
+                     t1=t1, accumulate=accumulate)
     if bne:
         h.part = part
     for dd in (d, d2):
@@ -604,11 +607,20 @@ class _MultiConvFn(torch.autograd.Function):
         n, ih, iw = ctx.shape
         dev = x.device
         dxt, o, per_plan = None, 0, []
-        for plan in ctx.plans:
+        fused_w = {}   # plan index -> weight gradients from the fused backward kernel (dgrad + wgrad in one)
+        for pi, plan in enumerate(ctx.plans):
             oh, ow = plan.out_hw(ih, iw)
             gys = [torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None else g.contiguous()
                    for g in grads[o:o + plan.Go]]
             o += plan.Go
+            if ctx.aug is None and ctx.needs_input_grad[4]:
+                # narrow plans: one fused launch (deferred dY rebuilt in staging), its dgrad added into dxt
+                fused = _fused_bwd(ctx, plan, gys, [x], (n, ih, iw, oh, ow), True, dev, dxt=dxt, pro=ctx.pro)
+                if fused is not None:
+                    dxt = fused[0][0]
+                    fused_w[pi] = fused[1]
+                    per_plan.append(None)
+                    continue
             dims_d = [n, oh, ow, plan.Go, plan.Cgo, ih, iw, plan.Gi, plan.Cgi, plan.ci_l, plan.T, plan.Kp_d, plan.stride]
             dy, dx = _taps(plan.taps_bwd)
             gys, bwd = _bwd_operands(gys, plan, dims_d, (dy, dx), plan.fwd_dims(n, ih, iw, oh, ow),
@@ -622,7 +634,13 @@ class _MultiConvFn(torch.autograd.Function):
                     dxt = torch.empty(n, ih, iw, plan.Cgi, dtype=torch.bfloat16, device=dev)
                 C.conv_fwd(gys, wd, [dxt], None, None, dims_d, dy, dx, False, accumulate=not first, **bk)
         wgrads = []
-        for plan, (gys, bk, bwd) in zip(ctx.plans, per_plan):
+        for pi, (plan, pp) in enumerate(zip(ctx.plans, per_plan)):
+            if pp is None:
+                wgrads += fused_w[pi]
+                if plan.ready_hook is not None:
+                    plan.ready_hook([b.weight for b in plan.branches])
+                continue
+            gys, bk, bwd = pp
             oh, ow = plan.out_hw(ih, iw)
             wgrads += _conv_wgrad(plan, gys, [x], (n, ih, iw, oh, ow), dev, ctx.pro, bk, aug=ctx.aug)
             if bwd is not None:

@@ -61,16 +61,28 @@ _FUSED_DECODERS = os.environ.get('MSP_FUSED_DECODERS', '1') != '0'
 # (tools/conv_bench.py, profiles/r02/conv_bench_duck_splits_bs128.log): 17 ch @352: 8 = 10.1 vs 5+3 =
 # 10.6 (the input is the largest tensor: reading it once wins); 34 @176: 8.4 vs 7.0; 68 @88: 8.4 vs 5.5;
 # 136 @44: 7.0 vs 5.1 vs 3+2+3 = 4.9; 272 @22: 7.1 vs 5.8 vs 4.9.
-def _default_split(cout):
+# Round 6: where the fused narrow-conv kernel takes every piece (input and output <= 48 / 40 channels), split 'P':
+# wide and mid as single 3x3 plans and each residual 3x3 with its own 1x1 shortcut as a Go = 2 pair -- every
+# launch then runs the fused forward mode and the fused data+weight-gradient backward (deferred dY rebuilt in
+# staging, the data-gradients summed by the accumulate epilogue): no apply passes, no chunked halo dgrad.
+_PAIRS = [[0], [1], [2, 5], [3, 6], [4, 7]]
+
+
+def _default_split(cout, cin=None, pairs_ok=True):
     c = (cout + 7) // 8 * 8
+    if pairs_ok and cin is not None and (cin + 7) // 8 * 8 <= 48 and c <= 40:
+        return 'P'
     return '8' if c <= 24 else ('5+3' if c <= 72 else '3+2+3')
 
 
-def duck_split(cout):
-    """Launches of a DUCK block's first convs (``cout`` output channels each): consecutive runs of the
-    order 0..7."""
+def duck_split(cout, cin=None, pairs_ok=True):
+    """Launches of a DUCK block's first convs (``cout`` output channels each, reading ``cin``): consecutive
+    runs of the order 0..7, or 'P' (see _PAIRS); ``pairs_ok`` False: the block needs one plan over all 8
+    (the first DUCK's in_bn shortcut)."""
     spec = (os.environ.get('MSP_DUCK_SPLIT') or os.environ.get(f'MSP_DUCK_SPLIT_{cout}')   # per-width override
-            or _default_split(cout))
+            or _default_split(cout, cin, pairs_ok))
+    if spec == 'P':
+        return [list(g) for g in _PAIRS]
     sizes = [int(n) for n in spec.split('+')]
     assert sum(sizes) == 8 and min(sizes) > 0, f'bad DUCK split {spec}'
     starts = [sum(sizes[:i]) for i in range(len(sizes))]
@@ -335,12 +347,6 @@ class FusedExecutor(SmpDecoders):
         # the 8 convs reading xb as one or more multi-output launches (duck_split); src[g] = (outputs,
         # partials, plan, index) of conv g
         src = [None] * 8
-        plans, orders = [], []
-        for li, idx in enumerate(duck_split(allc[0].out_channels)):
-            i3, i1 = [i for i in idx if i < 5], [i for i in idx if i >= 5]
-            plans.append(self.plan_fused3x3(('duck', id(m), li), [allc[i] for i in i3], [allc[i] for i in i1])
-                         if i3 else self.plan_fused1x1(('duck', id(m), li), [allc[i] for i in i1]))
-            orders.append(i3 + i1)   # plan output groups: 3x3 convs first, then the 1x1s
         # the separated branch's 1x7 reads xb too: it joins the same node (its data-gradient accumulates
         # into dL/dxb as well -- no autograd add pass for xb's gradient at all)
         sep_plan = self.plan_conv(b6[0][0])
@@ -355,6 +361,14 @@ class FusedExecutor(SmpDecoders):
                     and all(c.in_channels == nf for c in allc + [b6[0][0]])):
                 aug = InBnAug(st, nf)
                 xb = aug_in_bn(xb, nf)
+        plans, orders = [], []
+        split = duck_split(allc[0].out_channels, allc[0].in_channels, pairs_ok=multi and aug is None)
+        for li, idx in enumerate(split):
+            i3, i1 = [i for i in idx if i < 5], [i for i in idx if i >= 5]
+            plans.append(self.plan_fused3x3(('duck', id(m), li, len(split)), [allc[i] for i in i3],
+                                            [allc[i] for i in i1])
+                         if i3 else self.plan_fused1x1(('duck', id(m), li, len(split)), [allc[i] for i in i1]))
+            orders.append(i3 + i1)   # plan output groups: 3x3 convs first, then the 1x1s
         if multi:
             outs = conv_multi(plans + [sep_plan], xb, want_stats=training, aug=aug)
             sep_y, sep_part = outs[-1][0][0], outs[-1][1]

@@ -128,7 +128,8 @@ def test_fused_engine_coverage_of_smp_hub():
 
 def test_duck_split_partitions():
     """The DUCK first-conv launch split (runtime.fused_model.duck_split): every width's default and every
-    env override is a partition of the 8 convs into consecutive runs (3x3 convs 0-4 first)."""
+    env override is a partition of the 8 convs into consecutive runs (3x3 convs 0-4 first), or -- narrow blocks --
+    single 3x3 plans and (3x3, its 1x1 shortcut) pairs."""
     import os
     from medical_segmentation_pytorch_amd.runtime import fused_model
     for c in (17, 34, 68, 136, 272, 544):
@@ -137,6 +138,16 @@ def test_duck_split_partitions():
         assert all(p == list(range(p[0], p[0] + len(p))) for p in parts)
     assert fused_model.duck_split(17) == [list(range(8))]
     assert fused_model.duck_split(68) == [[0, 1, 2, 3, 4], [5, 6, 7]]
+    # narrow blocks (input <= 48, output <= 40 padded channels): singles + residual 3x3/1x1 pairs ('P')
+    pairs = [[0], [1], [2, 5], [3, 6], [4, 7]]
+    assert fused_model.duck_split(17, 17) == pairs and fused_model.duck_split(17, 34) == pairs
+    assert fused_model.duck_split(34, 34) == pairs
+    assert fused_model.duck_split(34, 68) == [[0, 1, 2, 3, 4], [5, 6, 7]]   # 72-channel input: the GEMM / halo split
+    assert fused_model.duck_split(17, 3, pairs_ok=False) == [list(range(8))]   # the first DUCK (in_bn shortcut)
+    for c, ci in ((17, 17), (34, 34)):
+        parts = fused_model.duck_split(c, ci)
+        assert sorted(i for p in parts for i in p) == list(range(8))
+        assert all(len(p) == 1 or (len(p) == 2 and p[0] < 5 <= p[1]) for p in parts)
     old = os.environ.get('MSP_DUCK_SPLIT')
     try:
         os.environ['MSP_DUCK_SPLIT'] = '3+2+3'
