@@ -433,7 +433,10 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       const int opitch = FWD ? a.opitch : Ci;
       uint16_t* const dxo_im = a.dxo + imoff * opitch;   // this tile's image
       uint16_t* const dxo2_im = FWD && a.co_split > 0 ? a.dxo2 + imoff * opitch : nullptr;
-      const uint16_t* const bny_im = BNE ? a.bn_y + imoff * Ci : nullptr;
+      // accumulate (never with BNE, conv_bwd_fused): the ring prefetches the stored dx instead of y1 -- a load in the
+      // epilogue itself exposed its whole latency (+0.76 ms on an L1 launch at bs320)
+      const bool accum = !FWD && a.accum != 0;   // block-uniform
+      const uint16_t* const bny_im = accum ? dxo_im : (BNE ? a.bn_y + imoff * Ci : nullptr);
       auto load_y = [&](int i) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -443,7 +446,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
         }
       };
       const bool lds_y = BNE && XPRO && s_ldsy != 0;   // block-uniform
-      if (BNE && !lds_y) load_y(0);
+      const bool ring = (BNE && !lds_y) || accum;
+      if (ring) load_y(0);
       f32x4_t acc[MI][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -469,7 +473,7 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
       // epilogue: dz1 (bf16, NHWC) for the in-image pixels and channels < Ci
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        if (BNE && !lds_y && i + 1 < MI) load_y(i + 1);
+        if (ring && i + 1 < MI) load_y(i + 1);
         const int cb = 16 * i + 4 * lg;
         if (cb >= Ci) continue;
         const bool og2 = FWD && a.co_split > 0 && cb >= a.co_split;   // (4-row blocks never straddle the split)
@@ -491,8 +495,8 @@ __global__ __launch_bounds__(fb_threads(CW), 1) void conv_bwd_fused_kernel(Fused
           if (FWD) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += bias4[i][r];
-          } else if (a.accum) {   // (block-uniform) sibling launches' data-gradients into one tensor
-            const uint2 ov = *reinterpret_cast<const uint2*>(obase + pp * opitch);
+          } else if (accum) {   // sibling launches' data-gradients into one tensor (the ring's prefetched dx)
+            const uint2 ov = yy[i & 1][j];
             v[0] += __uint_as_float(ov.x << 16); v[1] += __uint_as_float(ov.x & 0xffff0000u);
             v[2] += __uint_as_float(ov.y << 16); v[3] += __uint_as_float(ov.y & 0xffff0000u);
           }
@@ -762,6 +766,7 @@ int conv_bwd_fused(const FusedBwdArgs& a0, const ConvGeom& g, hipStream_t s) {
   a.N = g.N; a.H = g.IH; a.W = g.IW; a.Ci = g.Cgi; a.Co = g.Cgo; a.T = g.T;   // a.Kp: the dgrad packing's Kp
   a.Go = g.Go;
   if (g.Go == 2 && (a.dz2 == nullptr || a.t1 < 0 || a.t1 >= g.T)) return 8;
+  if (a.accum && a.bn_y != nullptr) return 8;   // (one epilogue prefetch ring: dx or y1, not both)
   if ((a.gy != nullptr) != (a.gs != nullptr) || (a.gy2 != nullptr) != (a.gs2 != nullptr)) return 8;
   for (int t = 0; t < g.T; ++t) { a.dy[t] = g.dy[t]; a.dx[t] = g.dx[t]; }
   fb_unit_order(a, fg);

@@ -53,8 +53,11 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize('acc', [False, True])
 @pytest.mark.parametrize('case', CASES)
-def test_fused_bwd_vs_fp32_conv_grads(gpu, case):
+def test_fused_bwd_vs_fp32_conv_grads(gpu, case, acc):
+    """``acc``: the accumulate epilogue (dx += this launch's data-gradient, the DUCK first convs' sibling launches)
+    on a pre-filled dx, without the BN epilogue (the kernel takes one or the other)."""
     from medical_segmentation_pytorch_amd.ops._ext import require
     from medical_segmentation_pytorch_amd.ops.conv import Branch, ConvPlan, _taps
     from medical_segmentation_pytorch_amd.ops.fm import cpad
@@ -119,13 +122,18 @@ def test_fused_bwd_vs_fp32_conv_grads(gpu, case):
     # the kernel
     wd, kp = plan.pack_dgrad(gpu)
     dxt = torch.empty(n, h, w, cp, dtype=torch.bfloat16, device=gpu)
+    if acc:
+        dxt.zero_()
+        dxt[..., :ci] = torch.randn(n, h, w, ci, device=gpu, generator=g).to(torch.bfloat16)
+        dx_ref = dx_ref + nchw(dxt, ci)
     part = torch.empty(nblk, 2, cp, device=gpu)
     dwp = torch.empty(nblk * plan.rows * plan.T * plan.Cip, device=gpu)
     kw2 = {}
     if go == 2:
         kw2 = dict(dz2=dzs[1], gy2=y2s[1], gs2=st2s[1], gk2=k2s[1], grelu2=True, t1=T // 2)
-    C.conv_bwd_fused(dzs[0], y2s[0], st2s[0], k2s[0], True, y1, st1, True, wd, kp, dxt, y1, st1[:3].contiguous(), True,
-                     part, dwp, dims, tdy, tdx, **kw2)
+    C.conv_bwd_fused(dzs[0], y2s[0], st2s[0], k2s[0], True, y1, st1, True, wd, kp, dxt, None if acc else y1,
+                     None if acc else st1[:3].contiguous(), True, None if acc else part, dwp, dims, tdy, tdx,
+                     accumulate=acc, **kw2)
     torch.cuda.synchronize()
     dx = nchw(dxt, ci)
     assert torch.isfinite(dx).all()
@@ -140,6 +148,8 @@ def test_fused_bwd_vs_fp32_conv_grads(gpu, case):
         else:
             got = got[:, T // 2, :].reshape(co, ci, 1, 1)
         assert _rel(got, ref) < 1e-2, (gi, _rel(got, ref))
+    if acc:
+        return
     # BN1 backward partials of the kernel's own (bf16) data-gradient: sum g, sum g * (y1 - mean)
     y1f = nchw(y1, ci)
     m1 = (y1f * st1[0, :ci].view(1, -1, 1, 1) + st1[1, :ci].view(1, -1, 1, 1)) > 0
