@@ -576,7 +576,8 @@ class _MultiConvFn(torch.autograd.Function):
     def forward(ctx, plans, want_stats, pro, aug, x, *weights):
         C = require()
         ctx.set_materialize_grads(False)
-        ctx.aug = aug
+        ctx.aug, aug = aug if isinstance(aug, tuple) else (aug, True)   # (InBnAug | None, fused backward allowed)
+        ctx.fused_ok = aug
         x = x.contiguous()
         coefs, rmask = pro
         n, ih, iw, _ = x.shape
@@ -613,7 +614,7 @@ class _MultiConvFn(torch.autograd.Function):
             gys = [torch.zeros(n, oh, ow, plan.Cgo, dtype=torch.bfloat16, device=dev) if g is None else g.contiguous()
                    for g in grads[o:o + plan.Go]]
             o += plan.Go
-            if ctx.aug is None and ctx.needs_input_grad[4]:
+            if ctx.aug is None and ctx.fused_ok and ctx.needs_input_grad[4]:
                 # narrow plans: one fused launch (deferred dY rebuilt in staging), its dgrad added into dxt
                 fused = _fused_bwd(ctx, plan, gys, [x], (n, ih, iw, oh, ow), True, dev, dxt=dxt, pro=ctx.pro)
                 if fused is not None:
@@ -655,10 +656,12 @@ class _MultiConvFn(torch.autograd.Function):
         return (None, None, None, None, dxt) + tuple(wgrads)
 
 
-def conv_multi(plans, x, want_stats=False, aug=None):
+def conv_multi(plans, x, want_stats=False, aug=None, fused_bwd=True):
     """Several stride-1 single-group plans on the same input ``x`` (tensor or Deferred) as one node;
     returns [(outputs, stat partials)] per plan.  ``aug``: ``x`` is :func:`ops.bn.aug_in_bn`'s tensor and
-    ``aug`` the :class:`InBnAug` that turns the weight-gradient slabs into in_bn's gradients."""
+    ``aug`` the :class:`InBnAug` that turns the weight-gradient slabs into in_bn's gradients.  ``fused_bwd``
+    False: every plan's backward on the separate data- / weight-gradient kernels (the in_bn-shortcut block with
+    the shortcut off, which must match the shortcut's weight gradients bitwise)."""
     from .bn import Deferred, materialize, split_inputs
     for p in plans:
         assert p.stride == 1 and p.Gi == 1 and not p.transposed and p.bias is None
@@ -669,7 +672,7 @@ def conv_multi(plans, x, want_stats=False, aug=None):
     x = x.z if isinstance(x, Deferred) and x.z is not None else x
     (t,), coefs, mask = split_inputs([x])
     weights = [b.weight for p in plans for b in p.branches]
-    out = _MultiConvFn.apply(plans, want_stats, (coefs, mask), aug, t, *weights)
+    out = _MultiConvFn.apply(plans, want_stats, (coefs, mask), (aug, fused_bwd), t, *weights)
     res, o = [], 0
     ngo = sum(p.Go for p in plans)
     for i, p in enumerate(plans):

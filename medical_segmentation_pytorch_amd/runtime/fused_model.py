@@ -351,18 +351,21 @@ class FusedExecutor(SmpDecoders):
         # into dL/dxb as well -- no autograd add pass for xb's gradient at all)
         sep_plan = self.plan_conv(b6[0][0])
         multi = _MULTI and sep_plan.stride == 1 and sep_plan.bias is None
-        aug = None
-        if multi and training and _AUG_INBN and len(xs) == 1 and isinstance(xs[0], torch.Tensor) and \
+        aug, aug_ok = None, False
+        if multi and training and len(xs) == 1 and isinstance(xs[0], torch.Tensor) and \
                 not xs[0].requires_grad and isinstance(xb, Deferred) and xb.relu:
             # in_bn over an input that needs no gradient (the image): the InBnAug shortcut
             st = self.bn(m.in_bn[0])
             nf = m.in_bn[0].num_features
-            if (xb.t.shape[-1] == 8 and 2 * nf <= 8 and st.weight_sink is not None and st.bias_sink is not None
-                    and all(c.in_channels == nf for c in allc + [b6[0][0]])):
+            aug_ok = (xb.t.shape[-1] == 8 and 2 * nf <= 8 and st.weight_sink is not None and st.bias_sink is not None
+                      and all(c.in_channels == nf for c in allc + [b6[0][0]]))
+            if aug_ok and _AUG_INBN:
                 aug = InBnAug(st, nf)
                 xb = aug_in_bn(xb, nf)
         plans, orders = [], []
-        split = duck_split(allc[0].out_channels, allc[0].in_channels, pairs_ok=multi and aug is None)
+        # (the shortcut-eligible block keeps its one 8-group plan with the shortcut off too: the data-gradient path
+        # then differs from the shortcut only in in_bn's gradients -- tests/test_gpu_models.py)
+        split = duck_split(allc[0].out_channels, allc[0].in_channels, pairs_ok=multi and not aug_ok)
         for li, idx in enumerate(split):
             i3, i1 = [i for i in idx if i < 5], [i for i in idx if i >= 5]
             plans.append(self.plan_fused3x3(('duck', id(m), li, len(split)), [allc[i] for i in i3],
@@ -370,7 +373,7 @@ class FusedExecutor(SmpDecoders):
                          if i3 else self.plan_fused1x1(('duck', id(m), li, len(split)), [allc[i] for i in i1]))
             orders.append(i3 + i1)   # plan output groups: 3x3 convs first, then the 1x1s
         if multi:
-            outs = conv_multi(plans + [sep_plan], xb, want_stats=training, aug=aug)
+            outs = conv_multi(plans + [sep_plan], xb, want_stats=training, aug=aug, fused_bwd=not aug_ok)
             sep_y, sep_part = outs[-1][0][0], outs[-1][1]
             outs = outs[:-1]
         else:

@@ -47,6 +47,9 @@ CASES = [
     (2, 44, 30, 34, 34, (7, 1), 1, 1),
     (2, 28, 66, 34, 34, (1, 7), 1, 1),
     (1, 30, 40, 40, 24, (3, 3), 1, 1),
+    # the 8-channel image input (the first DUCK's convs) into 17 channels: single and pair
+    (2, 36, 44, 8, 17, (3, 3), 1, 1),
+    (2, 33, 41, 8, 17, (3, 3), 1, 2),
     # the 34-channel level's 3x3 + 1x1 pair: two stacked 40-channel dY groups, 128-pixel tiles
     (2, 36, 52, 34, 34, (3, 3), 1, 2),
     (1, 29, 43, 40, 40, (3, 3), 1, 2),
