@@ -352,6 +352,20 @@ void bn_bwd_finalize_t(const at::Tensor& tmp, int64_t C, int64_t Cp, double coun
                   st + 2 * Cp, f32_opt_mut(dgamma), f32_opt_mut(dbeta), f32(coef), (float)pscale, cur_stream());
 }
 
+void bn_act_bwd_apply_part_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& coef,
+                             const at::Tensor& dy, const at::Tensor& y2, const at::Tensor& stats2, bool relu2,
+                             const at::Tensor& part, int64_t P, int64_t Cp, bool relu) {
+  CHECK_BF16(dz); CHECK_BF16(y); CHECK_BF16(dy); CHECK_BF16(y2); CHECK_F32(stats); CHECK_F32(coef);
+  CHECK_F32(stats2); CHECK_F32(part);
+  TORCH_CHECK(dz.numel() == P * Cp && y.numel() == P * Cp && dy.numel() == P * Cp && y2.numel() == P * Cp);
+  TORCH_CHECK(stats.numel() == 4 * Cp && stats2.numel() == 4 * Cp && coef.numel() == 3 * Cp, "stats / coef rows");
+  TORCH_CHECK(part.numel() == bn_partial_blocks(P, Cp) * 2 * Cp, "part numel mismatch");
+  const float* st = f32(stats);
+  const float* st2 = f32(stats2);
+  bn_act_bwd_apply_part(bf(dz), bf(y), st, st + Cp, f32(coef), bf(dy), bf(y2), st2, st2 + Cp, st2 + 2 * Cp,
+                        relu2 ? 1 : 0, f32(part), P, Cp, relu ? 1 : 0, cur_stream());
+}
+
 void bn_act_bwd_apply_t(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& stats, const at::Tensor& coef,
                         const at::Tensor& dy, int64_t P, int64_t Cp, bool relu) {
   CHECK_BF16(dz); CHECK_BF16(y); CHECK_BF16(dy); CHECK_F32(stats); CHECK_F32(coef);
@@ -1145,6 +1159,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_finalize", &bn_bwd_finalize_t, py::arg("tmp"), py::arg("C"), py::arg("Cp"), py::arg("count"),
         py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("pscale") = 1.0);
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
+  m.def("bn_act_bwd_apply_part", &bn_act_bwd_apply_part_t);
   m.def("bn_tail_partial", &bn_tail_partial_t);
   m.def("bn_tail_apply", &bn_tail_apply_t);
   m.def("bn_tail_blocks", [](int64_t P, int64_t Cp) { return bn_tail_blocks(P, (int)Cp); });

@@ -435,6 +435,75 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const float* __
   if (threadIdx.x == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The apply pass of a BN whose input y is a SUM with a second (deferred) BN's output among its summands -- the
+// ResidualBlock's bn(upper + relu(bn2(y2))) -- also emits bn2's backward partials: dy (this pass's stored, bf16
+// output) IS bn2's incoming gradient, so (sum g2, sum g2 * (y2 - mean2)), g2 = dy * relu2'(y2), come from one more
+// read of y2 instead of bn2's own partial pass over (dy, y2).  Grid and partial rows as bn_act_bwd_partial.
+__global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_part_kernel(
+    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ coef, uint16_t* __restrict__ dy,
+    const uint16_t* __restrict__ y2, const float* __restrict__ scale2, const float* __restrict__ shift2,
+    const float* __restrict__ mean2, int relu2, float* __restrict__ part, long P, int Cp, int relu) {
+  __shared__ float red[2][kBlock][8];
+  const int CG = Cp >> 3;
+  const int R = kBlock / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, r = tid / CG, c0 = 8 * cg;
+  float s[8], q[8], a[8], b[8], k1[8], k2[8], k3[8], a2[8], b2[8], mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  load8f(scale + c0, a); load8f(shift + c0, b);
+  load8f(coef + c0, k1); load8f(coef + Cp + c0, k2); load8f(coef + 2 * Cp + c0, k3);
+  load8f(scale2 + c0, a2); load8f(shift2 + c0, b2); load8f(mean2 + c0, mu);
+  if (!relu)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = INFINITY;
+  if (r < R) {
+    const long stride = (long)gridDim.x * R;
+    for (long p = (long)blockIdx.x * R + r; p < P; p += kPartUnroll * stride) {
+      uint4 gin[kPartUnroll], yin[kPartUnroll], zin[kPartUnroll];
+#pragma unroll
+      for (int u = 0; u < kPartUnroll; ++u) {
+        const long qq = p + u * stride;
+        const bool ok = qq < P;
+        gin[u] = ok ? *reinterpret_cast<const uint4*>(dz + qq * Cp + c0) : make_uint4(0, 0, 0, 0);
+        yin[u] = ok ? *reinterpret_cast<const uint4*>(y + qq * Cp + c0) : make_uint4(0, 0, 0, 0);
+        zin[u] = ok ? *reinterpret_cast<const uint4*>(y2 + qq * Cp + c0) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kPartUnroll; ++u) {
+        const long qq = p + u * stride;
+        if (qq >= P) break;
+        float g[8], v[8], w[8];
+        unpack8(gin[u], g);
+        unpack8(yin[u], v);
+        unpack8(zin[u], w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = bwd1(g[e], v[e], a[e], b[e], k1[e], k2[e], k3[e]);
+        const uint4 o = pack8(g);
+        *reinterpret_cast<uint4*>(dy + qq * Cp + c0) = o;
+        unpack8(o, g);   // bn2 sees the stored (bf16) gradient, as its own partial pass would
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gr = (!relu2 || fmaf(w[e], a2[e], b2[e]) > 0.f) ? g[e] : 0.f;
+          s[e] += gr;
+          q[e] += gr * (w[e] - mu[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+  __syncthreads();
+  for (int c = tid; c < Cp; c += kBlock) {
+    const int g = c >> 3, e = c & 7;
+    float ss = 0.f, qq = 0.f;
+    for (int rr = 0; rr < R; ++rr) { ss += red[0][rr * CG + g][e]; qq += red[1][rr * CG + g][e]; }
+    part[((long)blockIdx.x * 2 + 0) * Cp + c] = ss;
+    part[((long)blockIdx.x * 2 + 1) * Cp + c] = qq;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void bn_act_bwd_apply_kernel(
     const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ coef, uint16_t* __restrict__ dy, long P,
@@ -772,6 +841,14 @@ void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, 
     hipLaunchKernelGGL(bn_tail_apply_kernel<3>, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
   else
     hipLaunchKernelGGL(bn_tail_apply_kernel<kTailMax>, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);
+}
+
+void bn_act_bwd_apply_part(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                           const float* coef, uint16_t* dy, const uint16_t* y2, const float* scale2,
+                           const float* shift2, const float* mean2, int relu2, float* part, long P, int Cp, int relu,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(bn_act_bwd_apply_part_kernel, dim3(bn_partial_blocks(P, Cp)), dim3(kBlock), 0, s, dz, y, scale,
+                     shift, coef, dy, y2, scale2, shift2, mean2, relu2, part, P, Cp, relu);
 }
 
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,

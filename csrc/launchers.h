@@ -170,6 +170,12 @@ void bn_bwd_finalize(const double* tmp, int S, int C, int Cp, float count, const
                      float* coef, float pscale, hipStream_t s);
 void bn_act_bwd_apply(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
                       const float* coef, uint16_t* dy, long P, int Cp, int relu, hipStream_t s);
+// + the backward partials of a second BN (scale2 / shift2 / mean2, input y2) whose output is a summand of y: dy is
+// that BN's incoming gradient (bn_act_bwd_partial's rows and grid, part [bn_partial_blocks][2][Cp])
+void bn_act_bwd_apply_part(const uint16_t* dz, const uint16_t* y, const float* scale, const float* shift,
+                           const float* coef, uint16_t* dy, const uint16_t* y2, const float* scale2,
+                           const float* shift2, const float* mean2, int relu2, float* part, long P, int Cp, int relu,
+                           hipStream_t s);
 
 // elementwise.hip
 void nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t s);

@@ -57,11 +57,12 @@ class Deferred:
     consumer kernel applies the affine+ReLU while it loads ``t`` (the "BN prologue": conv halo/igemm
     staging, weight-gradient staging, branch sums), so no ``bn_act_apply`` pass ever writes ``z``.
     :func:`materialize` turns it into a plain tensor for consumers without a prologue."""
-    __slots__ = ('t', 'stats', 'relu', 'z')
+    __slots__ = ('t', 'stats', 'relu', 'z', 'bh')
 
-    def __init__(self, t, stats, relu):
+    def __init__(self, t, stats, relu, bh=None):
         self.t, self.stats, self.relu = t, stats, relu
         self.z = None   # materialised copy, made at most once (shared by every consumer that needs it)
+        self.bh = bh    # BwdStatsHandle of this BN when a summing BN may emit its backward partials (bn_act partner)
 
     @property
     def shape(self):
@@ -418,6 +419,9 @@ class _BNAct(torch.autograd.Function):
         ctx.st, ctx.relu, ctx.k, ctx.count, ctx.training = st, relu, len(xs), count, training
         ctx.defer_bwd = defer_bwd
         ctx.defer_dy = bool(mode[2]) if len(mode) > 2 else False
+        # partner: the handle of a deferred BN whose output is one of this BN's summands -- this BN's dy is that
+        # BN's incoming gradient, so the apply pass below emits its backward partials too (bn_act_bwd_apply_part)
+        ctx.partner = mode[3] if len(mode) > 3 and training else None
         ctx.handle = handle if training else None
         if ctx.handle is not None:
             handle.y, handle.stats, handle.relu, handle.part = y, stats, relu, None
@@ -474,6 +478,7 @@ class _BNAct(torch.autograd.Function):
                 if hook is not None:
                     hook([t for t in (st.weight, st.bias) if t is not None])
             _BWD.add(sums, st.group, job, dy.data_ptr())
+            ctx.partner = None   # (parked: the partner BN runs its own partial pass)
             if h is not None:
                 h.y = h.stats = h.part = None
                 ctx.handle = None
@@ -501,7 +506,14 @@ class _BNAct(torch.autograd.Function):
             dy = _register_deferred(dz, y, stats, coef, ctx.relu, ctx.k)
         elif need_dy:
             dy = torch.empty_like(y)
-            C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+            pt = ctx.partner
+            if pt is not None and pt.y is not None and pt.part is None and pt.y.shape == y.shape:
+                part2 = torch.empty(C.bn_partial_blocks(P, Cp), 2, Cp, dtype=torch.float32, device=dev)
+                C.bn_act_bwd_apply_part(dz, y, stats, coef, dy, pt.y, pt.stats, bool(pt.relu), part2, P, Cp, ctx.relu)
+                pt.part = part2
+            else:
+                C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+        ctx.partner = None
         if h is not None:   # break the output -> node -> ctx -> handle -> output cycle now
             h.y = h.stats = h.part = None
             ctx.handle = None
@@ -532,13 +544,14 @@ def _check_deferrable(ts):
 
 
 def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=None, deferred=False,
-           defer_bwd=False):
+           defer_bwd=False, partner=None, bh=None):
     """act(BN(sum(xs))) for NHWC bf16 feature maps (``xs``: tensors and/or :class:`Deferred` BN
     outputs).  ``part_info = (part, width, col_off)`` reuses conv-epilogue channel partials (single
     plain input only); ``handle``: see :class:`BwdStatsHandle`.  ``deferred=True`` returns a
     :class:`Deferred` (no normalise pass) -- only for callers whose consumers all take prologues.
     ``defer_bwd=True``: every input is read by this BN only (SyncBN backward exchange may be parked,
-    see :class:`_Pending`)."""
+    see :class:`_Pending`).  ``partner``: the :class:`BwdStatsHandle` of a Deferred input's BN (its backward partials
+    come from this BN's apply pass); ``bh``: this BN's own such handle (kept on the returned Deferred)."""
     if isinstance(xs, (torch.Tensor, Deferred)):
         xs = [xs]
     ts, coefs, mask = split_inputs(xs)
@@ -546,9 +559,12 @@ def bn_act(xs, st: BNState, relu=True, training=True, part_info=None, handle=Non
         _check_deferrable(ts)
     # the data-gradient stays deferred (DeferredGrad) when every input is a conv output read by this BN only
     defer_dy = DEFER_DY and defer_bwd and training and not coefs and _dy_deferrable(ts)
-    out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd, defer_dy), (coefs, mask),
-                              st.weight, st.bias, *ts)
-    return Deferred(out, stats, relu) if deferred else out
+    if bh is not None:
+        assert handle is None, 'one backward-partials handle per BN'
+        handle = bh
+    out, stats = _BNAct.apply(st, relu, training, part_info, handle, (deferred, defer_bwd, defer_dy, partner),
+                              (coefs, mask), st.weight, st.bias, *ts)
+    return Deferred(out, stats, relu, bh) if deferred else out
 
 
 # ------------------------------------------------------------------------------------------------

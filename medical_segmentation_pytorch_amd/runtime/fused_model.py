@@ -46,6 +46,9 @@ _MULTI = os.environ.get('MSP_DUCK_MULTI', '1') != '0'
 _AUG_INBN = True
 # DUCKNet skips: the decoder's share of dL/dskip is parked for the downsample conv (ops.elementwise.up2_add)
 _PARK_SKIP = True
+# ResidualBlock bn(upper + lower): its backward apply pass also emits the lower BN's backward partials (no partial
+# pass of its own; bitwise the same gradients).  A module constant the GPU test toggles.
+_RES_PARTNER = True
 # env MSP_LOCKSTEP=1/0 forces level-synchronous branch order on/off (default: on under multi-rank SyncBN)
 _LOCKSTEP = {'1': True, '0': False}.get(os.environ.get('MSP_LOCKSTEP', ''))
 # env MSP_FUSED_DECODERS=0 keeps every non-Unet smp decoder on the hybrid (eager decoder) path (A/B)
@@ -207,11 +210,15 @@ class FusedExecutor(SmpDecoders):
         return p
 
     # -- single-consumer BN outputs ------------------------------------------------------------------
-    def _bn_out(self, xs, st, relu, training, part_info=None, single=False):
-        """Deferred bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv."""
+    def _bn_out(self, xs, st, relu, training, part_info=None, single=False, bh=False, partner=None):
+        """Deferred bn_act; ``single``: the caller guarantees the output feeds exactly one stride-1 conv.
+        ``bh``: the output is a summand of exactly one summing BN, which gets its handle as ``partner`` (that BN's
+        apply pass emits this BN's backward partials: ops.bn.bn_act)."""
         h = BwdStatsHandle() if (single and training and _BN_EPILOGUE) else None
+        own = BwdStatsHandle() if (bh and h is None and training and _BN_EPILOGUE and _DEFER_BN) else None
         # every caller's inputs are conv outputs / BN outputs read by this BN only -> defer_bwd
-        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=_DEFER_BN, defer_bwd=True)
+        z = bn_act(xs, st, relu, training, part_info, handle=h, deferred=_DEFER_BN, defer_bwd=True,
+                   partner=partner if training else None, bh=own)
         key = z.t if isinstance(z, Deferred) else z
         if h is not None:
             self._handles[id(key)] = (key, h)
@@ -246,8 +253,8 @@ class FusedExecutor(SmpDecoders):
     # the level's statistic exchanges together (ops.bn._Pending: ONE collective per level instead of one
     # per BN); and since autograd runs ready nodes in reverse creation order, the backward reaches every
     # BN of a level before any conv of it, which batches the backward exchanges the same way.
-    def _g_cba(self, m, x, training, single=False, raw=False):
-        """``raw``: return the BN as a :class:`BNSpec` (applied later by the DUCK tail)."""
+    def _g_cba(self, m, x, training, single=False, raw=False, bh=False):
+        """``raw``: return the BN as a :class:`BNSpec` (applied later by the DUCK tail); ``bh``: see _bn_out."""
         xs = x if isinstance(x, (list, tuple)) else [x]
         plan = self.plan_conv(m[0], gi=len(xs))
         (y,), part = self._conv(plan, xs, training)
@@ -256,7 +263,7 @@ class FusedExecutor(SmpDecoders):
             z = BNSpec([y], self.bn(m[1]), _is_relu(m[2]), (part, plan.rows, 0))
         else:
             z = self._bn_out([y], self.bn(m[1]), _is_relu(m[2]), training,
-                             (part, plan.rows, 0) if training else None, single)
+                             (part, plan.rows, 0) if training else None, single, bh=bh)
         yield
         return z
 
@@ -270,11 +277,13 @@ class FusedExecutor(SmpDecoders):
     def _g_residual_tail(self, m, upper_y, low_fn, training, single_out=False, raw=False):
         """ResidualBlock whose fused 3x3+1x1 launch already ran: (low BN) -> cba -> bn(upper + lower)."""
         low = yield from self._g_bn(low_fn)
-        low = yield from self._g_cba(m.lower_branch[1], low, training)
+        # (not raw: the block's bn(upper + lower) backward emits the lower BN's backward partials in its apply pass)
+        low = yield from self._g_cba(m.lower_branch[1], low, training, bh=_RES_PARTNER and not raw)
         if raw:
             return (yield from self._g_bn(lambda: BNSpec([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]))))
+        partner = low.bh if isinstance(low, Deferred) else None
         return (yield from self._g_bn(lambda: self._bn_out([upper_y, low], self.bn(m.bn[0]), _is_relu(m.bn[1]),
-                                                            training, single=single_out)))
+                                                            training, single=single_out, partner=partner)))
 
     def _g_residual(self, m, x, training, single_out=False, raw=False):
         plan = self.plan_fused3x3(('res', id(m)), [m.lower_branch[0][0]], [m.upper_branch])

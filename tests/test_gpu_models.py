@@ -307,6 +307,32 @@ def test_first_duck_in_bn_shortcut(gpu, monkeypatch):
             assert torch.equal(a, b), n
 
 
+def test_residual_partner_partials_bitwise(gpu, monkeypatch):
+    """ResidualBlock bn(upper + relu(bn2(y2))): the sum BN's backward apply pass emits bn2's backward partials
+    (ops.bn.bn_act partner, csrc/bn.hip bn_act_bwd_apply_part) instead of bn2's own partial pass over (dy, y2): the
+    same dy bitwise and the same per-block partial rows up to fp32 rounding (1e-8 relative, tools/dev/
+    apply_part_probe.py) -- every gradient within fp32 rounding amplified through the step, the forward buffers equal."""
+    from medical_segmentation_pytorch_amd.runtime import fused_model
+    from medical_segmentation_pytorch_amd.runtime.bench_step import synthetic_batch
+    from medical_segmentation_pytorch_amd.runtime.trainer_engine import FusedStep
+    torch.manual_seed(0)
+    base = DuckNet(2, 3, 17).to(gpu).train()
+    x, t = synthetic_batch(2, 96, gpu)
+    res = {}
+    for on in (False, True):
+        monkeypatch.setattr(fused_model, '_RES_PARTNER', on)
+        s = FusedStep(copy.deepcopy(base), x.clone(), t.clone(), lr=1e-3, use_graph=False, total_steps=10)
+        s()
+        torch.cuda.synchronize()
+        res[on] = ({n: p.grad.detach().clone() for n, p in s.model.named_parameters()},
+                   [b.detach().clone() for b in s.model.buffers()])
+    for n, a in res[False][0].items():
+        b = res[True][0][n]
+        assert ((a.float() - b.float()).norm() / a.float().norm().clamp_min(1e-12)).item() < 1e-3, n
+    for a, b in zip(res[False][1], res[True][1]):
+        assert torch.equal(a, b)
+
+
 def test_ducknet_skip_grad_parked(gpu, monkeypatch):
     """DUCKNet skips (ops.elementwise.up2_add(park_skip=True)): the decoder's share of dL/dskip is added by
     the encoder's downsample conv in its data-gradient epilogue (strided phases included) instead of an
