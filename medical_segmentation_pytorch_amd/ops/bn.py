@@ -359,6 +359,18 @@ def _channel_sums(C, part, nblk, width, col_off, Cp, group, dev, reduce=True):
     return tmp
 
 
+def _apply_dy(C, dz, y, stats, coef, dy, P, Cp, relu, pt):
+    """dy = the BN backward apply pass; with a partner (the handle of a deferred BN whose output is a summand of
+    this BN's input) the same pass emits that BN's backward partials into ``pt.part`` -- on every rank count alike
+    (a parked SyncBN apply included), so single- and multi-rank steps take the same arithmetic."""
+    if pt is not None and pt.y is not None and pt.part is None and pt.y.shape == y.shape:
+        part2 = torch.empty(C.bn_partial_blocks(P, Cp), 2, Cp, dtype=torch.float32, device=y.device)
+        C.bn_act_bwd_apply_part(dz, y, stats, coef, dy, pt.y, pt.stats, bool(pt.relu), part2, P, Cp, relu)
+        pt.part = part2
+    else:
+        C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, relu)
+
+
 class _BNAct(torch.autograd.Function):
     # inputs: st, relu, training, part_info, handle, deferred, pro, gamma, beta, *xs  (gamma/beta are
     # inputs so that their grads reach autograd when the engine gives no grad sink).  pro = (coefs,
@@ -471,14 +483,16 @@ class _BNAct(torch.autograd.Function):
             relu, count, hook = ctx.relu, ctx.count, st.ready_hook
             dy = _register_deferred(dz, y, stats, coef, relu, ctx.k) if defer_dy else torch.empty_like(y)
 
+            pt = ctx.partner
+
             def job(sums, st=st, Cp=Cp, P=P):
                 C.bn_bwd_finalize(sums, st.C, Cp, count, stats, g_t, b_t, coef, 1.0 / world)
                 if not defer_dy:
-                    C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, relu)
+                    _apply_dy(C, dz, y, stats, coef, dy, P, Cp, relu, pt)
                 if hook is not None:
                     hook([t for t in (st.weight, st.bias) if t is not None])
             _BWD.add(sums, st.group, job, dy.data_ptr())
-            ctx.partner = None   # (parked: the partner BN runs its own partial pass)
+            ctx.partner = None
             if h is not None:
                 h.y = h.stats = h.part = None
                 ctx.handle = None
@@ -506,13 +520,7 @@ class _BNAct(torch.autograd.Function):
             dy = _register_deferred(dz, y, stats, coef, ctx.relu, ctx.k)
         elif need_dy:
             dy = torch.empty_like(y)
-            pt = ctx.partner
-            if pt is not None and pt.y is not None and pt.part is None and pt.y.shape == y.shape:
-                part2 = torch.empty(C.bn_partial_blocks(P, Cp), 2, Cp, dtype=torch.float32, device=dev)
-                C.bn_act_bwd_apply_part(dz, y, stats, coef, dy, pt.y, pt.stats, bool(pt.relu), part2, P, Cp, ctx.relu)
-                pt.part = part2
-            else:
-                C.bn_act_bwd_apply(dz, y, stats, coef, dy, P, Cp, ctx.relu)
+            _apply_dy(C, dz, y, stats, coef, dy, P, Cp, ctx.relu, ctx.partner)
         ctx.partner = None
         if h is not None:   # break the output -> node -> ctx -> handle -> output cycle now
             h.y = h.stats = h.part = None
