@@ -570,14 +570,15 @@ class _MultiConvFn(torch.autograd.Function):
     ``runtime.fused_model.duck_split``) as one autograd node: the backward writes the input gradient
     once -- the first plan's data-gradient stores it, every later plan's ACCUMULATES in its epilogue
     (``conv_fwd(accumulate=True)``: bitwise a separate bf16 add, minus its three tensor passes) --
-    then runs each plan's weight gradient.  Stride-1, single input group, no bias."""
+    then runs each plan's weight gradient.  Narrow plans (the 'P' split: singles and 3x3 + 1x1 pairs) take
+    the fused data+weight-gradient kernel instead, its accumulate epilogue adding into the same tensor
+    (:func:`_fused_bwd`).  Stride-1, single input group, no bias."""
 
     @staticmethod
-    def forward(ctx, plans, want_stats, pro, aug, x, *weights):
+    def forward(ctx, plans, want_stats, pro, mode, x, *weights):
         C = require()
         ctx.set_materialize_grads(False)
-        ctx.aug, aug = aug if isinstance(aug, tuple) else (aug, True)   # (InBnAug | None, fused backward allowed)
-        ctx.fused_ok = aug
+        ctx.aug, ctx.fused_ok = mode   # (InBnAug | None, narrow plans may take the fused data+weight-gradient kernel)
         x = x.contiguous()
         coefs, rmask = pro
         n, ih, iw, _ = x.shape
