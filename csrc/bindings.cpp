@@ -403,19 +403,30 @@ void bn_tail_partial_t(const at::Tensor& dz, const at::Tensor& ys, const at::Ten
 
 void bn_tail_apply_t(const at::Tensor& dz, const at::Tensor& ys, const at::Tensor& ostats, const at::Tensor& ocoef,
                      bool orelu, std::vector<at::Tensor> y, std::vector<at::Tensor> st, std::vector<at::Tensor> coef,
-                     int64_t relu_mask, std::vector<at::Tensor> dy, int64_t P, int64_t Cp) {
+                     int64_t relu_mask, std::vector<at::Tensor> dy, int64_t P, int64_t Cp,
+                     const c10::optional<at::Tensor>& g) {
   tail_check(dz, ys, ostats, ocoef, y, st, P, Cp);
   TORCH_CHECK(coef.size() == y.size() && dy.size() == y.size(), "coef / dy per branch");
   std::vector<const uint16_t*> yp;
   std::vector<const float*> sp, cp;
   std::vector<uint16_t*> dp;
+  bool deferred = false;
   for (size_t i = 0; i < y.size(); ++i) {
     CHECK_F32(coef[i]); CHECK_BF16(dy[i]);
-    TORCH_CHECK(coef[i].numel() == 3 * Cp && dy[i].numel() == P * Cp, "coef / dy size mismatch");
-    yp.push_back(bf(y[i])); sp.push_back(f32(st[i])); cp.push_back(f32(coef[i])); dp.push_back(bf(dy[i]));
+    // an empty dy: the branch's data-gradient is deferred (rebuilt from g by its producer)
+    TORCH_CHECK(coef[i].numel() == 3 * Cp && (dy[i].numel() == P * Cp || dy[i].numel() == 0), "coef / dy size mismatch");
+    deferred |= dy[i].numel() == 0;
+    yp.push_back(bf(y[i])); sp.push_back(f32(st[i])); cp.push_back(f32(coef[i]));
+    dp.push_back(dy[i].numel() == 0 ? nullptr : bf(dy[i]));
   }
+  uint16_t* gp = nullptr;
+  if (g.has_value() && g->defined()) {
+    CHECK_BF16(*g); TORCH_CHECK(g->numel() == P * Cp, "g numel");
+    gp = bf(*g);
+  }
+  TORCH_CHECK(!deferred || gp != nullptr, "deferred branches need g");
   bn_tail_apply(bf(dz), bf(ys), f32(ostats), f32(ocoef), orelu ? 1 : 0, (int)y.size(), yp.data(), sp.data(), cp.data(),
-                (unsigned)relu_mask, dp.data(), P, Cp, cur_stream());
+                (unsigned)relu_mask, dp.data(), P, Cp, cur_stream(), gp);
 }
 
 void nchw_to_nhwc_t(const at::Tensor& x, const at::Tensor& y, int64_t Cp) {
@@ -1161,7 +1172,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply_t);
   m.def("bn_act_bwd_apply_part", &bn_act_bwd_apply_part_t);
   m.def("bn_tail_partial", &bn_tail_partial_t);
-  m.def("bn_tail_apply", &bn_tail_apply_t);
+  m.def("bn_tail_apply", &bn_tail_apply_t, py::arg("dz"), py::arg("ys"), py::arg("ostats"), py::arg("ocoef"),
+        py::arg("orelu"), py::arg("y"), py::arg("st"), py::arg("coef"), py::arg("relu_mask"), py::arg("dy"),
+        py::arg("P"), py::arg("Cp"), py::arg("g") = py::none());
   m.def("bn_tail_blocks", [](int64_t P, int64_t Cp) { return bn_tail_blocks(P, (int)Cp); });
   m.attr("kTailMax") = kTailMax;
   m.attr("kTailMaxCp") = kTailMaxCp;

@@ -562,7 +562,8 @@ struct TailArgs {
   const float* st[kTailMax];              // their stats [4][Cp] (scale, shift, mean, invstd)
   const float* coef[kTailMax];            // their backward coef [3][Cp] (apply pass)
   unsigned relu;                          // bit i: branch i has a ReLU
-  uint16_t* dy[kTailMax];                 // branch data-gradients (apply pass)
+  uint16_t* dy[kTailMax];                 // branch data-gradients (apply pass; nullptr: deferred to the producer)
+  uint16_t* g;                            // nullable: out_bn's data-gradient (bf16), for the deferred branches
 };
 
 // 8 consecutive floats from LDS as two 16-B reads (the caller guarantees 32-B alignment)
@@ -678,9 +679,14 @@ __global__ __launch_bounds__(kBlock) void bn_tail_apply_kernel(TailArgs t, long 
     tail_dys(ok1 ? *reinterpret_cast<const uint4*>(t.dz + off1) : make_uint4(0, 0, 0, 0),
              ok1 ? *reinterpret_cast<const uint4*>(t.ys + off1) : make_uint4(0, 0, 0, 0), a, sh, k1, k2, k3,
              t.orelu != 0, d1);
+    if (t.g != nullptr) {   // (uniform) the deferred branches' dz: their producers rebuild dy from (g, y_i)
+      *reinterpret_cast<uint4*>(t.g + off0) = pack8(d0);
+      if (ok1) *reinterpret_cast<uint4*>(t.g + off1) = pack8(d1);
+    }
 #pragma unroll
     for (int i = 0; i < KM; ++i) {
       if (i >= t.k) break;
+      if (t.dy[i] == nullptr) continue;   // (uniform) deferred branch
       const uint4 y0 = *reinterpret_cast<const uint4*>(t.y[i] + off0);
       const uint4 y1 = ok1 ? *reinterpret_cast<const uint4*>(t.y[i] + off1) : make_uint4(0, 0, 0, 0);
       const float* cf = tsm + i * 5 * Cp + c0;
@@ -834,8 +840,9 @@ void bn_tail_partial(const uint16_t* dz, const uint16_t* ys, const float* ostats
 
 void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
                    const uint16_t* const* y, const float* const* st, const float* const* coef, unsigned relu,
-                   uint16_t* const* dy, long P, int Cp, hipStream_t s) {
-  const TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, coef, relu, dy, Cp);
+                   uint16_t* const* dy, long P, int Cp, hipStream_t s, uint16_t* g) {
+  TailArgs t = tail_args(dz, ys, ostats, ocoef, orelu, k, y, st, coef, relu, dy, Cp);
+  t.g = g;
   const size_t lds = (size_t)k * 5 * Cp * sizeof(float);
   if (k <= 3)
     hipLaunchKernelGGL(bn_tail_apply_kernel<3>, dim3(grid_rows(P, Cp / 8)), dim3(kBlock), lds, s, t, P, Cp);

@@ -136,7 +136,9 @@ void bn_tail_partial(const uint16_t* dz, const uint16_t* ys, const float* ostats
                      hipStream_t s);
 void bn_tail_apply(const uint16_t* dz, const uint16_t* ys, const float* ostats, const float* ocoef, int orelu, int k,
                    const uint16_t* const* y, const float* const* st, const float* const* coef, unsigned relu,
-                   uint16_t* const* dy, long P, int Cp, hipStream_t s);
+                   uint16_t* const* dy, long P, int Cp, hipStream_t s, uint16_t* g = nullptr);
+// (dy[i] nullptr: branch i's data-gradient is deferred to its producer, which rebuilds it from g = out_bn's
+// data-gradient, written when g != nullptr)
 // coefs[i] (nullable array / entries): deferred-BN prologue of input i (stats rows, ld = Cp), bit i of
 // relu_mask its ReLU -- the branch sums that feed a BN read the branches' pre-BN tensors directly.
 void sum_stats(const uint16_t* const* inputs, const float* const* coefs, unsigned relu_mask, int k, uint16_t* out,

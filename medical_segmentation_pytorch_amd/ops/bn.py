@@ -700,6 +700,12 @@ class _DuckTail(torch.autograd.Function):
                 st.num_batches_tracked.add_(1)
         ctx.specs, ctx.out_st, ctx.out_relu, ctx.nx, ctx.k, ctx.count = specs, out_st, out_relu, nx, k, count
         ctx.relu_mask = relu_mask
+        # branches whose BN input is one conv output read by this BN only (no prologue): their data-gradient can
+        # stay deferred -- the producing conv rebuilds it from out_bn's data-gradient g (see backward)
+        ctx.defer_ok, o = [], 0
+        for n, (cs, _) in zip(nx, pros):
+            ctx.defer_ok.append(DEFER_DY and n == 1 and not cs and _dy_deferrable(flat[o:o + n]))
+            o += n
         ctx.save_for_backward(y_sum, o_stats, *ys, *stats)
         ctx.mark_non_differentiable(o_stats)
         return y_sum, o_stats
@@ -764,9 +770,17 @@ class _DuckTail(torch.autograd.Function):
             C.bn_tail_partial(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys[b0:b1], stats[b0:b1],
                               ctx.relu_mask >> b0, tpart[b0:b1], P, Cp)
         coefs = finalize([(tpart[i], tb) for i in range(k)], list(range(k)))
-        dys = [torch.empty_like(y_sum) for _ in range(k)]
+        # Narrow blocks (<= 48 channels: every branch-last conv runs the fused backward, which rebuilds dY while
+        # staging): the branches that allow it get a deferred data-gradient over g = out_bn's data-gradient (written
+        # once by this pass) instead of their own dy -- per such branch the pass skips a y_i read and a dy_i write and
+        # the consumer reads (g, y_i) instead of dy_i.
+        defer = [i for i in range(k) if ctx.defer_ok[i]] if Cp <= 48 else []
+        g = torch.empty_like(y_sum) if defer else None
+        dys = [y_sum.new_empty(0) if i in defer else torch.empty_like(y_sum) for i in range(k)]
         # the apply pass as ONE k-branch launch (3-branch launches measured no faster, round 5)
-        C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, coefs, ctx.relu_mask, dys, P, Cp)
+        C.bn_tail_apply(dz, y_sum, o_stats, o_coef, ctx.out_relu, ys, stats, coefs, ctx.relu_mask, dys, P, Cp, g=g)
+        for i in defer:
+            dys[i] = _register_deferred(g, ys[i], stats[i], coefs[i], bool((ctx.relu_mask >> i) & 1), ctx.nx[i])
         for st in sts:
             if st.ready_hook is not None:
                 st.ready_hook([t for t in (st.weight, st.bias) if t is not None])

@@ -352,8 +352,9 @@ def test_ducknet_skip_grad_parked(gpu, monkeypatch):
         res[on] = {n: p.grad.detach().float().clone() for n, p in s.model.named_parameters()}
     assert losses[True] == losses[False]
     # a lost or doubled skip gradient moves every encoder parameter's gradient by O(1); one rounding fewer
-    # per skip moves them by bf16 noise, largest where the backward ends (the first DUCK's in_bn)
+    # per skip moves them by bf16 noise, largest where the backward ends (the first DUCK's in_bn: 0.061 on the
+    # round-6 final tree, whose DUCK tail hands three branches a bf16 out_bn gradient -- 0.1 still sits far below O(1))
     rel = {n: ((a - res[True][n]).norm() / a.norm().clamp_min(1e-12)).item() for n, a in res[False].items()}
     worst = sorted(rel.items(), key=lambda kv: -kv[1])[:5]
-    assert worst[0][1] < 6e-2, worst
+    assert worst[0][1] < 0.1, worst
     assert sorted(rel.values())[len(rel) // 2] < 5e-3, worst
